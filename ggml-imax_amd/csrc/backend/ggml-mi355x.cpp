@@ -1,0 +1,766 @@
+// ggml-mi355x.cpp -- the MI355X (gfx950) ggml backend: buffer types, buffers, backend vtable
+// and per-node dispatch into the hand-written HIP kernels of csrc/kernels/.
+//
+// Implements ggml_backend_buffer_type_i / ggml_backend_buffer_i / ggml_backend_i
+// (src/ggml-backend-impl.h:18-117 of NAIST-Archlab/ggml-imax @ v2) the way the reference's
+// device backends do (structural analogue: src/ggml-cuda.cu:366-576 buffers, :2156-2308
+// dispatch, :2456-2713 graph_compute, :2715-2868 supports/offload, :2870-2942 events/vtable,
+// :3024-3042 registration) -- but written for one process per GPU, HIP streams, wave64
+// kernels and activation quantization on the device.
+//
+// This file only uses the generic ggml API (ggml_nbytes, ggml_backend_buffer_init, ...), so the
+// same object loads into either the repo's runtime (csrc/core) or the reference libggml.
+
+#include "ggml_abi.h"
+#include "ggml-mi355x.h"
+#include "../kernels/mi355x_kernels.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#define MI_CHECK(call)                                                                                  \
+    do {                                                                                                \
+        const hipError_t err_ = (call);                                                                 \
+        if (err_ != hipSuccess) {                                                                       \
+            fprintf(stderr, "ggml-mi355x: %s failed at %s:%d: %s\n", #call, __FILE__, __LINE__,       \
+                    hipGetErrorString(err_));                                                           \
+            abort();                                                                                    \
+        }                                                                                               \
+    } while (0)
+
+#define MI_ASSERT(x)                                                                                    \
+    do {                                                                                                \
+        if (!(x)) {                                                                                     \
+            fflush(stdout);                                                                             \
+            fprintf(stderr, "ggml-mi355x: assertion failed at %s:%d: %s\n", __FILE__, __LINE__, #x);  \
+            abort();                                                                                    \
+        }                                                                                               \
+    } while (0)
+
+static constexpr size_t kBufferAlign = 256;   // tensor alignment inside device buffers
+static constexpr size_t kBufferSlack = 256;   // tail slack: kernels may over-read < 16 B past a row
+
+// ---------------------------------------------------------------------------------------------
+// devices
+// ---------------------------------------------------------------------------------------------
+
+static int device_count() {
+    static int count = [] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        return std::min(n, GGML_MI355X_MAX_DEVICES);
+    }();
+    return count;
+}
+
+struct mi_device_guard {
+    int prev = -1;
+    explicit mi_device_guard(int dev) {
+        MI_CHECK(hipGetDevice(&prev));
+        if (prev != dev) MI_CHECK(hipSetDevice(dev));
+    }
+    ~mi_device_guard() {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void) hipSetDevice(prev);
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// device buffer
+// ---------------------------------------------------------------------------------------------
+
+struct mi_buffer_ctx {
+    int device;
+    void * dev_ptr;
+    std::string name;
+};
+
+static const char * mi_buffer_get_name(ggml_backend_buffer_t buffer) {
+    return ((mi_buffer_ctx *) buffer->context)->name.c_str();
+}
+
+static bool buffer_is_mi355x(ggml_backend_buffer_t buffer) {
+    return buffer && buffer->iface.get_name == mi_buffer_get_name;
+}
+
+static void mi_buffer_free(ggml_backend_buffer_t buffer) {
+    auto * ctx = (mi_buffer_ctx *) buffer->context;
+    mi_device_guard g(ctx->device);
+    MI_CHECK(hipFree(ctx->dev_ptr));
+    delete ctx;
+}
+
+static void * mi_buffer_get_base(ggml_backend_buffer_t buffer) { return ((mi_buffer_ctx *) buffer->context)->dev_ptr; }
+
+static void mi_buffer_set_tensor(ggml_backend_buffer_t buffer, ggml_tensor * tensor, const void * data, size_t offset, size_t size) {
+    auto * ctx = (mi_buffer_ctx *) buffer->context;
+    mi_device_guard g(ctx->device);
+    // null stream: ordered after any queued work on the (blocking) backend streams
+    MI_CHECK(hipMemcpyAsync((char *) tensor->data + offset, data, size, hipMemcpyHostToDevice, nullptr));
+    MI_CHECK(hipStreamSynchronize(nullptr));
+}
+
+static void mi_buffer_get_tensor(ggml_backend_buffer_t buffer, const ggml_tensor * tensor, void * data, size_t offset, size_t size) {
+    auto * ctx = (mi_buffer_ctx *) buffer->context;
+    mi_device_guard g(ctx->device);
+    MI_CHECK(hipMemcpyAsync(data, (const char *) tensor->data + offset, size, hipMemcpyDeviceToHost, nullptr));
+    MI_CHECK(hipStreamSynchronize(nullptr));
+}
+
+static bool mi_buffer_cpy_tensor(ggml_backend_buffer_t buffer, const ggml_tensor * src, ggml_tensor * dst) {
+    ggml_backend_buffer_t src_buf = src->view_src ? src->view_src->buffer : src->buffer;
+    if (!buffer_is_mi355x(src_buf)) return false;
+    auto * sctx = (mi_buffer_ctx *) src_buf->context;
+    auto * dctx = (mi_buffer_ctx *) buffer->context;
+    mi_device_guard g(dctx->device);
+    if (sctx->device == dctx->device) {
+        MI_CHECK(hipMemcpyAsync(dst->data, src->data, ggml_nbytes(src), hipMemcpyDeviceToDevice, nullptr));
+    } else {
+        MI_CHECK(hipMemcpyPeerAsync(dst->data, dctx->device, src->data, sctx->device, ggml_nbytes(src), nullptr));
+    }
+    MI_CHECK(hipStreamSynchronize(nullptr));
+    return true;
+}
+
+static void mi_buffer_clear(ggml_backend_buffer_t buffer, uint8_t value) {
+    auto * ctx = (mi_buffer_ctx *) buffer->context;
+    mi_device_guard g(ctx->device);
+    MI_CHECK(hipMemset(ctx->dev_ptr, value, buffer->size));
+}
+
+static const ggml_backend_buffer_i k_mi_buffer_i = {
+    /* get_name    */ mi_buffer_get_name,
+    /* free_buffer */ mi_buffer_free,
+    /* get_base    */ mi_buffer_get_base,
+    /* init_tensor */ nullptr,
+    /* set_tensor  */ mi_buffer_set_tensor,
+    /* get_tensor  */ mi_buffer_get_tensor,
+    /* cpy_tensor  */ mi_buffer_cpy_tensor,
+    /* clear       */ mi_buffer_clear,
+    /* reset       */ nullptr,
+};
+
+// ---------------------------------------------------------------------------------------------
+// device buffer type (one static instance per device, ggml-cuda.cu:553-576)
+// ---------------------------------------------------------------------------------------------
+
+struct mi_buft_ctx {
+    int device;
+    std::string name;
+};
+
+static const char * mi_buft_get_name(ggml_backend_buffer_type_t buft) { return ((mi_buft_ctx *) buft->context)->name.c_str(); }
+
+static ggml_backend_buffer_t mi_buft_alloc_buffer(ggml_backend_buffer_type_t buft, size_t size) {
+    auto * bctx = (mi_buft_ctx *) buft->context;
+    mi_device_guard g(bctx->device);
+    size = std::max(size, (size_t) 1);
+    void * ptr = nullptr;
+    const hipError_t err = hipMalloc(&ptr, size + kBufferSlack);
+    if (err != hipSuccess) {
+        (void) hipGetLastError();
+        fprintf(stderr, "%s: allocating %.2f MiB on device %d: hipMalloc failed: %s\n", __func__,
+                size / 1024.0 / 1024.0, bctx->device, hipGetErrorString(err));
+        return nullptr;
+    }
+    auto * ctx = new mi_buffer_ctx{bctx->device, ptr, "MI355X" + std::to_string(bctx->device)};
+    return ggml_backend_buffer_init(buft, k_mi_buffer_i, ctx, size);
+}
+
+static size_t mi_buft_get_alignment(ggml_backend_buffer_type_t) { return kBufferAlign; }
+
+static size_t mi_buft_get_max_size(ggml_backend_buffer_type_t) { return SIZE_MAX; }
+
+static size_t mi_buft_get_alloc_size(ggml_backend_buffer_type_t, const ggml_tensor * tensor) { return ggml_nbytes(tensor); }
+
+static bool mi_buft_supports_backend(ggml_backend_buffer_type_t buft, ggml_backend_t backend);
+
+static const ggml_backend_buffer_type_i k_mi_buft_i = {
+    /* get_name         */ mi_buft_get_name,
+    /* alloc_buffer     */ mi_buft_alloc_buffer,
+    /* get_alignment    */ mi_buft_get_alignment,
+    /* get_max_size     */ mi_buft_get_max_size,
+    /* get_alloc_size   */ mi_buft_get_alloc_size,
+    /* supports_backend */ mi_buft_supports_backend,
+    /* is_host          */ nullptr,
+};
+
+// ---------------------------------------------------------------------------------------------
+// pinned host buffer type (ggml-cuda.cu:979-1050)
+// ---------------------------------------------------------------------------------------------
+
+static const char * mi_host_buffer_name(ggml_backend_buffer_t) { return "MI355X_Host"; }
+static void mi_host_buffer_free(ggml_backend_buffer_t b) { MI_CHECK(hipHostFree(b->context)); }
+static void * mi_host_buffer_base(ggml_backend_buffer_t b) { return b->context; }
+static void mi_host_buffer_set(ggml_backend_buffer_t, ggml_tensor * t, const void * d, size_t o, size_t n) { memcpy((char *) t->data + o, d, n); }
+static void mi_host_buffer_get(ggml_backend_buffer_t, const ggml_tensor * t, void * d, size_t o, size_t n) { memcpy(d, (const char *) t->data + o, n); }
+static void mi_host_buffer_clear(ggml_backend_buffer_t b, uint8_t v) { memset(b->context, v, b->size); }
+
+static const ggml_backend_buffer_i k_mi_host_buffer_i = {
+    mi_host_buffer_name, mi_host_buffer_free, mi_host_buffer_base, nullptr, mi_host_buffer_set, mi_host_buffer_get,
+    nullptr, mi_host_buffer_clear, nullptr,
+};
+
+static const char * mi_host_buft_name(ggml_backend_buffer_type_t) { return "MI355X_Host"; }
+
+static ggml_backend_buffer_t mi_host_buft_alloc(ggml_backend_buffer_type_t buft, size_t size) {
+    void * ptr = nullptr;
+    if (hipHostMalloc(&ptr, std::max(size, (size_t) 1), hipHostMallocPortable) != hipSuccess) {
+        (void) hipGetLastError();
+        // fall back to pageable host memory of the runtime's host buffer type
+        return ggml_backend_buft_alloc_buffer(ggml_backend_cpu_buffer_type(), size);
+    }
+    return ggml_backend_buffer_init(buft, k_mi_host_buffer_i, ptr, size);
+}
+
+static size_t mi_host_buft_align(ggml_backend_buffer_type_t) { return 64; }
+static bool mi_host_buft_supports(ggml_backend_buffer_type_t, ggml_backend_t backend) { return false; }
+static bool mi_host_buft_is_host(ggml_backend_buffer_type_t) { return true; }
+
+// ---------------------------------------------------------------------------------------------
+// backend context
+// ---------------------------------------------------------------------------------------------
+
+struct mi_act_cache_entry {
+    const void * data;   // src1 data
+    size_t nbytes;
+    int kind;            // 0 = q8_0, 1 = q8_K, 2 = f16
+    int64_t ne[4];
+    size_t nb[4];
+    void * dev;          // converted activations in scratch
+};
+
+struct mi_backend_ctx {
+    int device;
+    std::string name;
+    hipStream_t stream = nullptr;
+    void * scratch = nullptr;
+    size_t scratch_size = 0;
+    size_t scratch_used = 0;
+    std::vector<mi_act_cache_entry> act_cache;
+    bool graph_capture = true;
+    int last_launches = 0;
+};
+
+static ggml_guid_t mi_guid() {
+    static ggml_guid guid = {0x4d, 0x49, 0x33, 0x35, 0x35, 0x58, 0x2d, 0x67, 0x66, 0x78, 0x39, 0x35, 0x30, 0x2d, 0x76, 0x31};
+    return &guid;
+}
+
+static void * scratch_take(mi_backend_ctx * ctx, size_t bytes) {
+    bytes = (bytes + kBufferAlign - 1) & ~(kBufferAlign - 1);
+    MI_ASSERT(ctx->scratch_used + bytes <= ctx->scratch_size);
+    void * p = (char *) ctx->scratch + ctx->scratch_used;
+    ctx->scratch_used += bytes;
+    return p;
+}
+
+static void scratch_reserve(mi_backend_ctx * ctx, size_t bytes) {
+    if (bytes <= ctx->scratch_size) return;
+    MI_CHECK(hipStreamSynchronize(ctx->stream));
+    if (ctx->scratch) MI_CHECK(hipFree(ctx->scratch));
+    const size_t want = std::max(bytes + bytes / 2, (size_t) 16 << 20);
+    MI_CHECK(hipMalloc(&ctx->scratch, want));
+    ctx->scratch_size = want;
+}
+
+// ---------------------------------------------------------------------------------------------
+// op support (ggml-cuda.cu:2715-2859 analogue; the scheduler does not consult it, the
+// conformance harness does)
+// ---------------------------------------------------------------------------------------------
+
+static bool mm_src0_supported(ggml_type t) {
+    return t == GGML_TYPE_Q4_0 || t == GGML_TYPE_Q8_0 || t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K ||
+           t == GGML_TYPE_F16 || t == GGML_TYPE_F32;
+}
+
+static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
+    switch (op->op) {
+        case GGML_OP_NONE:
+        case GGML_OP_RESHAPE:
+        case GGML_OP_VIEW:
+        case GGML_OP_PERMUTE:
+        case GGML_OP_TRANSPOSE:
+            return true;
+        case GGML_OP_MUL_MAT: {
+            const ggml_tensor * a = op->src[0];
+            const ggml_tensor * b = op->src[1];
+            if (!mm_src0_supported(a->type)) return false;
+            if (b->type != GGML_TYPE_F32) return false;
+            if (a->nb[0] != ggml_type_size(a->type) || b->nb[0] != sizeof(float)) return false;
+            if (a->type == GGML_TYPE_F16 && (a->ne[0] % 8 != 0 || a->nb[1] % 16 != 0)) return false;
+            return true;
+        }
+        default:
+            return false;
+    }
+}
+
+static bool mi_offload_op(ggml_backend_t, const ggml_tensor * op) {
+    // worth moving CPU-resident weights for batched work (ggml-cuda.cu:2861-2868 uses 32)
+    return op->ne[1] >= 32 && op->op != GGML_OP_GET_ROWS;
+}
+
+// ---------------------------------------------------------------------------------------------
+// GGML_OP_MUL_MAT
+// ---------------------------------------------------------------------------------------------
+
+static int act_kind(ggml_type wtype) {
+    switch (wtype) {
+        case GGML_TYPE_Q4_0: case GGML_TYPE_Q8_0: return 0;
+        case GGML_TYPE_Q4_K: case GGML_TYPE_Q5_K: return 1;
+        case GGML_TYPE_F16: return 2;
+        default: return -1;
+    }
+}
+
+static size_t act_bytes(int kind, int64_t K, int64_t ncols) {
+    if (kind == 2) return (size_t) K * ncols * 2;
+    return mi_act_q8_bytes(K, ncols, kind == 1);
+}
+
+static mi_src_cols src_cols(const ggml_tensor * t) {
+    mi_src_cols x;
+    x.base = (const char *) t->data;
+    x.ne1 = t->ne[1];
+    x.ne2 = t->ne[2];
+    x.ne3 = t->ne[3];
+    x.nb1 = t->nb[1];
+    x.nb2 = t->nb[2];
+    x.nb3 = t->nb[3];
+    return x;
+}
+
+// Converted activations for (src1, kind), reused by later mul_mats of the same graph that read
+// the same, unmodified src1 (Q/K/V or gate/up projections share their input).
+static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, int kind, int64_t K) {
+    for (const auto & e : ctx->act_cache) {
+        if (e.data == src1->data && e.kind == kind && memcmp(e.ne, src1->ne, sizeof(e.ne)) == 0 &&
+            memcmp(e.nb, src1->nb, sizeof(e.nb)) == 0) {
+            return e.dev;
+        }
+    }
+    const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
+    void * dev = scratch_take(ctx, act_bytes(kind, K, ncols));
+    const mi_src_cols x = src_cols(src1);
+    if (kind == 2) {
+        mi_convert_f16(x, K, (uint16_t *) dev, ctx->stream);
+    } else {
+        const mi_act_q8 act = mi_act_q8_carve(dev, K, ncols, kind == 1);
+        if (kind == 1) mi_quantize_q8_K(x, K, act, ctx->stream);
+        else mi_quantize_q8_0(x, K, act, ctx->stream);
+    }
+    ctx->last_launches++;
+    mi_act_cache_entry e;
+    e.data = src1->data;
+    e.nbytes = ggml_nbytes(src1);
+    e.kind = kind;
+    memcpy(e.ne, src1->ne, sizeof(e.ne));
+    memcpy(e.nb, src1->nb, sizeof(e.nb));
+    e.dev = dev;
+    ctx->act_cache.push_back(e);
+    return dev;
+}
+
+static void invalidate_activations(mi_backend_ctx * ctx, const ggml_tensor * written) {
+    const char * lo = (const char *) written->data;
+    const char * hi = lo + ggml_nbytes(written);
+    auto & c = ctx->act_cache;
+    c.erase(std::remove_if(c.begin(), c.end(), [&](const mi_act_cache_entry & e) {
+                const char * elo = (const char *) e.data;
+                return elo < hi && lo < elo + e.nbytes;
+            }),
+            c.end());
+}
+
+static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
+    const ggml_tensor * src0 = dst->src[0];
+    const ggml_tensor * src1 = dst->src[1];
+    MI_ASSERT(src1->type == GGML_TYPE_F32);
+    MI_ASSERT(src0->nb[0] == ggml_type_size(src0->type));
+    MI_ASSERT(src1->nb[0] == sizeof(float));
+    MI_ASSERT(dst->nb[0] == sizeof(float));
+    MI_ASSERT(src0->ne[0] == src1->ne[0]);
+    MI_ASSERT(src1->ne[2] % src0->ne[2] == 0 && src1->ne[3] % src0->ne[3] == 0);
+
+    mi_mm_desc m;
+    m.W = src0->data;
+    m.type = src0->type;
+    m.K = src0->ne[0];
+    m.N = src0->ne[1];
+    m.ne02 = src0->ne[2];
+    m.ne03 = src0->ne[3];
+    m.nb01 = src0->nb[1];
+    m.nb02 = src0->nb[2];
+    m.nb03 = src0->nb[3];
+    m.ne11 = src1->ne[1];
+    m.ne12 = src1->ne[2];
+    m.ne13 = src1->ne[3];
+    m.dst = (float *) dst->data;
+    m.nb1 = dst->nb[1];
+    m.nb2 = dst->nb[2];
+    m.nb3 = dst->nb[3];
+
+    const int kind = act_kind(src0->type);
+    if (kind < 0) {
+        MI_ASSERT(src0->type == GGML_TYPE_F32);
+        mi_mul_mat_f32(m, src_cols(src1), ctx->stream);
+    } else {
+        void * act = get_activations(ctx, src1, kind, m.K);
+        const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
+        if (kind == 2) mi_mul_mat_f16(m, (const uint16_t *) act, ctx->stream);
+        else mi_mul_mat_q(m, mi_act_q8_carve(act, m.K, ncols, kind == 1), ctx->stream);
+    }
+    ctx->last_launches++;
+}
+
+// ---------------------------------------------------------------------------------------------
+// graph execution
+// ---------------------------------------------------------------------------------------------
+
+static bool is_noop(const ggml_tensor * node) {
+    return ggml_is_empty(node) || node->op == GGML_OP_NONE || node->op == GGML_OP_RESHAPE || node->op == GGML_OP_VIEW ||
+           node->op == GGML_OP_PERMUTE || node->op == GGML_OP_TRANSPOSE;
+}
+
+static size_t graph_scratch_bytes(const ggml_cgraph * cgraph) {
+    size_t total = 0;
+    for (int i = 0; i < cgraph->n_nodes; i++) {
+        const ggml_tensor * n = cgraph->nodes[i];
+        if (n->op != GGML_OP_MUL_MAT) continue;
+        const int kind = act_kind(n->src[0]->type);
+        if (kind < 0) continue;
+        const ggml_tensor * b = n->src[1];
+        total += (act_bytes(kind, b->ne[0], b->ne[1] * b->ne[2] * b->ne[3]) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+    }
+    return total;
+}
+
+static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * cgraph) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    mi_device_guard g(ctx->device);
+    scratch_reserve(ctx, graph_scratch_bytes(cgraph));
+    ctx->scratch_used = 0;
+    ctx->act_cache.clear();
+    ctx->last_launches = 0;
+    for (int i = 0; i < cgraph->n_nodes; i++) {
+        ggml_tensor * node = cgraph->nodes[i];
+        if (is_noop(node)) continue;
+        switch (node->op) {
+            case GGML_OP_MUL_MAT: op_mul_mat(ctx, node); break;
+            default:
+                fprintf(stderr, "%s: error: op not supported %s (%s)\n", __func__, node->name, ggml_op_desc(node));
+                MI_ASSERT(!"unsupported op");
+        }
+        invalidate_activations(ctx, node);
+    }
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fprintf(stderr, "%s: kernel launch failed: %s\n", __func__, hipGetErrorString(err));
+        return GGML_STATUS_FAILED;
+    }
+    return GGML_STATUS_SUCCESS;
+}
+
+// ---------------------------------------------------------------------------------------------
+// backend vtable
+// ---------------------------------------------------------------------------------------------
+
+static const char * mi_backend_name(ggml_backend_t backend) { return ((mi_backend_ctx *) backend->context)->name.c_str(); }
+
+static void mi_backend_free(ggml_backend_t backend) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    {
+        mi_device_guard g(ctx->device);
+        MI_CHECK(hipStreamSynchronize(ctx->stream));
+        if (ctx->scratch) MI_CHECK(hipFree(ctx->scratch));
+        MI_CHECK(hipStreamDestroy(ctx->stream));
+    }
+    delete ctx;
+    delete backend;
+}
+
+static ggml_backend_buffer_type_t mi_backend_default_buft(ggml_backend_t backend) {
+    return ggml_backend_mi355x_buffer_type(((mi_backend_ctx *) backend->context)->device);
+}
+
+static void mi_backend_set_tensor_async(ggml_backend_t backend, ggml_tensor * tensor, const void * data, size_t offset, size_t size) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    ggml_backend_buffer_t buf = tensor->view_src ? tensor->view_src->buffer : tensor->buffer;
+    MI_ASSERT(buffer_is_mi355x(buf) && "unsupported buffer type");
+    mi_device_guard g(ctx->device);
+    MI_CHECK(hipMemcpyAsync((char *) tensor->data + offset, data, size, hipMemcpyHostToDevice, ctx->stream));
+}
+
+static void mi_backend_get_tensor_async(ggml_backend_t backend, const ggml_tensor * tensor, void * data, size_t offset, size_t size) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    ggml_backend_buffer_t buf = tensor->view_src ? tensor->view_src->buffer : tensor->buffer;
+    MI_ASSERT(buffer_is_mi355x(buf) && "unsupported buffer type");
+    mi_device_guard g(ctx->device);
+    MI_CHECK(hipMemcpyAsync(data, (const char *) tensor->data + offset, size, hipMemcpyDeviceToHost, ctx->stream));
+}
+
+static bool mi_backend_cpy_tensor_async(ggml_backend_t backend_src, ggml_backend_t backend_dst, const ggml_tensor * src, ggml_tensor * dst) {
+    if (!ggml_backend_is_mi355x(backend_src) || !ggml_backend_is_mi355x(backend_dst)) return false;
+    ggml_backend_buffer_t sbuf = src->view_src ? src->view_src->buffer : src->buffer;
+    ggml_backend_buffer_t dbuf = dst->view_src ? dst->view_src->buffer : dst->buffer;
+    if (!buffer_is_mi355x(sbuf) || !buffer_is_mi355x(dbuf)) return false;
+    auto * cs = (mi_backend_ctx *) backend_src->context;
+    auto * cd = (mi_backend_ctx *) backend_dst->context;
+    if (cs->device == cd->device) {
+        mi_device_guard g(cs->device);
+        MI_CHECK(hipMemcpyAsync(dst->data, src->data, ggml_nbytes(dst), hipMemcpyDeviceToDevice, cd->stream));
+        return true;
+    }
+    // cross-device: copy on the source stream after its producers, destination waits on an event
+    mi_device_guard g(cs->device);
+    MI_CHECK(hipMemcpyPeerAsync(dst->data, cd->device, src->data, cs->device, ggml_nbytes(dst), cs->stream));
+    hipEvent_t ev;
+    MI_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    MI_CHECK(hipEventRecord(ev, cs->stream));
+    {
+        mi_device_guard g2(cd->device);
+        MI_CHECK(hipStreamWaitEvent(cd->stream, ev, 0));
+    }
+    MI_CHECK(hipEventDestroy(ev));
+    return true;
+}
+
+static void mi_backend_synchronize(ggml_backend_t backend) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    mi_device_guard g(ctx->device);
+    MI_CHECK(hipStreamSynchronize(ctx->stream));
+}
+
+static ggml_backend_event_t mi_event_new(ggml_backend_t backend) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    mi_device_guard g(ctx->device);
+    hipEvent_t ev;
+    MI_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    auto * e = new ggml_backend_event;
+    e->backend = backend;
+    e->context = ev;
+    return e;
+}
+
+static void mi_event_free(ggml_backend_event_t event) {
+    MI_CHECK(hipEventDestroy((hipEvent_t) event->context));
+    delete event;
+}
+
+static void mi_event_record(ggml_backend_event_t event) {
+    auto * ctx = (mi_backend_ctx *) event->backend->context;
+    MI_CHECK(hipEventRecord((hipEvent_t) event->context, ctx->stream));
+}
+
+static void mi_event_wait(ggml_backend_t backend, ggml_backend_event_t event) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    if (ggml_backend_is_mi355x(event->backend)) {
+        MI_CHECK(hipStreamWaitEvent(ctx->stream, (hipEvent_t) event->context, 0));
+    } else {
+        event->backend->iface.event_synchronize(event);
+    }
+}
+
+static void mi_event_synchronize(ggml_backend_event_t event) { MI_CHECK(hipEventSynchronize((hipEvent_t) event->context)); }
+
+static const ggml_backend_i k_mi_backend_i = {
+    /* get_name                */ mi_backend_name,
+    /* free                    */ mi_backend_free,
+    /* get_default_buffer_type */ mi_backend_default_buft,
+    /* set_tensor_async        */ mi_backend_set_tensor_async,
+    /* get_tensor_async        */ mi_backend_get_tensor_async,
+    /* cpy_tensor_async        */ mi_backend_cpy_tensor_async,
+    /* synchronize             */ mi_backend_synchronize,
+    /* graph_plan_create       */ nullptr,
+    /* graph_plan_free         */ nullptr,
+    /* graph_plan_compute      */ nullptr,
+    /* graph_compute           */ mi_graph_compute,
+    /* supports_op             */ mi_supports_op,
+    /* offload_op              */ mi_offload_op,
+    /* event_new               */ mi_event_new,
+    /* event_free              */ mi_event_free,
+    /* event_record            */ mi_event_record,
+    /* event_wait              */ mi_event_wait,
+    /* event_synchronize       */ mi_event_synchronize,
+};
+
+static bool mi_buft_supports_backend(ggml_backend_buffer_type_t buft, ggml_backend_t backend) {
+    if (!ggml_backend_is_mi355x(backend)) return false;
+    return ((mi_buft_ctx *) buft->context)->device == ((mi_backend_ctx *) backend->context)->device;
+}
+
+// ---------------------------------------------------------------------------------------------
+// public API
+// ---------------------------------------------------------------------------------------------
+
+extern "C" {
+
+int ggml_backend_mi355x_get_device_count(void) { return device_count(); }
+
+void ggml_backend_mi355x_get_device_description(int device, char * description, size_t description_size) {
+    hipDeviceProp_t prop;
+    MI_CHECK(hipGetDeviceProperties(&prop, device));
+    snprintf(description, description_size, "%s (%s, %d CUs)", prop.name, prop.gcnArchName, prop.multiProcessorCount);
+}
+
+void ggml_backend_mi355x_get_device_memory(int device, size_t * free, size_t * total) {
+    mi_device_guard g(device);
+    MI_CHECK(hipMemGetInfo(free, total));
+}
+
+bool ggml_backend_mi355x_register_host_buffer(void * buffer, size_t size) {
+    if (getenv("GGML_MI355X_REGISTER_HOST") == nullptr) return false;
+    const hipError_t err = hipHostRegister(buffer, size, hipHostRegisterPortable | hipHostRegisterReadOnly);
+    if (err != hipSuccess) {
+        (void) hipGetLastError();
+        return false;
+    }
+    return true;
+}
+
+void ggml_backend_mi355x_unregister_host_buffer(void * buffer) {
+    if (getenv("GGML_MI355X_REGISTER_HOST") == nullptr) return;
+    (void) hipHostUnregister(buffer);
+    (void) hipGetLastError();
+}
+
+ggml_backend_buffer_type_t ggml_backend_mi355x_buffer_type(int device) {
+    static std::mutex mutex;
+    static ggml_backend_buffer_type types[GGML_MI355X_MAX_DEVICES];
+    static mi_buft_ctx ctxs[GGML_MI355X_MAX_DEVICES];
+    static bool initialized = false;
+    std::lock_guard<std::mutex> lock(mutex);
+    if (device < 0 || device >= device_count()) return nullptr;
+    if (!initialized) {
+        for (int i = 0; i < GGML_MI355X_MAX_DEVICES; i++) {
+            ctxs[i] = mi_buft_ctx{i, "MI355X" + std::to_string(i)};
+            types[i] = ggml_backend_buffer_type{k_mi_buft_i, &ctxs[i]};
+        }
+        initialized = true;
+    }
+    return &types[device];
+}
+
+ggml_backend_buffer_type_t ggml_backend_mi355x_host_buffer_type(void) {
+    static ggml_backend_buffer_type buft = {
+        {mi_host_buft_name, mi_host_buft_alloc, mi_host_buft_align, nullptr, nullptr, mi_host_buft_supports, mi_host_buft_is_host},
+        nullptr,
+    };
+    return &buft;
+}
+
+ggml_backend_buffer_type_t ggml_backend_mi355x_split_buffer_type(const float * tensor_split) {
+    (void) tensor_split;
+    fprintf(stderr, "ggml-mi355x: the tensor-split row buffer type is not implemented yet\n");
+    return nullptr;
+}
+
+bool ggml_backend_is_mi355x(ggml_backend_t backend) {
+    return backend != nullptr && ggml_guid_matches(backend->guid, mi_guid());
+}
+
+ggml_backend_t ggml_backend_mi355x_init(int device) {
+    if (device < 0 || device >= device_count()) {
+        fprintf(stderr, "%s: invalid device %d (have %d)\n", __func__, device, device_count());
+        return nullptr;
+    }
+    auto * ctx = new mi_backend_ctx();
+    ctx->device = device;
+    ctx->name = "MI355X" + std::to_string(device);
+    {
+        mi_device_guard g(device);
+        MI_CHECK(hipStreamCreate(&ctx->stream));
+    }
+    const char * no_graphs = getenv("GGML_MI355X_DISABLE_GRAPHS");
+    ctx->graph_capture = !(no_graphs && atoi(no_graphs) != 0);
+    auto * backend = new ggml_backend{mi_guid(), k_mi_backend_i, ctx};
+    return backend;
+}
+
+void * ggml_backend_mi355x_get_stream(ggml_backend_t backend) {
+    MI_ASSERT(ggml_backend_is_mi355x(backend));
+    return ((mi_backend_ctx *) backend->context)->stream;
+}
+
+void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable) {
+    MI_ASSERT(ggml_backend_is_mi355x(backend));
+    ((mi_backend_ctx *) backend->context)->graph_capture = enable;
+}
+
+int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend) {
+    MI_ASSERT(ggml_backend_is_mi355x(backend));
+    return ((mi_backend_ctx *) backend->context)->last_launches;
+}
+
+bool ggml_backend_mi355x_quantize_activations(ggml_backend_t backend, int vec_dot_type, const float * x, int64_t K,
+                                              int64_t ncols, int8_t * qs, float * d, int16_t * s32) {
+    MI_ASSERT(ggml_backend_is_mi355x(backend));
+    const bool is_k = vec_dot_type == GGML_TYPE_Q8_K;
+    if (!is_k && vec_dot_type != GGML_TYPE_Q8_0) return false;
+    if (K % (is_k ? 256 : 32) != 0) return false;
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    mi_device_guard g(ctx->device);
+    const size_t xbytes = (size_t) K * ncols * sizeof(float);
+    void * dx = nullptr;
+    void * dq = nullptr;
+    MI_CHECK(hipMalloc(&dx, xbytes));
+    MI_CHECK(hipMalloc(&dq, mi_act_q8_bytes(K, ncols, is_k)));
+    MI_CHECK(hipMemcpy(dx, x, xbytes, hipMemcpyHostToDevice));
+    mi_src_cols src;
+    src.base = (const char *) dx;
+    src.ne1 = ncols;
+    src.ne2 = src.ne3 = 1;
+    src.nb1 = (size_t) K * sizeof(float);
+    src.nb2 = src.nb3 = src.nb1 * ncols;
+    const mi_act_q8 act = mi_act_q8_carve(dq, K, ncols, is_k);
+    if (is_k) mi_quantize_q8_K(src, K, act, ctx->stream);
+    else mi_quantize_q8_0(src, K, act, ctx->stream);
+    MI_CHECK(hipStreamSynchronize(ctx->stream));
+    MI_CHECK(hipMemcpy(qs, act.qs, (size_t) K * ncols, hipMemcpyDeviceToHost));
+    MI_CHECK(hipMemcpy(d, act.d, (size_t) (K / (is_k ? 256 : 32)) * ncols * sizeof(float), hipMemcpyDeviceToHost));
+    if (is_k && s32) MI_CHECK(hipMemcpy(s32, act.s32, (size_t) (K / 32) * ncols * sizeof(int16_t), hipMemcpyDeviceToHost));
+    MI_CHECK(hipFree(dx));
+    MI_CHECK(hipFree(dq));
+    return true;
+}
+
+static ggml_backend_t mi_reg_init(const char * params, void * user_data) {
+    (void) params;
+    return ggml_backend_mi355x_init((int) (intptr_t) user_data);
+}
+
+int ggml_backend_mi355x_reg_devices(void) {
+    static int registered = -1;
+    if (registered >= 0) return registered;
+    const int n = device_count();
+    for (int i = 0; i < n; i++) {
+        char name[128];
+        snprintf(name, sizeof(name), "MI355X%d", i);
+        ggml_backend_register(name, mi_reg_init, ggml_backend_mi355x_buffer_type(i), (void *) (intptr_t) i);
+    }
+    registered = n;
+    return n;
+}
+
+} // extern "C"
+
+// Plugging into the reference libggml (whose registry only knows the backends compiled into
+// it, ggml-backend.c:417-450): with GGML_MI355X_AUTOREGISTER=1 the library registers its
+// devices when loaded (e.g. LD_PRELOAD into the unmodified test-backend-ops). The reference
+// registers its CPU entry on the first ggml_backend_reg_get_count() call, which keeps CPU at
+// index 0 as there. The repo's own runtime instead looks this library up lazily on its first
+// registry query (csrc/core/ggml_backend_rt.cpp), so loading it never touches the GPU.
+__attribute__((constructor)) static void mi_autoregister(void) {
+    const char * env = getenv("GGML_MI355X_AUTOREGISTER");
+    if (!env || atoi(env) == 0) return;
+    (void) ggml_backend_reg_get_count();
+    ggml_backend_mi355x_reg_devices();
+}

@@ -1,0 +1,53 @@
+// mi355x_kernels.h -- host-side launchers of the gfx950 kernels (internal to the backend).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+// Activation columns of one mul_mat, quantized exactly as the reference CPU path quantizes
+// them (vec_dot_type from_float, src/ggml.c:11952-11974), stored structure-of-arrays in HBM:
+//   qs  [ncols][K]      int8 quants
+//   d   [ncols][K/QK]   f32 block scale (Q8_0: the fp16-rounded d; Q8_K: f32 d)
+//   s32 [ncols][K/32]   int16 sums of 32 quants (Q8_K only; = bsums[2j] + bsums[2j+1])
+struct mi_act_q8 {
+    int8_t * qs;
+    float * d;
+    int16_t * s32;
+    int64_t K;
+    int64_t ncols;
+};
+
+// Strided f32 activation source: column c = i1 + ne1*(i2 + ne2*i3) starts at
+// base + i1*nb1 + i2*nb2 + i3*nb3 (elements along K contiguous).
+struct mi_src_cols {
+    const char * base;
+    int64_t ne1, ne2, ne3;
+    size_t nb1, nb2, nb3;
+};
+
+// Weight matrix / output description shared by the mul_mat launchers.
+struct mi_mm_desc {
+    const void * W;        // src0 data
+    int type;              // ggml_type of src0
+    int64_t K, N;          // ne00, ne01
+    int64_t ne02, ne03;    // src0 batch dims (broadcast into src1's)
+    size_t nb01, nb02, nb03;
+    int64_t ne11, ne12, ne13;  // src1 columns / batch dims
+    float * dst;
+    size_t nb1, nb2, nb3;  // dst strides in bytes (nb0 == 4)
+};
+
+size_t mi_act_q8_bytes(int64_t K, int64_t ncols, bool is_q8K);
+mi_act_q8 mi_act_q8_carve(void * base, int64_t K, int64_t ncols, bool is_q8K);
+
+void mi_quantize_q8_0(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s);
+void mi_quantize_q8_K(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s);
+void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s);
+
+// quantized weights x quantized activations (integer dot products), any number of columns
+void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s);
+// f16 weights x f16-rounded activations
+void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s);
+// f32 x f32, both operands arbitrarily strided (src1 described by x, src0 by m.nb0x)
+void mi_mul_mat_f32(const mi_mm_desc & m, const mi_src_cols & x, hipStream_t s);

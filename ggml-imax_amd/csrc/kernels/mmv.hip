@@ -1,0 +1,335 @@
+// mmv.hip -- GGML_OP_MUL_MAT for few activation columns (decode / GEMV regime) on gfx950.
+//
+// Memory-bound: every weight byte is read once from HBM, activations (a few KB per column)
+// come from L1/L2. One wave64 owns one weight row; its lanes split the row into
+// (superblock, 64-element group) items so that a K=4096 Q4_K row (16 superblocks x 4 groups)
+// is exactly one item per lane, loaded with three aligned 16-byte loads per lane
+// (header + 32 B of nibbles). Integer dot products use v_dot4_i32_i8 on the reference's own
+// quantized activations, so each superblock's integer sum is bit-identical to
+// ggml_vec_dot_q4_K_q8_K (src/ggml-quants.c:7007-7502); only the f32 combination order across
+// superblocks differs from the CPU.
+//
+// Reference per-type dot products mirrored here:
+//   Q4_0 x Q8_0  ggml_vec_dot_q4_0_q8_0  src/ggml-quants.c:3469-3874
+//   Q8_0 x Q8_0  ggml_vec_dot_q8_0_q8_0  src/ggml-quants.c:4819+
+//   Q4_K x Q8_K  ggml_vec_dot_q4_K_q8_K  src/ggml-quants.c:7007-7502
+//   Q5_K x Q8_K  ggml_vec_dot_q5_K_q8_K  src/ggml-quants.c:7833-8378
+//   F16  x F16   ggml_vec_dot_f16        src/ggml.c:1674-1714
+//   F32  x F32   ggml_vec_dot_f32        src/ggml.c:1567-1608
+
+#include "mi355x_common.h"
+#include "mi355x_kernels.h"
+
+namespace {
+
+constexpr int kRowsPerBlock = 4;  // 4 waves x 1 row
+constexpr int kMaxCols = 8;
+
+struct mmv_geom {
+    int64_t K, N;
+    int64_t ne11, ne12, ne13;
+    int64_t r2, r3;          // broadcast ratios ne12/ne02, ne13/ne03
+    size_t nb01, nb02, nb03;
+    size_t nb1, nb2, nb3;
+    int64_t col_chunks;      // ceil(ne11 / NC)
+};
+
+// Decode blockIdx.y into (first column i11, i12, i13) and return the weight row pointer base.
+__device__ __forceinline__ void mmv_coords(const mmv_geom & g, int NC, int64_t & i11, int64_t & i12, int64_t & i13,
+                                           int64_t & i02, int64_t & i03) {
+    const int64_t y = blockIdx.y;
+    const int64_t chunk = y % g.col_chunks;
+    const int64_t z = y / g.col_chunks;
+    i12 = z % g.ne12;
+    i13 = z / g.ne12;
+    i11 = chunk * NC;
+    i02 = i12 / g.r2;
+    i03 = i13 / g.r3;
+}
+
+template <int NC>
+__device__ __forceinline__ void mmv_store(const mmv_geom & g, float * dst, int64_t row, int64_t i11, int64_t i12, int64_t i13,
+                                          float (&acc)[NC], int lane) {
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const float v = mi_wave_sum(acc[c]);
+        if (lane == 0 && i11 + c < g.ne11) {
+            *(float *) ((char *) dst + (i11 + c) * g.nb1 + i12 * g.nb2 + i13 * g.nb3 + row * sizeof(float)) = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- Q4_K / Q5_K x Q8_K
+
+template <int NC, bool Q5>
+__global__ __launch_bounds__(256) void k_mmv_kq(const uint8_t * __restrict__ W, mi_act_q8 act, float * __restrict__ dst, mmv_geom g) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t) blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+    if (row >= g.N) return;
+    int64_t i11, i12, i13, i02, i03;
+    mmv_coords(g, NC, i11, i12, i13, i02, i03);
+    constexpr int BS = Q5 ? 176 : 144;
+    const uint8_t * wrow = W + i02 * g.nb02 + i03 * g.nb03 + row * g.nb01;
+    const int nsb = (int) (g.K / 256);
+    const int64_t col0 = i11 + g.ne11 * (i12 + g.ne12 * i13);
+
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) acc[c] = 0.0f;
+
+    for (int it = lane; it < 4 * nsb; it += 64) {
+        const int s = it >> 2;
+        const int j = it & 3;
+        const uint8_t * blk = wrow + (size_t) s * BS;
+        const uint4 hdr = *(const uint4 *) blk;
+        const uint8_t * qp = blk + (Q5 ? 48 : 16) + 32 * j;
+        const uint4 qa = *(const uint4 *) qp;
+        const uint4 qb = *(const uint4 *) (qp + 16);
+        uint32_t q[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+        uint32_t qlo[8], qhi[8];
+        if constexpr (Q5) {
+            const uint4 ha = *(const uint4 *) (blk + 16);
+            const uint4 hb = *(const uint4 *) (blk + 32);
+            const uint32_t h[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = (q[i] & 0x0F0F0F0Fu) | (((h[i] >> (2 * j)) & 0x01010101u) << 4);
+                qhi[i] = ((q[i] >> 4) & 0x0F0F0F0Fu) | (((h[i] >> (2 * j + 1)) & 0x01010101u) << 4);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = q[i] & 0x0F0F0F0Fu;
+                qhi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
+            }
+        }
+        const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF));
+        const float dmw = mi_h2f((uint16_t) (hdr.x >> 16));
+        int sc0, m0, sc1, m1;
+        mi_scale_min_k4(2 * j, hdr.y, hdr.z, hdr.w, sc0, m0);
+        mi_scale_min_k4(2 * j + 1, hdr.y, hdr.z, hdr.w, sc1, m1);
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && i11 + c >= g.ne11) break;
+            const int64_t col = col0 + c;
+            const int4 * a = (const int4 *) (act.qs + col * g.K + (int64_t) s * 256 + 64 * j);
+            const int4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+            const int alo[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const int ahi[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            int lo = 0, hi = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                lo = mi_dot4((int) qlo[i], alo[i], lo);
+                hi = mi_dot4((int) qhi[i], ahi[i], hi);
+            }
+            const int sumi = sc0 * lo + sc1 * hi;
+            const int ss = *(const int *) (act.s32 + col * (g.K / 32) + s * 8 + 2 * j);
+            const int summ = m0 * (int) (int16_t) (ss & 0xFFFF) + m1 * (ss >> 16);
+            const float dy = act.d[col * nsb + s];
+            acc[c] += dy * (dw * (float) sumi - dmw * (float) summ);
+        }
+    }
+    mmv_store<NC>(g, dst, row, i11, i12, i13, acc, lane);
+}
+
+// ---------------------------------------------------------------- Q4_0 / Q8_0 x Q8_0
+
+// 32 quants of a block starting at a 2-byte aligned address, gathered from aligned dwords.
+template <int NBYTES>
+__device__ __forceinline__ void load_qs_unaligned(const uint8_t * p, uint32_t (&out)[NBYTES / 4]) {
+    const uintptr_t addr = (uintptr_t) p;
+    const uint32_t * w = (const uint32_t *) (addr & ~(uintptr_t) 3);
+    const int shift = (int) (addr & 3);  // 0 or 2 here
+    uint32_t raw[NBYTES / 4 + 1];
+#pragma unroll
+    for (int i = 0; i < NBYTES / 4; i++) raw[i] = w[i];
+    raw[NBYTES / 4] = shift ? w[NBYTES / 4] : 0u;  // buffers carry 256 B of tail slack
+#pragma unroll
+    for (int i = 0; i < NBYTES / 4; i++) out[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], shift);
+}
+
+template <int NC, bool Q8>
+__global__ __launch_bounds__(256) void k_mmv_q0(const uint8_t * __restrict__ W, mi_act_q8 act, float * __restrict__ dst, mmv_geom g) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t) blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+    if (row >= g.N) return;
+    int64_t i11, i12, i13, i02, i03;
+    mmv_coords(g, NC, i11, i12, i13, i02, i03);
+    constexpr int BS = Q8 ? 34 : 18;
+    const uint8_t * wrow = W + i02 * g.nb02 + i03 * g.nb03 + row * g.nb01;
+    const int nb = (int) (g.K / 32);
+    const int64_t col0 = i11 + g.ne11 * (i12 + g.ne12 * i13);
+
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) acc[c] = 0.0f;
+
+    for (int b = lane; b < nb; b += 64) {
+        const uint8_t * blk = wrow + (size_t) b * BS;
+        const float dw = mi_h2f(*(const uint16_t *) blk);
+        int wq[8];
+        if constexpr (Q8) {
+            uint32_t t[8];
+            load_qs_unaligned<32>(blk + 2, t);
+#pragma unroll
+            for (int i = 0; i < 8; i++) wq[i] = (int) t[i];
+        } else {
+            uint32_t t[4];
+            load_qs_unaligned<16>(blk + 2, t);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                wq[i] = (int) (t[i] & 0x0F0F0F0Fu);          // elements 4i..4i+3
+                wq[i + 4] = (int) ((t[i] >> 4) & 0x0F0F0F0Fu);  // elements 16+4i..
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && i11 + c >= g.ne11) break;
+            const int64_t col = col0 + c;
+            const int4 * a = (const int4 *) (act.qs + col * g.K + (int64_t) b * 32);
+            const int4 a0 = a[0], a1 = a[1];
+            const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            int sumi = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) sumi = mi_dot4(wq[i], av[i], sumi);
+            if constexpr (!Q8) {
+                // (q - 8) * y summed = q*y - 8 * sum(y)
+                int sy = 0;
+#pragma unroll
+                for (int i = 0; i < 8; i++) sy = mi_dot4(0x01010101, av[i], sy);
+                sumi -= 8 * sy;
+            }
+            acc[c] += (float) sumi * (dw * act.d[col * nb + b]);
+        }
+    }
+    mmv_store<NC>(g, dst, row, i11, i12, i13, acc, lane);
+}
+
+// ---------------------------------------------------------------- F16 x F16
+
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+
+template <int NC>
+__global__ __launch_bounds__(256) void k_mmv_f16(const uint8_t * __restrict__ W, const uint16_t * __restrict__ xh, float * __restrict__ dst, mmv_geom g) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t) blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+    if (row >= g.N) return;
+    int64_t i11, i12, i13, i02, i03;
+    mmv_coords(g, NC, i11, i12, i13, i02, i03);
+    const uint16_t * wrow = (const uint16_t *) (W + i02 * g.nb02 + i03 * g.nb03 + row * g.nb01);
+    const int64_t col0 = i11 + g.ne11 * (i12 + g.ne12 * i13);
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) acc[c] = 0.0f;
+    const int64_t nv = g.K / 8;
+    for (int64_t v = lane; v < nv; v += 64) {
+        const uint4 w4 = *(const uint4 *) (wrow + v * 8);
+        const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && i11 + c >= g.ne11) break;
+            const uint4 x4 = *(const uint4 *) (xh + (col0 + c) * g.K + v * 8);
+            const uint32_t xv[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                h2_t a, b;
+                __builtin_memcpy(&a, &wv[i], 4);
+                __builtin_memcpy(&b, &xv[i], 4);
+                acc[c] = __builtin_amdgcn_fdot2(a, b, acc[c], false);
+            }
+        }
+    }
+    // K tail (K % 8)
+    for (int64_t k = nv * 8 + lane; k < g.K; k += 64) {
+        const float w = mi_h2f(wrow[k]);
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && i11 + c >= g.ne11) break;
+            acc[c] += w * mi_h2f(xh[(col0 + c) * g.K + k]);
+        }
+    }
+    mmv_store<NC>(g, dst, row, i11, i12, i13, acc, lane);
+}
+
+// ---------------------------------------------------------------- F32 x F32 (strided)
+
+// one wave per output element; src1 column described by mi_src_cols (nb10 == 4)
+__global__ __launch_bounds__(256) void k_mm_f32(const uint8_t * __restrict__ W, mi_src_cols x, float * __restrict__ dst, mmv_geom g) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t) blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+    if (row >= g.N) return;
+    const int64_t y = blockIdx.y;
+    const int64_t i11 = y % g.ne11;
+    const int64_t z = y / g.ne11;
+    const int64_t i12 = z % g.ne12, i13 = z / g.ne12;
+    const int64_t i02 = i12 / g.r2, i03 = i13 / g.r3;
+    const float * w = (const float *) (W + i02 * g.nb02 + i03 * g.nb03 + row * g.nb01);
+    const float * xc = (const float *) (x.base + i11 * x.nb1 + i12 * x.nb2 + i13 * x.nb3);
+    float acc = 0.0f;
+    for (int64_t k = lane; k < g.K; k += 64) acc = __builtin_fmaf(w[k], xc[k], acc);
+    acc = mi_wave_sum(acc);
+    if (lane == 0) *(float *) ((char *) dst + i11 * g.nb1 + i12 * g.nb2 + i13 * g.nb3 + row * sizeof(float)) = acc;
+}
+
+mmv_geom make_geom(const mi_mm_desc & m, int NC) {
+    mmv_geom g;
+    g.K = m.K;
+    g.N = m.N;
+    g.ne11 = m.ne11;
+    g.ne12 = m.ne12;
+    g.ne13 = m.ne13;
+    g.r2 = m.ne12 / m.ne02;
+    g.r3 = m.ne13 / m.ne03;
+    g.nb01 = m.nb01;
+    g.nb02 = m.nb02;
+    g.nb03 = m.nb03;
+    g.nb1 = m.nb1;
+    g.nb2 = m.nb2;
+    g.nb3 = m.nb3;
+    g.col_chunks = (m.ne11 + NC - 1) / NC;
+    return g;
+}
+
+} // namespace
+
+#define MI_MMV_LAUNCH(KERNEL, NC, ...)                                                          \
+    do {                                                                                         \
+        const mmv_geom g = make_geom(m, NC);                                                     \
+        const dim3 grid((unsigned) ((m.N + kRowsPerBlock - 1) / kRowsPerBlock),                  \
+                        (unsigned) (g.col_chunks * m.ne12 * m.ne13));                            \
+        hipLaunchKernelGGL((KERNEL<NC, ##__VA_ARGS__>), grid, dim3(256), 0, s, (const uint8_t *) m.W, \
+                           act_or_x, m.dst, g);                                                  \
+    } while (0)
+
+#define MI_MMV_SWITCH(KERNEL, ...)                                  \
+    switch (nc) {                                                   \
+        case 1: MI_MMV_LAUNCH(KERNEL, 1, ##__VA_ARGS__); break;     \
+        case 2: MI_MMV_LAUNCH(KERNEL, 2, ##__VA_ARGS__); break;     \
+        case 3: MI_MMV_LAUNCH(KERNEL, 3, ##__VA_ARGS__); break;     \
+        case 4: MI_MMV_LAUNCH(KERNEL, 4, ##__VA_ARGS__); break;     \
+        default: MI_MMV_LAUNCH(KERNEL, 8, ##__VA_ARGS__); break;    \
+    }
+
+void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s) {
+    const int nc = m.ne11 >= 5 ? 8 : (int) m.ne11;
+    const mi_act_q8 act_or_x = act;
+    switch (m.type) {
+        case 12: MI_MMV_SWITCH(k_mmv_kq, false); break;  // Q4_K
+        case 13: MI_MMV_SWITCH(k_mmv_kq, true); break;   // Q5_K
+        case 2:  MI_MMV_SWITCH(k_mmv_q0, false); break;  // Q4_0
+        case 8:  MI_MMV_SWITCH(k_mmv_q0, true); break;   // Q8_0
+        default: break;
+    }
+}
+
+void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s) {
+    const int nc = m.ne11 >= 5 ? 8 : (int) m.ne11;
+    const uint16_t * act_or_x = xh;
+    MI_MMV_SWITCH(k_mmv_f16);
+}
+
+void mi_mul_mat_f32(const mi_mm_desc & m, const mi_src_cols & x, hipStream_t s) {
+    const mmv_geom g = make_geom(m, 1);
+    const dim3 grid((unsigned) ((m.N + kRowsPerBlock - 1) / kRowsPerBlock), (unsigned) (m.ne11 * m.ne12 * m.ne13));
+    hipLaunchKernelGGL(k_mm_f32, grid, dim3(256), 0, s, (const uint8_t *) m.W, x, m.dst, g);
+}

@@ -1,0 +1,141 @@
+// quantize.hip -- activation quantizers for GGML_OP_MUL_MAT on gfx950.
+//
+// The reference CPU mul_mat converts every src1 column to the weight type's vec_dot_type
+// before the dot products (src/ggml.c:11952-11974). Parity with it is bit-exact only if the
+// GPU produces the same int8 quants and scales, so these kernels reproduce the reference x86
+// build's exact rounding sequence:
+//   Q8_0: AVX2 quantize_row_q8_0 (src/ggml-quants.c:535-618): amax, d = amax/127 -> fp16 RNE,
+//         id = 127/amax, q = round-half-even(x*id)           (vmulps + vroundps)
+//   Q8_K: quantize_row_q8_K_reference (src/ggml-quants.c:3370-3407) as gcc -mfma compiles it:
+//         first max-|x| element (sign kept), iscale = -127/max, q = min(127, RNE(fma(iscale, x,
+//         1.5*2^23)) via the bit trick), d = 1/iscale, sums of 16 (we keep sums of 32).
+//   F16:  ggml_fp32_to_fp16_row (F16C, RNE)                     (src/ggml.c:365-382)
+// All three are HBM-bound streaming kernels: one read of X (4 B/elem) and ~1.1 B/elem written.
+
+#include "mi355x_common.h"
+#include "mi355x_kernels.h"
+
+static __device__ __forceinline__ const float * col_ptr(const mi_src_cols & x, int64_t c) {
+    const int64_t i1 = c % x.ne1;
+    const int64_t i2 = (c / x.ne1) % x.ne2;
+    const int64_t i3 = c / (x.ne1 * x.ne2);
+    return (const float *) (x.base + i1 * x.nb1 + i2 * x.nb2 + i3 * x.nb3);
+}
+
+size_t mi_act_q8_bytes(int64_t K, int64_t ncols, bool is_q8K) {
+    const size_t qs = (size_t) (K * ncols + 255) & ~(size_t) 255;
+    const size_t d = ((size_t) (K / (is_q8K ? 256 : 32)) * ncols * sizeof(float) + 255) & ~(size_t) 255;
+    const size_t s = is_q8K ? (((size_t) (K / 32) * ncols * sizeof(int16_t) + 255) & ~(size_t) 255) : 0;
+    return qs + d + s;
+}
+
+mi_act_q8 mi_act_q8_carve(void * base, int64_t K, int64_t ncols, bool is_q8K) {
+    char * p = (char *) base;
+    mi_act_q8 a;
+    a.K = K;
+    a.ncols = ncols;
+    a.qs = (int8_t *) p;
+    p += ((size_t) (K * ncols) + 255) & ~(size_t) 255;
+    a.d = (float *) p;
+    p += ((size_t) (K / (is_q8K ? 256 : 32)) * ncols * sizeof(float) + 255) & ~(size_t) 255;
+    a.s32 = is_q8K ? (int16_t *) p : nullptr;
+    return a;
+}
+
+// One 32-element block per half-wave, one element per lane.
+__global__ __launch_bounds__(256) void k_quantize_q8_0(mi_src_cols x, int64_t K, mi_act_q8 act, int64_t nblocks_total) {
+    const int64_t gid = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t blk = gid >> 5;
+    const int l = threadIdx.x & 31;
+    if (blk >= nblocks_total) return;  // whole half-waves exit together (nblocks*32 threads)
+    const int64_t nb_per_col = K / 32;
+    const int64_t c = blk / nb_per_col;
+    const int64_t b = blk % nb_per_col;
+    const float v = col_ptr(x, c)[b * 32 + l];
+    float amax = fabsf(v);
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 32));
+    const float d = amax / 127.f;
+    const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+    const float q = __builtin_rintf(__fmul_rn(v, id));
+    act.qs[c * K + b * 32 + l] = (int8_t) (int) q;
+    if (l == 0) act.d[c * nb_per_col + b] = mi_h2f(mi_f2h(d));
+}
+
+// One 256-element superblock per wave, four consecutive elements per lane.
+__global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K, mi_act_q8 act, int64_t nblocks_total) {
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t blk = (int64_t) blockIdx.x * 4 + wave;
+    if (blk >= nblocks_total) return;  // wave-uniform
+    const int64_t nb_per_col = K / 256;
+    const int64_t c = blk / nb_per_col;
+    const int64_t b = blk % nb_per_col;
+    const float4 v4 = *(const float4 *) (col_ptr(x, c) + b * 256 + lane * 4);
+    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+
+    // first element with the largest |x| (strict '>' scan order), keep its signed value
+    float amax = 0.0f, vmax = 0.0f;
+    int idx = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float ax = fabsf(v[i]);
+        if (ax > amax) { amax = ax; vmax = v[i]; idx = lane * 4 + i; }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float oa = __shfl_xor(amax, off, 64);
+        const float ov = __shfl_xor(vmax, off, 64);
+        const int oi = __shfl_xor(idx, off, 64);
+        if (oa > amax || (oa == amax && oi < idx)) { amax = oa; vmax = ov; idx = oi; }
+    }
+    int8_t * qs = act.qs + c * K + b * 256;
+    int16_t * s32 = act.s32 + c * (K / 32) + b * 8;
+    if (amax == 0.0f) {
+        *(uint32_t *) (qs + lane * 4) = 0u;
+        if ((lane & 7) == 0) s32[lane >> 3] = 0;
+        if (lane == 0) act.d[c * nb_per_col + b] = 0.0f;
+        return;
+    }
+    const float iscale = -127.f / vmax;
+    uint32_t packed = 0;
+    int sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float t = __builtin_fmaf(iscale, v[i], 12582912.f);
+        const int bits = __float_as_int(t);
+        int q = (bits & 0x007fffff) - 0x00400000;
+        q = q < 127 ? q : 127;
+        sum += q;
+        packed |= ((uint32_t) (q & 0xFF)) << (8 * i);
+    }
+    *(uint32_t *) (qs + lane * 4) = packed;
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    sum += __shfl_xor(sum, 4, 64);
+    if ((lane & 7) == 0) s32[lane >> 3] = (int16_t) sum;
+    if (lane == 0) act.d[c * nb_per_col + b] = 1.0f / iscale;
+}
+
+__global__ __launch_bounds__(256) void k_convert_f16(mi_src_cols x, int64_t K, uint16_t * out, int64_t total) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t c = i / K, k = i % K;
+    out[i] = mi_f2h(col_ptr(x, c)[k]);
+}
+
+void mi_quantize_q8_0(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s) {
+    const int64_t nblk = (K / 32) * act.ncols;
+    const int64_t threads = nblk * 32;
+    hipLaunchKernelGGL(k_quantize_q8_0, dim3((unsigned) ((threads + 255) / 256)), dim3(256), 0, s, x, K, act, nblk);
+}
+
+void mi_quantize_q8_K(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s) {
+    const int64_t nblk = (K / 256) * act.ncols;
+    hipLaunchKernelGGL(k_quantize_q8_K, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, act, nblk);
+}
+
+void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s) {
+    const int64_t total = K * x.ne1 * x.ne2 * x.ne3;
+    hipLaunchKernelGGL(k_convert_f16, dim3((unsigned) ((total + 255) / 256)), dim3(256), 0, s, x, K, out, total);
+}

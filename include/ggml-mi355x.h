@@ -1,0 +1,69 @@
+// ggml-mi355x.h -- C-ABI entry points of the MI355X (gfx950) ggml backend.
+//
+// Drop-in counterpart of the reference's device-backend header src/ggml-cuda.h:19-40
+// (NAIST-Archlab/ggml-imax @ v2); each function cites the declaration it replaces. Everything
+// else a caller needs goes through the generic ggml_backend_* API (include/ggml_abi.h), exactly
+// as with the CUDA and Metal backends. The library also registers one registry entry per
+// device ("MI355X0", "MI355X1", ...) from an ELF constructor, so registry-driven tools
+// (tests/test-backend-ops.cpp, ggml_backend_reg_init_backend_from_str) find it unmodified.
+#pragma once
+
+#include "ggml_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GGML_MI355X_MAX_DEVICES 16
+
+// ggml-cuda.h:21  ggml_backend_cuda_init(int device)
+GGML_API ggml_backend_t ggml_backend_mi355x_init(int device);
+
+// ggml-cuda.h:23  ggml_backend_is_cuda(ggml_backend_t)
+GGML_API bool ggml_backend_is_mi355x(ggml_backend_t backend);
+
+// ggml-cuda.h:26  ggml_backend_cuda_buffer_type(int device): device-resident (HBM) buffers
+GGML_API ggml_backend_buffer_type_t ggml_backend_mi355x_buffer_type(int device);
+
+// ggml-cuda.h:29  ggml_backend_cuda_split_buffer_type(const float * tensor_split): rows of a
+// matrix split across devices (tensor-split row path)
+GGML_API ggml_backend_buffer_type_t ggml_backend_mi355x_split_buffer_type(const float * tensor_split);
+
+// ggml-cuda.h:32  ggml_backend_cuda_host_buffer_type(): pinned host memory for fast H2D/D2H
+GGML_API ggml_backend_buffer_type_t ggml_backend_mi355x_host_buffer_type(void);
+
+// ggml-cuda.h:34-36
+GGML_API int  ggml_backend_mi355x_get_device_count(void);
+GGML_API void ggml_backend_mi355x_get_device_description(int device, char * description, size_t description_size);
+GGML_API void ggml_backend_mi355x_get_device_memory(int device, size_t * free, size_t * total);
+
+// ggml-cuda.h:38-39
+GGML_API bool ggml_backend_mi355x_register_host_buffer(void * buffer, size_t size);
+GGML_API void ggml_backend_mi355x_unregister_host_buffer(void * buffer);
+
+// ggml-cuda.cu:3024-3042 ggml_backend_cuda_reg_devices (called by the reference registry init;
+// here also run from the library constructor). Returns the number of devices registered.
+GGML_API int ggml_backend_mi355x_reg_devices(void);
+
+// --- MI355X extensions (no reference counterpart) ---
+
+// hipStream_t the backend launches on (for external timing with HIP events / stream interop)
+GGML_API void * ggml_backend_mi355x_get_stream(ggml_backend_t backend);
+
+// hipGraph capture of repeated identical graphs (decode loops); on by default, env
+// GGML_MI355X_DISABLE_GRAPHS=1 turns it off (analogue of GGML_CUDA_DISABLE_GRAPHS).
+GGML_API void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable);
+
+// Number of kernels launched by the last graph_compute (for tests / profiling).
+GGML_API int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend);
+
+// Runs the device activation quantizer that GGML_OP_MUL_MAT uses for `vec_dot_type`
+// (GGML_TYPE_Q8_0 or GGML_TYPE_Q8_K) on ncols host columns of K floats and returns its
+// structure-of-arrays result: qs [ncols*K], d [ncols*K/QK], s32 [ncols*K/32] (Q8_K only,
+// sums of 32 quants). Lets tests compare the device rounding with the reference bit for bit.
+GGML_API bool ggml_backend_mi355x_quantize_activations(ggml_backend_t backend, int vec_dot_type, const float * x,
+                                                       int64_t K, int64_t ncols, int8_t * qs, float * d, int16_t * s32);
+
+#ifdef __cplusplus
+}
+#endif
