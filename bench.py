@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X ggml backend on BASELINE.json's headline metric.
+
+Workload (BASELINE.json metric "Q4_K 4096x4096 mul_mat GB/s-effective", configs[1..2] shape):
+  one step = one ggml_backend_graph_compute of a graph holding R independent GGML_OP_MUL_MAT
+  nodes  Y_r = W_r . X_r  with W_r Q4_K [K=4096, N=4096] (R distinct weight copies, >256 MiB in
+  total so the 256 MiB Infinity Cache cannot serve them) and X_r f32 [4096, B=1] -- i.e. R
+  decode-style GEMVs, inputs resident in HBM, activation quantization included.
+  value = R * algorithmic bytes * steps * world / max-over-ranks wall time of the timed steps,
+  algorithmic bytes per unit = N*(K/256)*144 + 4*K*B + 4*N*B.
+
+Multi-GPU (--gpus N via torch.distributed.run): independent prompts shard across GPUs, each
+rank owns a full replica of its weights and runs the same per-GPU work ("scaling": "weak"); the
+only collective is the timing barrier / max-reduction (no data-path exchange exists).
+
+Extra fields: "roofline" (dominant kernel: algorithmic bytes per launch / HIP-event duration on
+the backend's own stream, vs 8 TB/s HBM), "cpu_baseline" (the reference ggml CPU backend,
+oracle/_ref/libggml_ref.so, timed on this host -- rank 0, N=1 only) and a per-config sweep.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ggml-imax_amd"))
+
+from ggml_mi355x import ggml as G  # noqa: E402
+from ggml_mi355x import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+TYPE_NAMES = {"q4_K": 12, "q5_K": 13, "q4_0": 2, "q8_0": 8, "f16": 1}
+
+
+def unit_bytes(t: int, K: int, N: int, B: int) -> int:
+    return G.row_size(t, K) * N + 4 * K * B + 4 * N * B
+
+
+class MulMatWorkload:
+    """R independent mul_mat nodes in one graph, all tensors resident on `backend`."""
+
+    def __init__(self, lib, backend, t, K, N, B, R, seed=42):
+        self.lib, self.backend, self.t, self.K, self.N, self.B, self.R = lib, backend, t, K, N, B, R
+        ovh = lib.ggml_tensor_overhead() * (3 * R + 8) + lib.ggml_graph_overhead_custom(4 * R + 16, False)
+        self.ctx = G.Context(lib, ovh, no_alloc=True)
+        c = self.ctx.ctx
+        self.w = [lib.ggml_new_tensor_2d(c, t, K, N) for _ in range(R)]
+        self.x = [lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F32, K, B) for _ in range(R)]
+        self.y = [lib.ggml_mul_mat(c, self.w[r], self.x[r]) for r in range(R)]
+        self.graph = lib.ggml_new_graph_custom(c, 4 * R + 16, False)
+        for y in self.y:
+            lib.ggml_build_forward_expand(self.graph, y)
+        self.buf = lib.ggml_backend_alloc_ctx_tensors(c, backend)
+        assert self.buf, "device allocation failed"
+        wf = synth.uniform(seed, K * N)
+        wq = np.empty(G.row_size(t, K) * N, np.uint8)
+        lib.ggml_quantize_chunk(t, wf.ctypes.data, wq.ctypes.data, 0, N, K, None)
+        self.wq = wq
+        for r in range(R):
+            G.tensor_set(lib, self.w[r], wq)
+            G.tensor_set(lib, self.x[r], synth.uniform(seed + 1 + r, K * B))
+
+    def step(self):
+        st = self.lib.ggml_backend_graph_compute_async(self.backend, self.graph)
+        assert st == 0, st
+
+    def free(self):
+        self.lib.ggml_backend_buffer_free(self.buf)
+        self.ctx.free()
+
+
+def cpu_baseline(t, K, N, B, seconds=10.0):
+    """The reference ggml CPU backend (oracle/_ref/libggml_ref.so, compiled from the reference
+    sources with its own x86 flags) on a bounded sample of the same workload."""
+    ref_path = os.path.join(REPO, "oracle", "_ref", "libggml_ref.so")
+    if not os.path.exists(ref_path):
+        return None
+    ref = G.Lib([ref_path], isolated=True)
+    threads = int(os.environ.get("BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    cpu = ref.ggml_backend_cpu_init()
+    ref.ggml_backend_cpu_set_n_threads(cpu, threads)
+    R = 32  # same rotation depth as the GPU run: the weights do not fit the CPU caches either
+    wl = MulMatWorkload(ref, cpu, t, K, N, B, R)
+    wl.lib.ggml_backend_graph_compute(cpu, wl.graph)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        ref.ggml_backend_graph_compute(cpu, wl.graph)
+        n += 1
+    dt = time.perf_counter() - t0
+    wl.free()
+    ref.ggml_backend_free(cpu)
+    units = n * R
+    return {
+        "value": round(units * unit_bytes(t, K, N, B) / dt / 1e9, 2), "unit": "GB/s",
+        "cores": threads, "kind": "reference",
+        "sample": f"{units} mul_mats ({n} graphs x {R}) of the same workload in {dt:.1f} s; "
+                  f"us/mul_mat={dt / units * 1e6:.1f}; host={_cpu_model()}",
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def event_time_per_step(torch, wl, stream_ptr, iters=20):
+    """HIP-event duration of one step on the backend's own stream (ms)."""
+    s = torch.cuda.ExternalStream(stream_ptr)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        wl.step()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def load_traffic(kernel_hint: str):
+    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary
+    (tools/pmc_traffic.py -> profiles/*_pmc_traffic.json), or None."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if kernel_hint in k:
+                return v.get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--type", default="q4_K", choices=sorted(TYPE_NAMES))
+    ap.add_argument("--K", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=4096)
+    ap.add_argument("--B", type=int, default=1)
+    ap.add_argument("--rotate", type=int, default=32)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    lib = G.runtime()
+    backend = G.mi355x_backend(lib, local_rank)
+    stream_ptr = lib.ggml_backend_mi355x_get_stream(backend)
+    t = TYPE_NAMES[args.type]
+    K, N, B, R = args.K, args.N, args.B, args.rotate
+    wl = MulMatWorkload(lib, backend, t, K, N, B, R)
+
+    for _ in range(args.warmup):
+        wl.step()
+    lib.ggml_backend_synchronize(backend)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step()
+    lib.ggml_backend_synchronize(backend)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    ub = unit_bytes(t, K, N, B)
+    value = R * ub * args.steps * world / dt / 1e9
+    launches = lib.ggml_backend_mi355x_last_launch_count(backend)
+
+    # dominant kernel: HIP events on the backend stream around whole steps, per launch
+    step_ms = event_time_per_step(torch, wl, stream_ptr)
+    mm_launches = R  # one GEMV launch per mul_mat node
+    per_launch_s = step_ms / 1e3 / max(launches, 1)
+    achieved = ub / (step_ms / 1e3 / mm_launches) / 1e9
+    traffic = load_traffic("mmv")
+
+    result = {
+        "metric": "Q4_K 4096x4096 mul_mat GB/s-effective (+ GPT-2 tokens/s), 1 GPU",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "q4_K x q8_K int8-dot, f32 accumulate" if t in (12, 13) else args.type,
+        "data": "synthetic (splitmix64 seed 42 weights quantized by the runtime's ggml_quantize_chunk; seeded X)",
+        "config": {"workload": f"{R} independent {args.type} {K}x{N} mul_mat (GEMV, B={B}) per step, rotated weights "
+                               f"({R * G.row_size(t, K) * N / 2**20:.0f} MiB)", "K": K, "N": N, "B": B,
+                   "rotated_copies": R, "parallelism": f"replica x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel_launches_per_step": launches, "event_ms_per_step": round(step_ms, 4),
+                     "note": "achieved = algorithmic bytes per mul_mat / (HIP-event step time / mul_mats per step); "
+                             "includes activation quantization and inter-kernel gaps"},
+    }
+
+    if rank == 0 and world == 1 and not args.no_sweep:
+        sweep = {}
+        for name, tt, k, n in (("q4_0_4096x4096", 2, 4096, 4096), ("q4_K_4096x11008", 12, 4096, 11008),
+                               ("q5_K_4096x11008", 13, 4096, 11008), ("q8_0_4096x11008", 8, 4096, 11008)):
+            r = max(8, int(320 * 2**20 // (G.row_size(tt, k) * n)) + 1)
+            w2 = MulMatWorkload(lib, backend, tt, k, n, 1, r)
+            for _ in range(3):
+                w2.step()
+            lib.ggml_backend_synchronize(backend)
+            ms = event_time_per_step(torch, w2, stream_ptr, iters=10)
+            sweep[name] = {"GB/s": round(r * unit_bytes(tt, k, n, 1) / (ms / 1e3) / 1e9, 1),
+                           "us_per_mul_mat": round(ms * 1e3 / r, 2)}
+            w2.free()
+        result["sweep"] = sweep
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(t, K, N, B, args.cpu_seconds)
+
+    wl.free()
+    lib.ggml_backend_free(backend)
+    if rank == 0:
+        print(json.dumps(result))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

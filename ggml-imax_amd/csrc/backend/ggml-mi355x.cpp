@@ -443,6 +443,74 @@ static size_t graph_scratch_bytes(const ggml_cgraph * cgraph) {
     return total;
 }
 
+// ---- decode-regime fusion: quantize-in-kernel GEMV, independent mul_mats in one launch ----
+
+static bool overlaps(const ggml_tensor * a, const ggml_tensor * b) {
+    const char * a0 = (const char *) a->data;
+    const char * b0 = (const char *) b->data;
+    return a0 < b0 + ggml_nbytes(b) && b0 < a0 + ggml_nbytes(a);
+}
+
+static bool fused_mv_eligible(const ggml_tensor * n) {
+    if (n->op != GGML_OP_MUL_MAT) return false;
+    const ggml_tensor * a = n->src[0];
+    const ggml_tensor * b = n->src[1];
+    if (b->type != GGML_TYPE_F32 || !mi_mmv_fused_supported(a->type, a->ne[0], b->ne[1])) return false;
+    if (a->ne[2] != 1 || a->ne[3] != 1 || b->ne[2] != 1 || b->ne[3] != 1) return false;
+    if (a->nb[0] != ggml_type_size(a->type) || b->nb[0] != sizeof(float) || n->nb[0] != sizeof(float)) return false;
+    if (((uintptr_t) a->data | a->nb[1]) % 16 != 0 || ((uintptr_t) b->data | b->nb[1]) % 16 != 0) return false;
+    return true;
+}
+
+static bool same_group_shape(const ggml_tensor * x, const ggml_tensor * y) {
+    const ggml_tensor * xa = x->src[0];
+    const ggml_tensor * ya = y->src[0];
+    return xa->type == ya->type && xa->ne[0] == ya->ne[0] && xa->ne[1] == ya->ne[1] && xa->nb[1] == ya->nb[1] &&
+           x->src[1]->ne[1] == y->src[1]->ne[1] && x->src[1]->nb[1] == y->src[1]->nb[1] && x->nb[1] == y->nb[1];
+}
+
+// Launches nodes[i] and following independent same-shape mul_mats as one fused kernel.
+// Returns the index of the last node consumed.
+static int run_fused_group(mi_backend_ctx * ctx, ggml_cgraph * cgraph, int i) {
+    static_assert(sizeof(mi_mmv_group) < 4096, "kernel argument block");
+    ggml_tensor * first = cgraph->nodes[i];
+    std::vector<ggml_tensor *> members = {first};
+    int last = i;
+    for (int j = i + 1; j < cgraph->n_nodes && (int) members.size() < kMiMaxMembers; j++) {
+        ggml_tensor * n = cgraph->nodes[j];
+        if (is_noop(n)) continue;
+        if (!fused_mv_eligible(n) || !same_group_shape(first, n)) break;
+        bool independent = true;
+        for (ggml_tensor * m : members) {
+            if (overlaps(n->src[1], m) || overlaps(n->src[0], m) || overlaps(n, m->src[0]) || overlaps(n, m->src[1]) || overlaps(n, m)) {
+                independent = false;
+                break;
+            }
+        }
+        if (!independent) break;
+        members.push_back(n);
+        last = j;
+    }
+    mi_mmv_group g;
+    g.type = first->src[0]->type;
+    g.n = (int) members.size();
+    g.ncols = (int) first->src[1]->ne[1];
+    g.K = first->src[0]->ne[0];
+    g.N = first->src[0]->ne[1];
+    g.nb01 = first->src[0]->nb[1];
+    g.xcol = first->src[1]->nb[1];
+    g.ycol = first->nb[1];
+    for (int m = 0; m < g.n; m++) {
+        g.m[m].W = members[m]->src[0]->data;
+        g.m[m].X = (const char *) members[m]->src[1]->data;
+        g.m[m].dst = (float *) members[m]->data;
+    }
+    mi_mul_mat_q_fused(g, ctx->stream);
+    ctx->last_launches++;
+    for (ggml_tensor * m : members) invalidate_activations(ctx, m);
+    return last;
+}
+
 static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * cgraph) {
     auto * ctx = (mi_backend_ctx *) backend->context;
     mi_device_guard g(ctx->device);
@@ -450,11 +518,18 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
     ctx->scratch_used = 0;
     ctx->act_cache.clear();
     ctx->last_launches = 0;
+    static const bool no_fuse = getenv("GGML_MI355X_NO_FUSED_MMV") != nullptr;
     for (int i = 0; i < cgraph->n_nodes; i++) {
         ggml_tensor * node = cgraph->nodes[i];
         if (is_noop(node)) continue;
         switch (node->op) {
-            case GGML_OP_MUL_MAT: op_mul_mat(ctx, node); break;
+            case GGML_OP_MUL_MAT:
+                if (!no_fuse && fused_mv_eligible(node)) {
+                    i = run_fused_group(ctx, cgraph, i);
+                    continue;
+                }
+                op_mul_mat(ctx, node);
+                break;
             default:
                 fprintf(stderr, "%s: error: op not supported %s (%s)\n", __func__, node->name, ggml_op_desc(node));
                 MI_ASSERT(!"unsupported op");

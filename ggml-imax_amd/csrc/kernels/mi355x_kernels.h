@@ -47,6 +47,30 @@ void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_
 
 // quantized weights x quantized activations (integer dot products), any number of columns
 void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s);
+
+// Decode-regime mul_mat with the activation quantizer fused in; one launch serves up to
+// kMiMaxMembers independent mul_mats of identical weight type / shape (2-D weights, 2-D f32 src1
+// with 16-byte aligned columns, contiguous f32 dst columns).
+constexpr int kMiMaxMembers = 32;
+struct mi_mmv_member {
+    const void * W;
+    const char * X;
+    float * dst;
+};
+struct mi_mmv_group {
+    int type;
+    int n;                  // members in this launch
+    int ncols;              // src1 columns (ne11), 1..8
+    int blocks_per_member;  // set by the launcher
+    int64_t K, N;
+    size_t nb01;            // weight row stride (bytes)
+    size_t xcol;            // src1 column stride (bytes)
+    size_t ycol;            // dst column stride (bytes)
+    mi_mmv_member m[kMiMaxMembers];
+};
+bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols);
+size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);
+void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s);
 // f16 weights x f16-rounded activations
 void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s);
 // f32 x f32, both operands arbitrarily strided (src1 described by x, src0 by m.nb0x)
