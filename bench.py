@@ -198,12 +198,15 @@ def main():
     value = R * ub * args.steps * world / dt / 1e9
     launches = lib.ggml_backend_mi355x_last_launch_count(backend)
 
-    # dominant kernel: HIP events on the backend stream around whole steps, per launch
+    # dominant kernel: HIP events on the backend's own stream around whole steps. The backend
+    # serves the R independent mul_mats of a step with `launches` kernel launches (1 when the
+    # fused streaming GEMV groups them), so per launch: bytes = R*ub/launches, duration =
+    # step time / launches.
     step_ms = event_time_per_step(torch, wl, stream_ptr)
-    mm_launches = R  # one GEMV launch per mul_mat node
-    per_launch_s = step_ms / 1e3 / max(launches, 1)
-    achieved = ub / (step_ms / 1e3 / mm_launches) / 1e9
-    traffic = load_traffic("mmv")
+    launches = max(launches, 1)
+    bytes_per_launch = R * ub / launches
+    achieved = bytes_per_launch / (step_ms / 1e3 / launches) / 1e9
+    traffic = load_traffic("k_mmv_kq_stream")
 
     result = {
         "metric": "Q4_K 4096x4096 mul_mat GB/s-effective (+ GPT-2 tokens/s), 1 GPU",
@@ -224,8 +227,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel_launches_per_step": launches, "event_ms_per_step": round(step_ms, 4),
-                     "note": "achieved = algorithmic bytes per mul_mat / (HIP-event step time / mul_mats per step); "
-                             "includes activation quantization and inter-kernel gaps"},
+                     "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                     "note": "achieved = algorithmic bytes per launch (R mul_mats x (N*K/256*144 + 4K + 4N) / launches) "
+                             "/ HIP-event duration per launch on the backend stream; activation quantization is inside "
+                             "the kernel; traffic = PMC HBM bytes per launch (tools/pmc_traffic.py, gfx950-corrected)"},
     }
 
     if rank == 0 and world == 1 and not args.no_sweep:

@@ -775,6 +775,18 @@ int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend) {
     return ((mi_backend_ctx *) backend->context)->last_launches;
 }
 
+bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
+    if (strcmp(name, "mmv_blocks") == 0 && value > 0) {
+        g_mi_tuning.mmv_blocks = value;
+        return true;
+    }
+    if (strcmp(name, "mmv_variant") == 0) {
+        g_mi_tuning.mmv_variant = value;
+        return true;
+    }
+    return false;
+}
+
 bool ggml_backend_mi355x_quantize_activations(ggml_backend_t backend, int vec_dot_type, const float * x, int64_t K,
                                               int64_t ncols, int8_t * qs, float * d, int16_t * s32) {
     MI_ASSERT(ggml_backend_is_mi355x(backend));

@@ -51,6 +51,101 @@ __device__ __forceinline__ float mi_wave_max(float v) {
 
 __device__ __forceinline__ int mi_dot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
 
+// ---- DPP wave reductions (gfx9 family: quad_perm, row_half_mirror, row_mirror, row_bcast15/31).
+// The total lands in lane 63 and is broadcast with v_readlane into an SGPR, so the result is
+// wave-uniform. The whole wave must be active (call from wave-uniform control flow).
+#define MI_DPP_QP_1032 0xB1
+#define MI_DPP_QP_2301 0x4E
+#define MI_DPP_ROW_HALF_MIRROR 0x141
+#define MI_DPP_ROW_MIRROR 0x140
+#define MI_DPP_ROW_BCAST15 0x142
+#define MI_DPP_ROW_BCAST31 0x143
+
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ int mi_dpp(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xF, false);
+}
+
+__device__ __forceinline__ float mi_wave_sum_u(float v) {  // uniform result
+    auto f = [](int x) { return __int_as_float(x); };
+    auto i = [](float x) { return __float_as_int(x); };
+    v += f(mi_dpp<MI_DPP_QP_1032>(0, i(v)));
+    v += f(mi_dpp<MI_DPP_QP_2301>(0, i(v)));
+    v += f(mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, i(v)));
+    v += f(mi_dpp<MI_DPP_ROW_MIRROR>(0, i(v)));
+    v += f(mi_dpp<MI_DPP_ROW_BCAST15, 0xA>(0, i(v)));
+    v += f(mi_dpp<MI_DPP_ROW_BCAST31, 0xC>(0, i(v)));
+    return __int_as_float(__builtin_amdgcn_readlane(i(v), 63));
+}
+
+__device__ __forceinline__ uint32_t mi_wave_max_u32_u(uint32_t v) {  // uniform result
+    auto mx = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+    v = mx(v, (uint32_t) mi_dpp<MI_DPP_QP_1032>(0, (int) v));
+    v = mx(v, (uint32_t) mi_dpp<MI_DPP_QP_2301>(0, (int) v));
+    v = mx(v, (uint32_t) mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, (int) v));
+    v = mx(v, (uint32_t) mi_dpp<MI_DPP_ROW_MIRROR>(0, (int) v));
+    v = mx(v, (uint32_t) mi_dpp<MI_DPP_ROW_BCAST15, 0xA>(0, (int) v));
+    v = mx(v, (uint32_t) mi_dpp<MI_DPP_ROW_BCAST31, 0xC>(0, (int) v));
+    return (uint32_t) __builtin_amdgcn_readlane((int) v, 63);
+}
+
+__device__ __forceinline__ uint32_t mi_wave_min_u32_u(uint32_t v) {  // uniform result
+    auto mn = [](uint32_t a, uint32_t b) { return a < b ? a : b; };
+    constexpr int kId = -1;  // 0xFFFFFFFF: identity of unsigned min for lanes DPP leaves untouched
+    v = mn(v, (uint32_t) mi_dpp<MI_DPP_QP_1032>(kId, (int) v));
+    v = mn(v, (uint32_t) mi_dpp<MI_DPP_QP_2301>(kId, (int) v));
+    v = mn(v, (uint32_t) mi_dpp<MI_DPP_ROW_HALF_MIRROR>(kId, (int) v));
+    v = mn(v, (uint32_t) mi_dpp<MI_DPP_ROW_MIRROR>(kId, (int) v));
+    v = mn(v, (uint32_t) mi_dpp<MI_DPP_ROW_BCAST15, 0xA>(kId, (int) v));
+    v = mn(v, (uint32_t) mi_dpp<MI_DPP_ROW_BCAST31, 0xC>(kId, (int) v));
+    return (uint32_t) __builtin_amdgcn_readlane((int) v, 63);
+}
+
+// sum over each aligned group of 8 lanes (every lane of the group gets it)
+__device__ __forceinline__ int mi_sum8(int v) {
+    v += mi_dpp<MI_DPP_QP_1032>(0, v);
+    v += mi_dpp<MI_DPP_QP_2301>(0, v);
+    v += mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, v);
+    return v;
+}
+
+// Q8_K quantization of one 256-superblock held four consecutive floats per lane
+// (quantize_row_q8_K_reference, src/ggml-quants.c:3370-3407, as the reference's gcc -mfma build
+// computes it): the FIRST element of largest |x| keeps its sign, iscale = -127/max,
+// q = min(127, RNE(fma(iscale, x, 1.5*2^23)) via the bit trick), d = 1/iscale.
+// Writes 4 quants per lane (packed dword), the sums of 32 (one per 8-lane group) and d.
+__device__ __forceinline__ void mi_q8K_superblock(const float (&v)[4], int lane, uint32_t & packed, int & sum32, float & d) {
+    float best = 0.0f;
+    int bidx = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float ax = fabsf(v[i]);
+        if (ax > best) { best = ax; bidx = i; }  // first occurrence within the lane
+    }
+    const uint32_t amax_bits = mi_wave_max_u32_u(__float_as_uint(best));  // |x| >= 0: bit order = value order
+    packed = 0;
+    sum32 = 0;
+    d = 0.0f;
+    if (amax_bits == 0) return;  // wave-uniform
+    const uint32_t my_idx = __float_as_uint(best) == amax_bits ? (uint32_t) (lane * 4 + bidx) : 0xFFFFFFFFu;
+    const uint32_t idx = mi_wave_min_u32_u(my_idx);
+    const int owner = (int) (idx >> 2), sel = (int) (idx & 3);
+    const float mine = sel == 0 ? v[0] : sel == 1 ? v[1] : sel == 2 ? v[2] : v[3];
+    const float vmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), owner));
+    const float iscale = -127.f / vmax;
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float t = __builtin_fmaf(iscale, v[i], 12582912.f);
+        int q = (__float_as_int(t) & 0x007fffff) - 0x00400000;
+        q = q < 127 ? q : 127;
+        s += q;
+        packed |= ((uint32_t) (q & 0xFF)) << (8 * i);
+    }
+    sum32 = mi_sum8(s);
+    d = 1.0f / iscale;
+}
+
 // 6-bit scale / min j of the 12-byte K-quant scale array (src/ggml-quants.c:1357-1364),
 // taking the array as three little-endian dwords.
 __device__ __forceinline__ void mi_scale_min_k4(int j, uint32_t s0, uint32_t s1, uint32_t s2, int & sc, int & m) {

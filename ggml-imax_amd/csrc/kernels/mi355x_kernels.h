@@ -62,6 +62,7 @@ struct mi_mmv_group {
     int n;                  // members in this launch
     int ncols;              // src1 columns (ne11), 1..8
     int blocks_per_member;  // set by the launcher
+    int64_t rows_per_block; // set by the launcher
     int64_t K, N;
     size_t nb01;            // weight row stride (bytes)
     size_t xcol;            // src1 column stride (bytes)
@@ -69,6 +70,13 @@ struct mi_mmv_group {
     mi_mmv_member m[kMiMaxMembers];
 };
 bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols);
+
+// launch-shape knobs of the streaming kernels (defaults tuned on MI355X; settable for A/B runs)
+struct mi_tuning {
+    int mmv_blocks;   // target resident workgroups for the fused GEMV (all members)
+    int mmv_variant;  // 10*prefetch_depth + {0: activations in VGPRs, 1: from LDS, 2: LDS + waves/EU cap}
+};
+extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);
 void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s);
 // f16 weights x f16-rounded activations

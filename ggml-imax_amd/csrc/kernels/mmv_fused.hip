@@ -1,74 +1,51 @@
 // mmv_fused.hip -- decode-regime GGML_OP_MUL_MAT with the activation quantizer fused in, and
-// several independent mul_mat nodes of one graph served by a single launch.
+// several independent mul_mat nodes of one graph served by a single streaming launch.
 //
-// Per workgroup (256 threads = 4 wave64s, RPW weight rows per wave):
-//   1. every lane issues its weight loads for the first K-item of each of its RPW rows
-//      (aligned 16-byte global loads straight to VGPRs; nothing else is waited on yet),
-//   2. the workgroup quantizes the NC f32 activation columns of its group member into LDS with
-//      the reference's exact Q8_K rounding (see quantize.hip) -- X is a few KB, L2-resident,
-//   3. barrier, then integer dot products (v_dot4_i32_i8) of the prefetched weights against the
-//      LDS activations; activations are read from LDS once per lane and reused for RPW rows.
-// A launch covers up to kMaxMembers independent mul_mats with the same weight type and shape
-// (blockIdx.x -> member, row block), so a decode graph's independent projections stream their
-// weights back to back without launch gaps.
+// Structure (HBM-bound weight stream; MI355X_MICROARCH.md: 8 TB/s, ~6.3 TB/s achievable):
+//   * grid = ~4 workgroups per CU; each workgroup owns a contiguous row range of ONE group
+//     member (blockIdx.x -> member, row range), so the activation quantization below is paid
+//     once per ~16-128 rows instead of once per row;
+//   * per workgroup: issue the weight loads of the first row chunk (aligned 16-byte global loads
+//     straight to VGPRs), quantize the member's NC f32 activation columns into LDS with the
+//     reference's exact Q8_K rounding (quantize.hip), barrier;
+//   * then each wave streams its chunks of RPW rows with one chunk of loads always in flight
+//     (prefetch chunk k+1, then v_dot4_i32_i8 on chunk k); for K <= 4096 a lane's K-item is the
+//     same for every row, so its activation slice is read from LDS once and kept in VGPRs.
+// One K-item = (superblock s, 64-element group j): 16 B header + 32 B nibbles (+ 32 B qh for
+// Q5_K), so a K=4096 Q4_K row is exactly one item per lane, three 16-byte loads.
 //
-// Numerics are identical to mmv.hip (bit-exact activation quants, exact per-superblock int
-// sums, f32 combination); reference dot products: ggml_vec_dot_q4_K_q8_K
-// (src/ggml-quants.c:7007-7502), ggml_vec_dot_q5_K_q8_K (:7833-8378).
+// Numerics: bit-exact activation quants, exact per-item integer sums, f32 combination per
+// superblock, i.e. ggml_vec_dot_q4_K_q8_K (src/ggml-quants.c:7007-7502) /
+// ggml_vec_dot_q5_K_q8_K (:7833-8378) up to f32 summation order.
 
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
 
+#include <stdlib.h>
+
 namespace {
 
-// Q8_K quantization of one 256-superblock from registers (four floats per lane) into LDS.
-// Same rounding sequence as k_quantize_q8_K / quantize_row_q8_K_reference.
+// Q8_K quantization of one 256-superblock (four floats per lane) into LDS; rounding identical
+// to k_quantize_q8_K / quantize_row_q8_K_reference (mi_q8K_superblock).
 __device__ __forceinline__ void quantize_sb_to_lds(float4 v4, int lane, int8_t * qs, float * d, int16_t * s32) {
     const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-    float amax = 0.0f, vmax = 0.0f;
-    int idx = 0x7fffffff;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const float ax = fabsf(v[i]);
-        if (ax > amax) { amax = ax; vmax = v[i]; idx = lane * 4 + i; }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float oa = __shfl_xor(amax, off, 64);
-        const float ov = __shfl_xor(vmax, off, 64);
-        const int oi = __shfl_xor(idx, off, 64);
-        if (oa > amax || (oa == amax && oi < idx)) { amax = oa; vmax = ov; idx = oi; }
-    }
-    uint32_t packed = 0;
-    int sum = 0;
-    float dd = 0.0f;
-    if (amax != 0.0f) {
-        const float iscale = -127.f / vmax;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const float t = __builtin_fmaf(iscale, v[i], 12582912.f);
-            int q = (__float_as_int(t) & 0x007fffff) - 0x00400000;
-            q = q < 127 ? q : 127;
-            sum += q;
-            packed |= ((uint32_t) (q & 0xFF)) << (8 * i);
-        }
-        dd = 1.0f / iscale;
-    }
+    uint32_t packed;
+    int sum32;
+    float dd;
+    mi_q8K_superblock(v, lane, packed, sum32, dd);
     *(uint32_t *) (qs + lane * 4) = packed;
-    sum += __shfl_xor(sum, 1, 64);
-    sum += __shfl_xor(sum, 2, 64);
-    sum += __shfl_xor(sum, 4, 64);
-    if ((lane & 7) == 0) s32[lane >> 3] = (int16_t) sum;
+    if ((lane & 7) == 0) s32[lane >> 3] = (int16_t) sum32;
     if (lane == 0) *d = dd;
 }
 
+template <bool Q5>
 struct kq_regs {
-    uint4 hdr, qa, qb, ha, hb;
+    uint4 hdr, qa, qb;
+    uint4 ha, hb;  // Q5 only (dead for Q4)
 };
 
 template <bool Q5>
-__device__ __forceinline__ kq_regs kq_load(const uint8_t * blk, int j) {
-    kq_regs r;
+__device__ __forceinline__ void kq_load(kq_regs<Q5> & r, const uint8_t * blk, int j) {
     r.hdr = *(const uint4 *) blk;
     const uint8_t * qp = blk + (Q5 ? 48 : 16) + 32 * j;
     r.qa = *(const uint4 *) qp;
@@ -77,13 +54,33 @@ __device__ __forceinline__ kq_regs kq_load(const uint8_t * blk, int j) {
         r.ha = *(const uint4 *) (blk + 16);
         r.hb = *(const uint4 *) (blk + 32);
     }
-    return r;
 }
 
-// One K-item (superblock s, 64-element group j) of one row against NC LDS columns.
+// activation slice of one K-item for one column: 64 int8 (32 pair with low nibbles, 32 with
+// high), the superblock scale and the two sums of 32 the item's sub-blocks need
+struct act_item {
+    int lo[8], hi[8];
+    float d;
+    int s0, s1;
+};
+
+__device__ __forceinline__ void act_load(act_item & a, const int8_t * lqs, const float * ld, const int16_t * ls32,
+                                         int64_t K, int c, int s, int j) {
+    const int4 * p = (const int4 *) (lqs + c * K + (int64_t) s * 256 + 64 * j);
+    const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+    a.lo[0] = a0.x; a.lo[1] = a0.y; a.lo[2] = a0.z; a.lo[3] = a0.w;
+    a.lo[4] = a1.x; a.lo[5] = a1.y; a.lo[6] = a1.z; a.lo[7] = a1.w;
+    a.hi[0] = a2.x; a.hi[1] = a2.y; a.hi[2] = a2.z; a.hi[3] = a2.w;
+    a.hi[4] = a3.x; a.hi[5] = a3.y; a.hi[6] = a3.z; a.hi[7] = a3.w;
+    a.d = ld[c * (K / 256) + s];
+    const int ss = *(const int *) (ls32 + c * (K / 32) + s * 8 + 2 * j);
+    a.s0 = (int) (int16_t) (ss & 0xFFFF);
+    a.s1 = ss >> 16;
+}
+
+// contribution of one K-item of one weight row to NC columns
 template <int NC, bool Q5>
-__device__ __forceinline__ void kq_item(const kq_regs & r, int s, int j, int ncols, const int8_t * lqs, const float * ld,
-                                        const int16_t * ls32, int64_t K, float (&acc)[NC]) {
+__device__ __forceinline__ void kq_dot(const kq_regs<Q5> & r, int j, const act_item (&a)[NC], int ncols, float (&acc)[NC]) {
     const uint32_t q[8] = {r.qa.x, r.qa.y, r.qa.z, r.qa.w, r.qb.x, r.qb.y, r.qb.z, r.qb.w};
     uint32_t qlo[8], qhi[8];
     if constexpr (Q5) {
@@ -108,29 +105,70 @@ __device__ __forceinline__ void kq_item(const kq_regs & r, int s, int j, int nco
 #pragma unroll
     for (int c = 0; c < NC; c++) {
         if (NC > 1 && c >= ncols) break;
-        const int4 * a = (const int4 *) (lqs + c * K + (int64_t) s * 256 + 64 * j);
-        const int4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
-        const int alo[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const int ahi[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
         int lo = 0, hi = 0;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            lo = mi_dot4((int) qlo[i], alo[i], lo);
-            hi = mi_dot4((int) qhi[i], ahi[i], hi);
+            lo = mi_dot4((int) qlo[i], a[c].lo[i], lo);
+            hi = mi_dot4((int) qhi[i], a[c].hi[i], hi);
         }
         const int sumi = sc0 * lo + sc1 * hi;
-        const int ss = *(const int *) (ls32 + c * (K / 32) + s * 8 + 2 * j);
-        const int summ = m0 * (int) (int16_t) (ss & 0xFFFF) + m1 * (ss >> 16);
-        const float dy = ld[c * (K / 256) + s];
-        acc[c] += dy * (dw * (float) sumi - dmw * (float) summ);
+        const int summ = m0 * a[c].s0 + m1 * a[c].s1;
+        acc[c] += a[c].d * (dw * (float) sumi - dmw * (float) summ);
     }
 }
 
-template <int NC, bool Q5, int RPW>
-__global__ __launch_bounds__(256) void k_mmv_kq_fused(mi_mmv_group g) {
+// One weight row of the stream: dot products of its K-items against the LDS / VGPR activations,
+// wave reduction, store.
+template <int NC, bool Q5, bool KEEP>
+__device__ __forceinline__ void kq_row(const kq_regs<Q5> & first, const uint8_t * wrow, int64_t row, const mi_mmv_group & g,
+                                       bool have_first, bool single_item, int s0, int j0, int lane, int nitems, int ncols,
+                                       const act_item (&a0)[KEEP ? NC : 1], const int8_t * lqs, const float * ld,
+                                       const int16_t * ls32, float * dst) {
+    constexpr int BS = Q5 ? 176 : 144;
+    const int64_t K = g.K;
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) acc[c] = 0.0f;
+    if (have_first) {
+        if constexpr (KEEP) {
+            if (single_item) kq_dot<NC, Q5>(first, j0, *(const act_item(*)[NC]) a0, ncols, acc);
+        }
+        if (!KEEP || !single_item) {
+            act_item a[NC];
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                if (NC > 1 && c >= ncols) break;
+                act_load(a[c], lqs, ld, ls32, K, c, s0, j0);
+            }
+            kq_dot<NC, Q5>(first, j0, a, ncols, acc);
+        }
+    }
+    for (int it = lane + 64; it < nitems; it += 64) {
+        const int s = it >> 2, j = it & 3;
+        kq_regs<Q5> rr;
+        kq_load<Q5>(rr, wrow + (size_t) s * BS, j);
+        act_item a[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            act_load(a[c], lqs, ld, ls32, K, c, s, j);
+        }
+        kq_dot<NC, Q5>(rr, j, a, ncols, acc);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const float v = mi_wave_sum_u(acc[c]);
+        if (lane == 0 && c < ncols) *(float *) ((char *) dst + c * g.ycol + row * sizeof(float)) = v;
+    }
+}
+
+// PD = rows of weight loads a wave keeps in flight ahead of the row it is computing.
+template <int NC, bool Q5, int PD, bool KEEP_ACT, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_mmv_kq_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int BS = Q5 ? 176 : 144;
-    const int wave = threadIdx.x >> 6;
+    constexpr int NB = PD + 1;  // ring slots
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int member = blockIdx.x / g.blocks_per_member;
     const int rb = blockIdx.x - member * g.blocks_per_member;
@@ -146,70 +184,108 @@ __global__ __launch_bounds__(256) void k_mmv_kq_fused(mi_mmv_group g) {
     float * ld = (float *) (lds + NC * K);
     int16_t * ls32 = (int16_t *) (lds + NC * K + NC * (K / 256) * 4);
 
-    const int64_t row0 = ((int64_t) rb * 4 + wave) * RPW;
+    const int64_t row_begin = (int64_t) rb * g.rows_per_block;
+    const int64_t row_end = row_begin + g.rows_per_block < g.N ? row_begin + g.rows_per_block : g.N;
+    // wave w streams rows row_begin + w, row_begin + w + 4, ...
+    const int64_t nrows = row_end - row_begin > wave ? (row_end - row_begin - wave + 3) / 4 : 0;
 
-    // 1) weight prefetch for the first K-item of every row of this wave
-    kq_regs pre[RPW];
+    const bool single_item = nitems <= 64;
     const bool have_first = lane < nitems;
     const int s0 = lane >> 2, j0 = lane & 3;
+    const size_t item_off = (size_t) s0 * BS;
+    auto wrow_of = [&](int64_t k) { return W + (row_begin + 4 * k + wave) * g.nb01; };
+
+    // 1) the first PD rows' weights in flight
+    kq_regs<Q5> ring[NB];
 #pragma unroll
-    for (int r = 0; r < RPW; r++) {
-        const int64_t row = row0 + r;
-        if (have_first && row < g.N) pre[r] = kq_load<Q5>(W + row * g.nb01 + (size_t) s0 * BS, j0);
+    for (int u = 0; u < PD; u++) {
+        if (have_first && u < nrows) kq_load<Q5>(ring[u], wrow_of(u) + item_off, j0);
     }
 
-    // 2) quantize X (NC columns) into LDS: wave w takes superblocks w, w+4, ...
-    for (int p = wave; p < nsb * ncols; p += 4) {
-        const int c = p / nsb, s = p - c * nsb;
-        const float4 v4 = *(const float4 *) (X + c * g.xcol + ((size_t) s * 256 + lane * 4) * sizeof(float));
-        quantize_sb_to_lds(v4, lane, lqs + c * K + s * 256, ld + c * nsb + s, ls32 + c * (K / 32) + s * 8);
+    // 2) quantize the member's activation columns into LDS (wave w: superblocks w, w+4, ...)
+    {
+        const int total = nsb * ncols;
+        for (int p0 = wave; p0 < total; p0 += 16) {
+            // unconditional loads (clamped index): a predicated load makes hipcc wait vmcnt(0)
+            // per element instead of once for the batch
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = min(p0 + 4 * u, total - 1);
+                const int c = p / nsb, sb = p - c * nsb;
+                v[u] = *(const float4 *) (X + c * g.xcol + ((size_t) sb * 256 + lane * 4) * sizeof(float));
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = p0 + 4 * u;
+                if (p < total) {
+                    const int c = p / nsb, sb = p - c * nsb;
+                    quantize_sb_to_lds(v[u], lane, lqs + c * K + sb * 256, ld + c * nsb + sb, ls32 + c * (K / 32) + sb * 8);
+                }
+            }
+        }
     }
     __syncthreads();
 
-    // 3) dot products
-#pragma unroll
-    for (int r = 0; r < RPW; r++) {
-        const int64_t row = row0 + r;
-        if (row >= g.N) break;  // wave-uniform
-        float acc[NC];
-#pragma unroll
-        for (int c = 0; c < NC; c++) acc[c] = 0.0f;
-        if (have_first) kq_item<NC, Q5>(pre[r], s0, j0, ncols, lqs, ld, ls32, K, acc);
-        for (int it = lane + 64; it < nitems; it += 64) {
-            const int s = it >> 2, j = it & 3;
-            const kq_regs rr = kq_load<Q5>(W + row * g.nb01 + (size_t) s * BS, j);
-            kq_item<NC, Q5>(rr, s, j, ncols, lqs, ld, ls32, K, acc);
-        }
+    // few columns: the lane's activation slice may live in VGPRs for the whole stream
+    constexpr bool KEEP = KEEP_ACT && NC <= 2;
+    act_item a0[KEEP ? NC : 1];
+    if (KEEP && single_item && have_first) {
 #pragma unroll
         for (int c = 0; c < NC; c++) {
-            const float v = mi_wave_sum(acc[c]);
-            if (lane == 0 && c < ncols) *(float *) ((char *) dst + c * g.ycol + row * sizeof(float)) = v;
+            if (NC > 1 && c >= ncols) break;
+            act_load(a0[c], lqs, ld, ls32, K, c, s0, j0);
+        }
+    }
+
+    // 3) stream: ring slot u holds row k0+u; refill it with row k0+u+PD right before using it
+    for (int64_t k0 = 0; k0 < nrows; k0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; u++) {
+            const int64_t k = k0 + u;
+            if (k >= nrows) break;  // wave-uniform
+            if (have_first && k + PD < nrows) kq_load<Q5>(ring[(u + PD) % NB], wrow_of(k + PD) + item_off, j0);
+            kq_row<NC, Q5, KEEP>(ring[u], wrow_of(k), row_begin + 4 * k + wave, g, have_first, single_item, s0, j0, lane,
+                                 nitems, ncols, a0, lqs, ld, ls32, dst);
         }
     }
 }
 
 template <int NC, bool Q5>
-void launch_kq(const mi_mmv_group & g, int rpw, hipStream_t s) {
+void launch_kq(const mi_mmv_group & g, int pd, hipStream_t s) {
     const size_t lds = (size_t) NC * (g.K + (g.K / 256) * 4 + (g.K / 32) * 2);
     const dim3 grid((unsigned) (g.blocks_per_member * g.n));
-    switch (rpw) {
-        case 1: hipLaunchKernelGGL((k_mmv_kq_fused<NC, Q5, 1>), grid, dim3(256), lds, s, g); break;
-        case 2: hipLaunchKernelGGL((k_mmv_kq_fused<NC, Q5, 2>), grid, dim3(256), lds, s, g); break;
-        default: hipLaunchKernelGGL((k_mmv_kq_fused<NC, Q5, 4>), grid, dim3(256), lds, s, g); break;
+    // variant codes (tuning): 10*PD + v, v: 0 = act in VGPRs, 1 = act from LDS, 2 = LDS + 5 waves/EU
+    switch (pd) {
+        case 10: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 1, true, 1>), grid, dim3(256), lds, s, g); break;
+        case 11: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 1, false, 1>), grid, dim3(256), lds, s, g); break;
+        case 12: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 1, false, 5>), grid, dim3(256), lds, s, g); break;
+        case 20: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 2, true, 1>), grid, dim3(256), lds, s, g); break;
+        case 21: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 2, false, 1>), grid, dim3(256), lds, s, g); break;
+        case 22: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 2, false, 4>), grid, dim3(256), lds, s, g); break;
+        case 31: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 3, false, 1>), grid, dim3(256), lds, s, g); break;
+        case 32: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 3, false, 4>), grid, dim3(256), lds, s, g); break;
+        case 41: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 4, false, 1>), grid, dim3(256), lds, s, g); break;
+        default: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 1, true, 1>), grid, dim3(256), lds, s, g); break;
     }
 }
 
 template <bool Q5>
-void launch_kq_nc(const mi_mmv_group & g, int rpw, hipStream_t s) {
+void launch_kq_nc(const mi_mmv_group & g, int pd, hipStream_t s) {
     switch (g.ncols) {
-        case 1: launch_kq<1, Q5>(g, rpw, s); break;
-        case 2: launch_kq<2, Q5>(g, rpw, s); break;
-        case 3: case 4: launch_kq<4, Q5>(g, rpw, s); break;
-        default: launch_kq<8, Q5>(g, rpw, s); break;
+        case 1: launch_kq<1, Q5>(g, pd, s); break;
+        case 2: launch_kq<2, Q5>(g, pd, s); break;
+        case 3: case 4: launch_kq<4, Q5>(g, pd, s); break;
+        default: launch_kq<8, Q5>(g, pd, s); break;
     }
 }
 
 } // namespace
+
+static int env_int(const char * name, int def) {
+    const char * v = getenv(name);
+    return v ? atoi(v) : def;
+}
 
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols) {
     const int64_t nc = ncols <= 2 ? ncols : (ncols <= 4 ? 4 : 8);
@@ -223,14 +299,18 @@ bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols) {
     return mi_mmv_fused_lds_bytes(type, K, ncols) <= 64 * 1024;
 }
 
+mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 1024), env_int("GGML_MI355X_MMV_VARIANT", 21)};
+
 void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s) {
-    // rows per wave: amortize the per-workgroup activation quantization when there is enough
-    // work to fill the chip (256 CUs x 4+ workgroups), otherwise maximize parallelism
-    const int64_t total_rows = g.N * g.n;
-    int rpw = 1;
-    if (total_rows >= 256 * 16 * 4) rpw = 4;
-    else if (total_rows >= 256 * 16 * 2) rpw = 2;
-    g.blocks_per_member = (int) ((g.N + 4 * rpw - 1) / (4 * rpw));
-    if (g.type == 12) launch_kq_nc<false>(g, rpw, s);
-    else launch_kq_nc<true>(g, rpw, s);
+    // ~4 resident workgroups per CU over all members; each workgroup streams a row range
+    const int target_blocks = g_mi_tuning.mmv_blocks;
+    const int variant = g_mi_tuning.mmv_variant;
+    int bpm = target_blocks / g.n;
+    if (bpm < 1) bpm = 1;
+    int64_t rows = (g.N + bpm - 1) / bpm;
+    rows = (rows + 3) / 4 * 4;
+    g.rows_per_block = rows;
+    g.blocks_per_member = (int) ((g.N + rows - 1) / rows);
+    if (g.type == 12) launch_kq_nc<false>(g, variant, s);
+    else launch_kq_nc<true>(g, variant, s);
 }

@@ -161,6 +161,7 @@ _SIGS = {
     "ggml_backend_mi355x_get_stream": ([c_void_p], c_void_p),
     "ggml_backend_mi355x_set_graph_capture": ([c_void_p, c_bool], None),
     "ggml_backend_mi355x_last_launch_count": ([c_void_p], c_int),
+    "ggml_backend_mi355x_set_tuning": ([c_char_p, c_int], c_bool),
     "ggml_backend_mi355x_quantize_activations": ([c_void_p, c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p], c_bool),
 }
 

@@ -57,6 +57,11 @@ GGML_API void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool
 // Number of kernels launched by the last graph_compute (for tests / profiling).
 GGML_API int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend);
 
+// Launch-shape knobs of the streaming kernels, for A/B tuning inside one process:
+// "mmv_blocks" (resident workgroups of the fused GEMV), "mmv_variant" (see mi355x_kernels.h).
+// Returns false for an unknown name.
+GGML_API bool ggml_backend_mi355x_set_tuning(const char * name, int value);
+
 // Runs the device activation quantizer that GGML_OP_MUL_MAT uses for `vec_dot_type`
 // (GGML_TYPE_Q8_0 or GGML_TYPE_Q8_K) on ncols host columns of K floats and returns its
 // structure-of-arrays result: qs [ncols*K], d [ncols*K/QK], s32 [ncols*K/32] (Q8_K only,
