@@ -63,8 +63,9 @@ def main():
         }
     res = {"bench_args": bench_args, "kernels": kernels}
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
-    path = os.path.join(REPO, "profiles", f"{a.tag}_pmc_traffic.json")
-    json.dump(res, open(path, "w"), indent=1)
+    for d in ("profiles", "gpurun_out"):  # gpurun_out/ is what a GPU-box run hands back
+        os.makedirs(os.path.join(REPO, d), exist_ok=True)
+        json.dump(res, open(os.path.join(REPO, d, f"{a.tag}_pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
