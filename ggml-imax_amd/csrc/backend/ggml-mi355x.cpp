@@ -776,7 +776,7 @@ int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend) {
 }
 
 bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
-    if (strcmp(name, "mmv_blocks") == 0 && value > 0) {
+    if (strcmp(name, "mmv_blocks") == 0 && value >= 0) {
         g_mi_tuning.mmv_blocks = value;
         return true;
     }

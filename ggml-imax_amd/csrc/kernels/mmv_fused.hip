@@ -2,171 +2,232 @@
 // several independent mul_mat nodes of one graph served by a single streaming launch.
 //
 // Structure (HBM-bound weight stream; MI355X_MICROARCH.md: 8 TB/s, ~6.3 TB/s achievable):
-//   * grid = ~4 workgroups per CU; each workgroup owns a contiguous row range of ONE group
-//     member (blockIdx.x -> member, row range), so the activation quantization below is paid
-//     once per ~16-128 rows instead of once per row;
-//   * per workgroup: issue the weight loads of the first row chunk (aligned 16-byte global loads
-//     straight to VGPRs), quantize the member's NC f32 activation columns into LDS with the
-//     reference's exact Q8_K rounding (quantize.hip), barrier;
-//   * then each wave streams its chunks of RPW rows with one chunk of loads always in flight
-//     (prefetch chunk k+1, then v_dot4_i32_i8 on chunk k); for K <= 4096 a lane's K-item is the
-//     same for every row, so its activation slice is read from LDS once and kept in VGPRs.
-// One K-item = (superblock s, 64-element group j): 16 B header + 32 B nibbles (+ 32 B qh for
-// Q5_K), so a K=4096 Q4_K row is exactly one item per lane, three 16-byte loads.
+//   * grid = ~4 workgroups per CU (all resident); each workgroup owns a contiguous row range of
+//     ONE group member (blockIdx.x -> member, row range), so the activation quantization is paid
+//     once per workgroup, not per row;
+//   * prologue: issue the weight loads of the first rows (global loads straight to VGPRs), then
+//     quantize the member's NC f32 activation columns into LDS with the reference's exact
+//     rounding (Q8_K for Q4_K/Q5_K, AVX2-path Q8_0 for Q4_0/Q8_0), barrier;
+//   * stream: wave w walks rows w, w+4, ... keeping PD rows of loads in flight in a register ring
+//     ahead of the row being computed; v_dot4_i32_i8 against the LDS activations; DPP wave
+//     reduction; one store per row.
+// A lane's K-items are the same for every row: item = lane + 64*i. Items:
+//   Q4_K / Q5_K: (superblock s, 64-element group j): 16 B header + 32 B nibbles (+32 B qh),
+//                aligned dwordx4 loads; a K=4096 row is one item per lane.
+//   Q4_0 / Q8_0: one 32-element block (18 / 34 B, only 2-byte aligned): aligned dword loads
+//                re-aligned with v_alignbyte; a K=4096 row is two items per lane.
 //
-// Numerics: bit-exact activation quants, exact per-item integer sums, f32 combination per
-// superblock, i.e. ggml_vec_dot_q4_K_q8_K (src/ggml-quants.c:7007-7502) /
-// ggml_vec_dot_q5_K_q8_K (:7833-8378) up to f32 summation order.
+// Numerics: bit-exact activation quants, exact integer sums per item, f32 combination, i.e.
+// ggml_vec_dot_q4_K_q8_K (src/ggml-quants.c:7007-7502), ggml_vec_dot_q5_K_q8_K (:7833-8378),
+// ggml_vec_dot_q4_0_q8_0 (:3469-3874), ggml_vec_dot_q8_0_q8_0 (:4819+) up to summation order.
 
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
 
 #include <stdlib.h>
 
+static int env_int(const char * name, int def) {
+    const char * v = getenv(name);
+    return v ? atoi(v) : def;
+}
+
+// mmv_blocks == 0: size the grid from the kernel's residency (hipOccupancy...) per instance
+mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 0), env_int("GGML_MI355X_MMV_VARIANT", 0)};
+
 namespace {
 
-// Q8_K quantization of one 256-superblock (four floats per lane) into LDS; rounding identical
-// to k_quantize_q8_K / quantize_row_q8_K_reference (mi_q8K_superblock).
-__device__ __forceinline__ void quantize_sb_to_lds(float4 v4, int lane, int8_t * qs, float * d, int16_t * s32) {
+// ------------------------------------------------------------------ activations in LDS
+// layout per member: qs [NC][K] int8 | d [NC][K/QKA] f32 | s32 [NC][K/32] int16
+
+struct lds_act {
+    int8_t * qs;
+    float * d;
+    int16_t * s32;
+};
+
+template <int QKA>
+__device__ __forceinline__ lds_act lds_carve(uint8_t * lds, int NC, int64_t K) {
+    lds_act a;
+    a.qs = (int8_t *) lds;
+    a.d = (float *) (lds + NC * K);
+    a.s32 = (int16_t *) (lds + NC * K + NC * (K / QKA) * 4);
+    return a;
+}
+
+template <int QKA>
+__host__ __device__ constexpr size_t lds_bytes(int NC, int64_t K) {
+    return (size_t) NC * (K + (K / QKA) * 4 + (K / 32) * 2);
+}
+
+// one 256-element slice (four floats per lane) of column c into LDS
+template <int QKA>
+__device__ __forceinline__ void quantize_slice(float4 v4, int lane, const lds_act & a, int64_t K, int c, int sl) {
     const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-    uint32_t packed;
-    int sum32;
-    float dd;
-    mi_q8K_superblock(v, lane, packed, sum32, dd);
-    *(uint32_t *) (qs + lane * 4) = packed;
-    if ((lane & 7) == 0) s32[lane >> 3] = (int16_t) sum32;
-    if (lane == 0) *d = dd;
-}
-
-template <bool Q5>
-struct kq_regs {
-    uint4 hdr, qa, qb;
-    uint4 ha, hb;  // Q5 only (dead for Q4)
-};
-
-template <bool Q5>
-__device__ __forceinline__ void kq_load(kq_regs<Q5> & r, const uint8_t * blk, int j) {
-    r.hdr = *(const uint4 *) blk;
-    const uint8_t * qp = blk + (Q5 ? 48 : 16) + 32 * j;
-    r.qa = *(const uint4 *) qp;
-    r.qb = *(const uint4 *) (qp + 16);
-    if constexpr (Q5) {
-        r.ha = *(const uint4 *) (blk + 16);
-        r.hb = *(const uint4 *) (blk + 32);
-    }
-}
-
-// activation slice of one K-item for one column: 64 int8 (32 pair with low nibbles, 32 with
-// high), the superblock scale and the two sums of 32 the item's sub-blocks need
-struct act_item {
-    int lo[8], hi[8];
-    float d;
-    int s0, s1;
-};
-
-__device__ __forceinline__ void act_load(act_item & a, const int8_t * lqs, const float * ld, const int16_t * ls32,
-                                         int64_t K, int c, int s, int j) {
-    const int4 * p = (const int4 *) (lqs + c * K + (int64_t) s * 256 + 64 * j);
-    const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-    a.lo[0] = a0.x; a.lo[1] = a0.y; a.lo[2] = a0.z; a.lo[3] = a0.w;
-    a.lo[4] = a1.x; a.lo[5] = a1.y; a.lo[6] = a1.z; a.lo[7] = a1.w;
-    a.hi[0] = a2.x; a.hi[1] = a2.y; a.hi[2] = a2.z; a.hi[3] = a2.w;
-    a.hi[4] = a3.x; a.hi[5] = a3.y; a.hi[6] = a3.z; a.hi[7] = a3.w;
-    a.d = ld[c * (K / 256) + s];
-    const int ss = *(const int *) (ls32 + c * (K / 32) + s * 8 + 2 * j);
-    a.s0 = (int) (int16_t) (ss & 0xFFFF);
-    a.s1 = ss >> 16;
-}
-
-// contribution of one K-item of one weight row to NC columns
-template <int NC, bool Q5>
-__device__ __forceinline__ void kq_dot(const kq_regs<Q5> & r, int j, const act_item (&a)[NC], int ncols, float (&acc)[NC]) {
-    const uint32_t q[8] = {r.qa.x, r.qa.y, r.qa.z, r.qa.w, r.qb.x, r.qb.y, r.qb.z, r.qb.w};
-    uint32_t qlo[8], qhi[8];
-    if constexpr (Q5) {
-        const uint32_t h[8] = {r.ha.x, r.ha.y, r.ha.z, r.ha.w, r.hb.x, r.hb.y, r.hb.z, r.hb.w};
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            qlo[i] = (q[i] & 0x0F0F0F0Fu) | (((h[i] >> (2 * j)) & 0x01010101u) << 4);
-            qhi[i] = ((q[i] >> 4) & 0x0F0F0F0Fu) | (((h[i] >> (2 * j + 1)) & 0x01010101u) << 4);
-        }
+    int8_t * qs = a.qs + c * K + sl * 256;
+    if constexpr (QKA == 256) {
+        // Q8_K (quantize_row_q8_K_reference as the reference's gcc -mfma build rounds it)
+        uint32_t packed;
+        int sum32;
+        float dd;
+        mi_q8K_superblock(v, lane, packed, sum32, dd);
+        *(uint32_t *) (qs + lane * 4) = packed;
+        if ((lane & 7) == 0) a.s32[c * (K / 32) + sl * 8 + (lane >> 3)] = (int16_t) sum32;
+        if (lane == 0) a.d[c * (K / 256) + sl] = dd;
     } else {
+        // Q8_0, AVX2 branch of quantize_row_q8_0 (src/ggml-quants.c:535-618): per 32-block
+        // amax, d = amax/127 -> fp16 (RNE), id = 127/amax, q = round-half-even(x*id).
+        // 8 lanes hold one block; max over the 8-lane group with DPP.
+        float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+        uint32_t ab = __float_as_uint(am);
+        ab = max(ab, (uint32_t) mi_dpp<MI_DPP_QP_1032>(0, (int) ab));
+        ab = max(ab, (uint32_t) mi_dpp<MI_DPP_QP_2301>(0, (int) ab));
+        ab = max(ab, (uint32_t) mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, (int) ab));
+        const float amax = __uint_as_float(ab);
+        const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+        uint32_t packed = 0;
+        int s = 0;
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            qlo[i] = q[i] & 0x0F0F0F0Fu;
-            qhi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
+        for (int i = 0; i < 4; i++) {
+            const int q = (int) __builtin_rintf(__fmul_rn(v[i], id));
+            s += q;
+            packed |= ((uint32_t) (q & 0xFF)) << (8 * i);
         }
-    }
-    const float dw = mi_h2f((uint16_t) (r.hdr.x & 0xFFFF));
-    const float dmw = mi_h2f((uint16_t) (r.hdr.x >> 16));
-    int sc0, m0, sc1, m1;
-    mi_scale_min_k4(2 * j, r.hdr.y, r.hdr.z, r.hdr.w, sc0, m0);
-    mi_scale_min_k4(2 * j + 1, r.hdr.y, r.hdr.z, r.hdr.w, sc1, m1);
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-        if (NC > 1 && c >= ncols) break;
-        int lo = 0, hi = 0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            lo = mi_dot4((int) qlo[i], a[c].lo[i], lo);
-            hi = mi_dot4((int) qhi[i], a[c].hi[i], hi);
+        s = mi_sum8(s);
+        *(uint32_t *) (qs + lane * 4) = packed;
+        if ((lane & 7) == 0) {
+            const int blk = sl * 8 + (lane >> 3);
+            a.d[c * (K / 32) + blk] = mi_h2f(mi_f2h(amax / 127.f));
+            a.s32[c * (K / 32) + blk] = (int16_t) s;
         }
-        const int sumi = sc0 * lo + sc1 * hi;
-        const int summ = m0 * a[c].s0 + m1 * a[c].s1;
-        acc[c] += a[c].d * (dw * (float) sumi - dmw * (float) summ);
     }
 }
 
-// One weight row of the stream: dot products of its K-items against the LDS / VGPR activations,
-// wave reduction, store.
-template <int NC, bool Q5, bool KEEP>
-__device__ __forceinline__ void kq_row(const kq_regs<Q5> & first, const uint8_t * wrow, int64_t row, const mi_mmv_group & g,
-                                       bool have_first, bool single_item, int s0, int j0, int lane, int nitems, int ncols,
-                                       const act_item (&a0)[KEEP ? NC : 1], const int8_t * lqs, const float * ld,
-                                       const int16_t * ls32, float * dst) {
-    constexpr int BS = Q5 ? 176 : 144;
-    const int64_t K = g.K;
-    float acc[NC];
-#pragma unroll
-    for (int c = 0; c < NC; c++) acc[c] = 0.0f;
-    if (have_first) {
-        if constexpr (KEEP) {
-            if (single_item) kq_dot<NC, Q5>(first, j0, *(const act_item(*)[NC]) a0, ncols, acc);
-        }
-        if (!KEEP || !single_item) {
-            act_item a[NC];
-#pragma unroll
-            for (int c = 0; c < NC; c++) {
-                if (NC > 1 && c >= ncols) break;
-                act_load(a[c], lqs, ld, ls32, K, c, s0, j0);
-            }
-            kq_dot<NC, Q5>(first, j0, a, ncols, acc);
+// ------------------------------------------------------------------ weight formats
+
+template <bool Q5>
+struct FmtKQ {
+    static constexpr int QKA = 256;  // activation block
+    static constexpr int ITEM = 64;  // elements per item
+    static constexpr int BS = Q5 ? 176 : 144;
+    struct Regs {
+        uint4 hdr, qa, qb;
+        uint4 ha, hb;  // Q5 only
+    };
+    __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item) {
+        const int s = item >> 2, j = item & 3;
+        const uint8_t * blk = row + (size_t) s * BS;
+        r.hdr = *(const uint4 *) blk;
+        const uint8_t * qp = blk + (Q5 ? 48 : 16) + 32 * j;
+        r.qa = *(const uint4 *) qp;
+        r.qb = *(const uint4 *) (qp + 16);
+        if constexpr (Q5) {
+            r.ha = *(const uint4 *) (blk + 16);
+            r.hb = *(const uint4 *) (blk + 32);
         }
     }
-    for (int it = lane + 64; it < nitems; it += 64) {
-        const int s = it >> 2, j = it & 3;
-        kq_regs<Q5> rr;
-        kq_load<Q5>(rr, wrow + (size_t) s * BS, j);
-        act_item a[NC];
+    template <int NC>
+    __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
+        const int s = item >> 2, j = item & 3;
+        const uint32_t q[8] = {r.qa.x, r.qa.y, r.qa.z, r.qa.w, r.qb.x, r.qb.y, r.qb.z, r.qb.w};
+        uint32_t qlo[8], qhi[8];
+        if constexpr (Q5) {
+            const uint32_t h[8] = {r.ha.x, r.ha.y, r.ha.z, r.ha.w, r.hb.x, r.hb.y, r.hb.z, r.hb.w};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = (q[i] & 0x0F0F0F0Fu) | (((h[i] >> (2 * j)) & 0x01010101u) << 4);
+                qhi[i] = ((q[i] >> 4) & 0x0F0F0F0Fu) | (((h[i] >> (2 * j + 1)) & 0x01010101u) << 4);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = q[i] & 0x0F0F0F0Fu;
+                qhi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
+            }
+        }
+        const float dw = mi_h2f((uint16_t) (r.hdr.x & 0xFFFF));
+        const float dmw = mi_h2f((uint16_t) (r.hdr.x >> 16));
+        int sc0, m0, sc1, m1;
+        mi_scale_min_k4(2 * j, r.hdr.y, r.hdr.z, r.hdr.w, sc0, m0);
+        mi_scale_min_k4(2 * j + 1, r.hdr.y, r.hdr.z, r.hdr.w, sc1, m1);
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             if (NC > 1 && c >= ncols) break;
-            act_load(a[c], lqs, ld, ls32, K, c, s, j);
-        }
-        kq_dot<NC, Q5>(rr, j, a, ncols, acc);
-    }
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) s * 256 + 64 * j);
+            const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            const int alo[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const int ahi[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            int lo = 0, hi = 0;
 #pragma unroll
-    for (int c = 0; c < NC; c++) {
-        const float v = mi_wave_sum_u(acc[c]);
-        if (lane == 0 && c < ncols) *(float *) ((char *) dst + c * g.ycol + row * sizeof(float)) = v;
+            for (int i = 0; i < 8; i++) {
+                lo = mi_dot4((int) qlo[i], alo[i], lo);
+                hi = mi_dot4((int) qhi[i], ahi[i], hi);
+            }
+            const int ss = *(const int *) (a.s32 + c * (K / 32) + s * 8 + 2 * j);
+            const int sumi = sc0 * lo + sc1 * hi;
+            const int summ = m0 * (int) (int16_t) (ss & 0xFFFF) + m1 * (ss >> 16);
+            acc[c] += a.d[c * (K / 256) + s] * (dw * (float) sumi - dmw * (float) summ);
+        }
     }
-}
+};
 
-// PD = rows of weight loads a wave keeps in flight ahead of the row it is computing.
-template <int NC, bool Q5, int PD, bool KEEP_ACT, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_mmv_kq_stream(mi_mmv_group g) {
+// Q4_0 (18 B) / Q8_0 (34 B) blocks: 2-byte aligned. Load the dwords covering the quants
+// (aligned down) and re-align with v_alignbyte; d is a separate 2-byte load.
+template <bool Q8>
+struct FmtQ0 {
+    static constexpr int QKA = 32;
+    static constexpr int ITEM = 32;
+    static constexpr int BS = Q8 ? 34 : 18;
+    static constexpr int NQ = Q8 ? 8 : 4;  // quant dwords per block
+    struct Regs {
+        uint32_t w[NQ + 1];
+        uint32_t d;
+        uint32_t shift;
+    };
+    __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item) {
+        const uint8_t * blk = row + (size_t) item * BS;
+        const uintptr_t qa = (uintptr_t) (blk + 2);
+        const uint32_t * w = (const uint32_t *) (qa & ~(uintptr_t) 3);
+        r.shift = (uint32_t) (qa & 3);  // 0 or 2
+#pragma unroll
+        for (int i = 0; i <= NQ; i++) r.w[i] = w[i];  // buffers carry 256 B of tail slack
+        r.d = *(const uint16_t *) blk;
+    }
+    template <int NC>
+    __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
+        uint32_t t[NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; i++) t[i] = __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], r.shift);
+        const float dw = mi_h2f((uint16_t) r.d);
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 32);
+            const int4 a0 = p[0], a1 = p[1];
+            const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            int sumi = 0;
+            if constexpr (Q8) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) sumi = mi_dot4((int) t[i], av[i], sumi);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    sumi = mi_dot4((int) (t[i] & 0x0F0F0F0Fu), av[i], sumi);
+                    sumi = mi_dot4((int) ((t[i] >> 4) & 0x0F0F0F0Fu), av[i + 4], sumi);
+                }
+                sumi -= 8 * (int) a.s32[c * (K / 32) + item];  // (q - 8) * y
+            }
+            acc[c] += (float) sumi * (dw * a.d[c * (K / 32) + item]);
+        }
+    }
+};
+
+// ------------------------------------------------------------------ the streaming kernel
+
+// IPL = items per lane held in the prefetch ring (further items of long rows are loaded
+// in-line); PD = rows in flight ahead of the row being computed.
+template <class F, int NC, int PD, int IPL>
+__global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr int BS = Q5 ? 176 : 144;
     constexpr int NB = PD + 1;  // ring slots
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -176,67 +237,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     const char * X = g.m[member].X;
     float * dst = g.m[member].dst;
     const int64_t K = g.K;
-    const int nsb = (int) (K / 256);
-    const int nitems = 4 * nsb;
+    const int nitems = (int) (K / F::ITEM);
     const int ncols = g.ncols;
-
-    int8_t * lqs = (int8_t *) lds;
-    float * ld = (float *) (lds + NC * K);
-    int16_t * ls32 = (int16_t *) (lds + NC * K + NC * (K / 256) * 4);
+    const lds_act act = lds_carve<F::QKA>(lds, NC, K);
 
     const int64_t row_begin = (int64_t) rb * g.rows_per_block;
     const int64_t row_end = row_begin + g.rows_per_block < g.N ? row_begin + g.rows_per_block : g.N;
-    // wave w streams rows row_begin + w, row_begin + w + 4, ...
     const int64_t nrows = row_end - row_begin > wave ? (row_end - row_begin - wave + 3) / 4 : 0;
-
-    const bool single_item = nitems <= 64;
-    const bool have_first = lane < nitems;
-    const int s0 = lane >> 2, j0 = lane & 3;
-    const size_t item_off = (size_t) s0 * BS;
     auto wrow_of = [&](int64_t k) { return W + (row_begin + 4 * k + wave) * g.nb01; };
 
+    typename F::Regs ring[NB][IPL];
+    auto prefetch = [&](typename F::Regs (&slot)[IPL], int64_t k) {
+        const uint8_t * wr = wrow_of(k);
+#pragma unroll
+        for (int i = 0; i < IPL; i++) {
+            const int item = lane + 64 * i;
+            if (item < nitems) F::load(slot[i], wr, item);
+        }
+    };
+
     // 1) the first PD rows' weights in flight
-    kq_regs<Q5> ring[NB];
 #pragma unroll
     for (int u = 0; u < PD; u++) {
-        if (have_first && u < nrows) kq_load<Q5>(ring[u], wrow_of(u) + item_off, j0);
+        if (u < nrows) prefetch(ring[u], u);
     }
 
-    // 2) quantize the member's activation columns into LDS (wave w: superblocks w, w+4, ...)
+    // 2) quantize the member's activation columns into LDS (wave w: 256-slices w, w+4, ...)
     {
-        const int total = nsb * ncols;
+        const int nsl = (int) (K / 256);
+        const int total = nsl * ncols;
         for (int p0 = wave; p0 < total; p0 += 16) {
-            // unconditional loads (clamped index): a predicated load makes hipcc wait vmcnt(0)
-            // per element instead of once for the batch
+            // unconditional (clamped) loads: a predicated load makes hipcc wait vmcnt(0) per load
             float4 v[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int p = min(p0 + 4 * u, total - 1);
-                const int c = p / nsb, sb = p - c * nsb;
-                v[u] = *(const float4 *) (X + c * g.xcol + ((size_t) sb * 256 + lane * 4) * sizeof(float));
+                const int c = p / nsl, sl = p - c * nsl;
+                v[u] = *(const float4 *) (X + c * g.xcol + ((size_t) sl * 256 + lane * 4) * sizeof(float));
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int p = p0 + 4 * u;
                 if (p < total) {
-                    const int c = p / nsb, sb = p - c * nsb;
-                    quantize_sb_to_lds(v[u], lane, lqs + c * K + sb * 256, ld + c * nsb + sb, ls32 + c * (K / 32) + sb * 8);
+                    const int c = p / nsl, sl = p - c * nsl;
+                    quantize_slice<F::QKA>(v[u], lane, act, K, c, sl);
                 }
             }
         }
     }
     __syncthreads();
-
-    // few columns: the lane's activation slice may live in VGPRs for the whole stream
-    constexpr bool KEEP = KEEP_ACT && NC <= 2;
-    act_item a0[KEEP ? NC : 1];
-    if (KEEP && single_item && have_first) {
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            if (NC > 1 && c >= ncols) break;
-            act_load(a0[c], lqs, ld, ls32, K, c, s0, j0);
-        }
-    }
 
     // 3) stream: ring slot u holds row k0+u; refill it with row k0+u+PD right before using it
     for (int64_t k0 = 0; k0 < nrows; k0 += NB) {
@@ -244,73 +293,116 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         for (int u = 0; u < NB; u++) {
             const int64_t k = k0 + u;
             if (k >= nrows) break;  // wave-uniform
-            if (have_first && k + PD < nrows) kq_load<Q5>(ring[(u + PD) % NB], wrow_of(k + PD) + item_off, j0);
-            kq_row<NC, Q5, KEEP>(ring[u], wrow_of(k), row_begin + 4 * k + wave, g, have_first, single_item, s0, j0, lane,
-                                 nitems, ncols, a0, lqs, ld, ls32, dst);
+            if (k + PD < nrows) prefetch(ring[(u + PD) % NB], k + PD);
+            float acc[NC];
+#pragma unroll
+            for (int c = 0; c < NC; c++) acc[c] = 0.0f;
+#pragma unroll
+            for (int i = 0; i < IPL; i++) {
+                const int item = lane + 64 * i;
+                if (item < nitems) F::template dot<NC>(ring[u][i], item, act, K, ncols, acc);
+            }
+            const uint8_t * wr = wrow_of(k);
+            for (int item = lane + 64 * IPL; item < nitems; item += 64) {
+                typename F::Regs rr;
+                F::load(rr, wr, item);
+                F::template dot<NC>(rr, item, act, K, ncols, acc);
+            }
+            const int64_t row = row_begin + 4 * k + wave;
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const float v = mi_wave_sum_u(acc[c]);
+                if (lane == 0 && c < ncols) *(float *) ((char *) dst + c * g.ycol + row * sizeof(float)) = v;
+            }
         }
     }
 }
 
-template <int NC, bool Q5>
-void launch_kq(const mi_mmv_group & g, int pd, hipStream_t s) {
-    const size_t lds = (size_t) NC * (g.K + (g.K / 256) * 4 + (g.K / 32) * 2);
-    const dim3 grid((unsigned) (g.blocks_per_member * g.n));
-    // variant codes (tuning): 10*PD + v, v: 0 = act in VGPRs, 1 = act from LDS, 2 = LDS + 5 waves/EU
-    switch (pd) {
-        case 10: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 1, true, 1>), grid, dim3(256), lds, s, g); break;
-        case 11: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 1, false, 1>), grid, dim3(256), lds, s, g); break;
-        case 12: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 1, false, 5>), grid, dim3(256), lds, s, g); break;
-        case 20: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 2, true, 1>), grid, dim3(256), lds, s, g); break;
-        case 21: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 2, false, 1>), grid, dim3(256), lds, s, g); break;
-        case 22: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 2, false, 4>), grid, dim3(256), lds, s, g); break;
-        case 31: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 3, false, 1>), grid, dim3(256), lds, s, g); break;
-        case 32: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 3, false, 4>), grid, dim3(256), lds, s, g); break;
-        case 41: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 4, false, 1>), grid, dim3(256), lds, s, g); break;
-        default: hipLaunchKernelGGL((k_mmv_kq_stream<NC, Q5, 1, true, 1>), grid, dim3(256), lds, s, g); break;
-    }
+// Workgroups that fit on the chip at once for this kernel instance (all of them are launched
+// in one wave, so no workgroup waits for another to retire). Speed only: nothing relies on
+// co-residency. Cached per kernel.
+int resident_blocks(const void * fn, size_t lds) {
+    struct entry { const void * fn; size_t lds; int n; };
+    static entry cache[64];
+    static int ncache = 0;
+    for (int i = 0; i < ncache; i++) if (cache[i].fn == fn && cache[i].lds == lds) return cache[i].n;
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    (void) hipGetDevice(&dev);
+    (void) hipGetDeviceProperties(&prop, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    const int n = per_cu * prop.multiProcessorCount;
+    if (ncache < 64) cache[ncache++] = entry{fn, lds, n};
+    return n;
 }
 
-template <bool Q5>
-void launch_kq_nc(const mi_mmv_group & g, int pd, hipStream_t s) {
-    switch (g.ncols) {
-        case 1: launch_kq<1, Q5>(g, pd, s); break;
-        case 2: launch_kq<2, Q5>(g, pd, s); break;
-        case 3: case 4: launch_kq<4, Q5>(g, pd, s); break;
-        default: launch_kq<8, Q5>(g, pd, s); break;
-    }
-}
-
-} // namespace
-
-static int env_int(const char * name, int def) {
-    const char * v = getenv(name);
-    return v ? atoi(v) : def;
-}
-
-size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols) {
-    const int64_t nc = ncols <= 2 ? ncols : (ncols <= 4 ? 4 : 8);
-    if (type == 12 || type == 13) return (size_t) nc * (K + (K / 256) * 4 + (K / 32) * 2);
-    return SIZE_MAX;
-}
-
-bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols) {
-    if (type != 12 && type != 13) return false;
-    if (ncols < 1 || ncols > 8) return false;
-    return mi_mmv_fused_lds_bytes(type, K, ncols) <= 64 * 1024;
-}
-
-mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 1024), env_int("GGML_MI355X_MMV_VARIANT", 21)};
-
-void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s) {
-    // ~4 resident workgroups per CU over all members; each workgroup streams a row range
-    const int target_blocks = g_mi_tuning.mmv_blocks;
-    const int variant = g_mi_tuning.mmv_variant;
-    int bpm = target_blocks / g.n;
+template <class F, int NC, int PD, int IPL>
+void launch_one(mi_mmv_group g, hipStream_t s) {
+    const size_t lds = lds_bytes<F::QKA>(NC, g.K);
+    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL>;
+    const int target = g_mi_tuning.mmv_blocks > 0 ? g_mi_tuning.mmv_blocks : resident_blocks(fn, lds);
+    int bpm = target / g.n;
     if (bpm < 1) bpm = 1;
     int64_t rows = (g.N + bpm - 1) / bpm;
     rows = (rows + 3) / 4 * 4;
     g.rows_per_block = rows;
     g.blocks_per_member = (int) ((g.N + rows - 1) / rows);
-    if (g.type == 12) launch_kq_nc<false>(g, variant, s);
-    else launch_kq_nc<true>(g, variant, s);
+    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds, s, g);
+}
+
+template <class F, int NC>
+void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
+    const int items = (int) (g.K / F::ITEM);
+    if (items > 64) {
+        // two items per lane in the ring (Q4_0 / Q8_0 at K=4096)
+        if (variant / 10 == 1) launch_one<F, NC, 1, 2>(g, s);
+        else launch_one<F, NC, 2, 2>(g, s);
+        return;
+    }
+    switch (variant / 10) {
+        case 1: launch_one<F, NC, 1, 1>(g, s); break;
+        case 3: launch_one<F, NC, 3, 1>(g, s); break;
+        default: launch_one<F, NC, 2, 1>(g, s); break;
+    }
+}
+
+template <class F>
+void launch_stream_nc(const mi_mmv_group & g, int variant, hipStream_t s) {
+    switch (g.ncols) {
+        case 1: launch_stream<F, 1>(g, variant, s); break;
+        case 2: launch_stream<F, 2>(g, variant, s); break;
+        case 3: case 4: launch_stream<F, 4>(g, variant, s); break;
+        default: launch_stream<F, 8>(g, variant, s); break;
+    }
+}
+
+int qka_of(int type) { return (type == 12 || type == 13) ? 256 : 32; }
+
+} // namespace
+
+size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols) {
+    const int nc = ncols <= 2 ? (int) ncols : (ncols <= 4 ? 4 : 8);
+    return qka_of(type) == 256 ? lds_bytes<256>(nc, K) : lds_bytes<32>(nc, K);
+}
+
+bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols) {
+    if (type != 12 && type != 13 && type != 2 && type != 8) return false;
+    if (ncols < 1 || ncols > 8 || K % 256 != 0) return false;
+    return mi_mmv_fused_lds_bytes(type, K, ncols) <= 64 * 1024;
+}
+
+
+
+void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s) {
+    // variant 0 = per-type default, from interleaved A/B runs on MI355X (tools/mmv_tune.py):
+    // prefetch depth 2 for Q4_K / Q8_0, depth 1 for Q5_K / Q4_0 (fewer VGPRs, more waves)
+    int variant = g_mi_tuning.mmv_variant;
+    if (variant == 0) variant = (g.type == 12 || g.type == 8) ? 21 : 11;
+    switch (g.type) {
+        case 12: launch_stream_nc<FmtKQ<false>>(g, variant, s); break;
+        case 13: launch_stream_nc<FmtKQ<true>>(g, variant, s); break;
+        case 2: launch_stream_nc<FmtQ0<false>>(g, variant, s); break;
+        case 8: launch_stream_nc<FmtQ0<true>>(g, variant, s); break;
+        default: break;
+    }
 }
