@@ -246,6 +246,18 @@ def main():
             sweep[name] = {"GB/s": round(r * unit_bytes(tt, k, n, 1) / (ms / 1e3) / 1e9, 1),
                            "us_per_mul_mat": round(ms * 1e3 / r, 2)}
             w2.free()
+        # configs[4]: batched B=512 prefill Q4_K 4096x4096 on MFMA tiles (per GPU; the 8-GPU run
+        # shards the 512 prompt columns, 64 per GPU)
+        for bb in (512, 64):
+            w3 = MulMatWorkload(lib, backend, 12, 4096, 4096, bb, 8)
+            for _ in range(3):
+                w3.step()
+            lib.ggml_backend_synchronize(backend)
+            ms = event_time_per_step(torch, w3, stream_ptr, iters=10)
+            flops = 2.0 * 4096 * 4096 * bb * 8
+            sweep[f"q4_K_4096x4096_b{bb}_prefill"] = {"TFLOP/s": round(flops / (ms / 1e3) / 1e12, 2),
+                                                       "us_per_mul_mat": round(ms * 1e3 / 8, 2)}
+            w3.free()
         result["sweep"] = sweep
 
     if rank == 0 and world == 1 and not args.no_cpu:

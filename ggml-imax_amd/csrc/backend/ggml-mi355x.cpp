@@ -415,8 +415,18 @@ static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
     } else {
         void * act = get_activations(ctx, src1, kind, m.K);
         const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
-        if (kind == 2) mi_mul_mat_f16(m, (const uint16_t *) act, ctx->stream);
-        else mi_mul_mat_q(m, mi_act_q8_carve(act, m.K, ncols, kind == 1), ctx->stream);
+        static const bool no_mmq = getenv("GGML_MI355X_NO_MMQ") != nullptr;
+        const bool batched = !no_mmq && src1->ne[1] > 8 && m.ne02 == 1 && m.ne03 == 1 && m.ne12 == 1 && m.ne13 == 1 &&
+                             mi_mmq_supported(m.type, m.K, m.nb01, m.nb1) && ((uintptr_t) m.W % 16) == 0;
+        if (batched) {
+            const mi_act_q8 aq = kind == 2 ? mi_act_q8{} : mi_act_q8_carve(act, m.K, ncols, kind == 1);
+            mi_mul_mat_mmq(m.type, m.W, m.nb01, m.K, m.N, aq, kind == 2 ? (const uint16_t *) act : nullptr, ncols, m.dst,
+                           m.nb1, ctx->stream);
+        } else if (kind == 2) {
+            mi_mul_mat_f16(m, (const uint16_t *) act, ctx->stream);
+        } else {
+            mi_mul_mat_q(m, mi_act_q8_carve(act, m.K, ncols, kind == 1), ctx->stream);
+        }
     }
     ctx->last_launches++;
 }

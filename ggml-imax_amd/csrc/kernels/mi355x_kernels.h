@@ -79,6 +79,13 @@ struct mi_tuning {
 extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);
 void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s);
+// Batched (prefill) mul_mat on MFMA: 2-D weights [K, N] of type Q4_0/Q8_0/Q4_K/Q5_K/F16,
+// `ncols` activation columns already converted (act for quantized types, xh for F16),
+// dst columns of ycol bytes. Requires K % 256 == 0.
+bool mi_mmq_supported(int type, int64_t K, size_t nb01, size_t ycol);
+void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_q8 & act, const uint16_t * xh,
+                    int64_t ncols, float * dst, size_t ycol, hipStream_t s);
+
 // f16 weights x f16-rounded activations
 void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s);
 // f32 x f32, both operands arbitrarily strided (src1 described by x, src0 by m.nb0x)
