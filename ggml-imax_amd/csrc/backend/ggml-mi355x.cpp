@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -247,6 +248,7 @@ struct mi_backend_ctx {
     std::vector<mi_act_cache_entry> act_cache;
     bool graph_capture = true;
     int last_launches = 0;
+    uint16_t * tables = nullptr;  // device: exp, gelu, silu fp16 tables (3 x 65536)
 };
 
 static ggml_guid_t mi_guid() {
@@ -281,7 +283,12 @@ static bool mm_src0_supported(ggml_type t) {
            t == GGML_TYPE_F16 || t == GGML_TYPE_F32;
 }
 
+static bool is_f32(const ggml_tensor * t) { return t && t->type == GGML_TYPE_F32; }
+static bool is_f16_or_f32(const ggml_tensor * t) { return t && (t->type == GGML_TYPE_F32 || t->type == GGML_TYPE_F16); }
+
 static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
+    const ggml_tensor * a = op->src[0];
+    const ggml_tensor * b = op->src[1];
     switch (op->op) {
         case GGML_OP_NONE:
         case GGML_OP_RESHAPE:
@@ -290,13 +297,50 @@ static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
         case GGML_OP_TRANSPOSE:
             return true;
         case GGML_OP_MUL_MAT: {
-            const ggml_tensor * a = op->src[0];
-            const ggml_tensor * b = op->src[1];
             if (!mm_src0_supported(a->type)) return false;
             if (b->type != GGML_TYPE_F32) return false;
             if (a->nb[0] != ggml_type_size(a->type) || b->nb[0] != sizeof(float)) return false;
             if (a->type == GGML_TYPE_F16 && (a->ne[0] % 8 != 0 || a->nb[1] % 16 != 0)) return false;
             return true;
+        }
+        case GGML_OP_ADD:
+        case GGML_OP_SUB:
+        case GGML_OP_MUL:
+        case GGML_OP_DIV:
+            return is_f16_or_f32(a) && is_f16_or_f32(b) && is_f16_or_f32(op);
+        case GGML_OP_SCALE:
+            return is_f32(a) && is_f32(op);
+        case GGML_OP_NORM:
+        case GGML_OP_RMS_NORM:
+            return is_f32(a) && is_f32(op) && a->nb[0] == sizeof(float);
+        case GGML_OP_SOFT_MAX: {
+            float max_bias;
+            memcpy(&max_bias, (const float *) op->op_params + 1, sizeof(float));
+            return is_f32(a) && is_f32(op) && max_bias == 0.0f && (!b || is_f16_or_f32(b)) && ggml_is_contiguous(a);
+        }
+        case GGML_OP_DIAG_MASK_INF:
+        case GGML_OP_DIAG_MASK_ZERO:
+            return is_f32(a) && is_f32(op);
+        case GGML_OP_UNARY:
+            switch (ggml_get_unary_op(op)) {
+                case GGML_UNARY_OP_GELU:
+                case GGML_UNARY_OP_SILU:
+                    return is_f32(a) && is_f32(op);
+                default:
+                    return false;
+            }
+        case GGML_OP_GET_ROWS:
+            return is_f16_or_f32(a) && b->type == GGML_TYPE_I32 && is_f32(op);
+        case GGML_OP_CPY:
+        case GGML_OP_DUP:
+        case GGML_OP_CONT:
+            return is_f16_or_f32(a) && is_f16_or_f32(op);
+        case GGML_OP_ROPE: {
+            const int32_t * pp = (const int32_t *) op->op_params;
+            const int mode = pp[2];
+            float xpos_base;
+            memcpy(&xpos_base, pp + 11, sizeof(float));
+            return is_f32(a) && is_f32(op) && (mode == 0 || mode == 2) && xpos_base == 0.0f && a->nb[0] == sizeof(float);
         }
         default:
             return false;
@@ -432,6 +476,140 @@ static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// companion ops (GPT-2 / LLaMA-shaped graphs)
+// ---------------------------------------------------------------------------------------------
+
+static uint16_t host_f2h(float f) {  // round-to-nearest-even, as F16C _cvtss_sh(x, 0)
+    uint32_t x;
+    memcpy(&x, &f, 4);
+    const uint32_t sign = (x >> 16) & 0x8000u;
+    const uint32_t ax = x & 0x7fffffffu;
+    if (ax > 0x7f800000u) return (uint16_t) (sign | 0x7e00u | ((ax >> 13) & 0x3ffu));
+    if (ax >= 0x477ff000u) return (uint16_t) (sign | 0x7c00u);
+    if (ax < 0x38800000u) {  // subnormal half
+        const float v = fabsf(f) * 16777216.0f;  // exact scaling by 2^24
+        return (uint16_t) (sign | (uint32_t) nearbyintf(v));
+    }
+    const uint32_t r = ax + 0xfffu + ((ax >> 13) & 1u) - 0x38000000u;
+    return (uint16_t) (sign | (r >> 13));
+}
+
+static float host_h2f(uint16_t h) {
+    const uint32_t sign = (uint32_t) (h & 0x8000u) << 16;
+    const uint32_t e = (h >> 10) & 0x1f, m = h & 0x3ff;
+    float r;
+    if (e == 0) r = ldexpf((float) m, -24);
+    else if (e == 31) r = m ? NAN : INFINITY;
+    else r = ldexpf((float) (m | 0x400), (int) e - 25);
+    uint32_t u;
+    memcpy(&u, &r, 4);
+    u |= sign;
+    memcpy(&r, &u, 4);
+    return r;
+}
+
+// the reference's fp16 lookup tables (src/ggml.c:2884-2898), same formulas and libm
+static const float kGeluCoefA = 0.044715f;
+static const float kSqrt2OverPi = 0.79788456080286535587989211986876f;
+static float gelu_ref(float x) { return 0.5f * x * (1.0f + tanhf(kSqrt2OverPi * x * (1.0f + kGeluCoefA * x * x))); }
+static float silu_ref(float x) { return x / (1.0f + expf(-x)); }
+
+static const uint16_t * op_tables(mi_backend_ctx * ctx) {
+    if (!ctx->tables) {
+        std::vector<uint16_t> h(3 * 65536);
+        for (int i = 0; i < 65536; i++) {
+            const float f = host_h2f((uint16_t) i);
+            h[i] = host_f2h(expf(f));
+            h[65536 + i] = host_f2h(gelu_ref(f));
+            h[2 * 65536 + i] = host_f2h(silu_ref(f));
+        }
+        MI_CHECK(hipMalloc(&ctx->tables, h.size() * sizeof(uint16_t)));
+        MI_CHECK(hipMemcpy(ctx->tables, h.data(), h.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    }
+    return ctx->tables;
+}
+
+static mi_tensor_desc desc(const ggml_tensor * t) {
+    mi_tensor_desc d;
+    d.data = t ? (char *) t->data : nullptr;
+    d.type = t ? (int) t->type : 0;
+    for (int i = 0; i < 4; i++) {
+        d.ne[i] = t ? t->ne[i] : 1;
+        d.nb[i] = t ? t->nb[i] : 0;
+    }
+    return d;
+}
+
+static float op_param_f(const ggml_tensor * t, int i) {
+    float v;
+    memcpy(&v, (const int32_t *) t->op_params + i, sizeof(float));
+    return v;
+}
+
+// ggml_rope_yarn_corr_dims (src/ggml.c:13746-13773)
+static void rope_corr_dims(int n_dims, int n_orig_ctx, float freq_base, float beta_fast, float beta_slow, float dims[2]) {
+    auto corr_dim = [&](float n_rot) {
+        return n_dims * logf(n_orig_ctx / (n_rot * 2 * (float) M_PI)) / (2 * logf(freq_base));
+    };
+    const float start = floorf(corr_dim(beta_fast));
+    const float end = ceilf(corr_dim(beta_slow));
+    dims[0] = std::max(0.0f, start);
+    dims[1] = std::min((float) (n_dims - 1), end);
+}
+
+static void op_companion(mi_backend_ctx * ctx, ggml_tensor * node) {
+    const ggml_tensor * a = node->src[0];
+    const ggml_tensor * b = node->src[1];
+    hipStream_t st = ctx->stream;
+    switch (node->op) {
+        case GGML_OP_ADD: mi_op_binary(desc(node), desc(a), desc(b), MI_OP_ADD, st); break;
+        case GGML_OP_SUB: mi_op_binary(desc(node), desc(a), desc(b), MI_OP_SUB, st); break;
+        case GGML_OP_MUL: mi_op_binary(desc(node), desc(a), desc(b), MI_OP_MUL, st); break;
+        case GGML_OP_DIV: mi_op_binary(desc(node), desc(a), desc(b), MI_OP_DIV, st); break;
+        case GGML_OP_SCALE: mi_op_unary(desc(node), desc(a), MI_OP_SCALE, op_param_f(node, 0), nullptr, st); break;
+        case GGML_OP_NORM: mi_op_norm(desc(node), desc(a), op_param_f(node, 0), false, st); break;
+        case GGML_OP_RMS_NORM: mi_op_norm(desc(node), desc(a), op_param_f(node, 0), true, st); break;
+        case GGML_OP_SOFT_MAX: mi_op_soft_max(desc(node), desc(a), desc(b), op_param_f(node, 0), op_tables(ctx), st); break;
+        case GGML_OP_DIAG_MASK_INF:
+            mi_op_diag_mask(desc(node), desc(a), ((const int32_t *) node->op_params)[0], -INFINITY, st);
+            break;
+        case GGML_OP_DIAG_MASK_ZERO:
+            mi_op_diag_mask(desc(node), desc(a), ((const int32_t *) node->op_params)[0], 0.0f, st);
+            break;
+        case GGML_OP_UNARY: {
+            const ggml_unary_op u = ggml_get_unary_op(node);
+            MI_ASSERT(u == GGML_UNARY_OP_GELU || u == GGML_UNARY_OP_SILU);
+            const uint16_t * t = op_tables(ctx) + (u == GGML_UNARY_OP_GELU ? 65536 : 2 * 65536);
+            mi_op_unary(desc(node), desc(a), u == GGML_UNARY_OP_GELU ? MI_OP_GELU : MI_OP_SILU, 0.0f, t, st);
+            break;
+        }
+        case GGML_OP_GET_ROWS: mi_op_get_rows(desc(node), desc(a), desc(b), st); break;
+        case GGML_OP_CPY:
+        case GGML_OP_DUP:
+        case GGML_OP_CONT:
+            MI_ASSERT(ggml_nelements(node) == ggml_nelements(a));
+            mi_op_cpy(desc(node), desc(a), st);
+            break;
+        case GGML_OP_ROPE: {
+            const int32_t * pp = (const int32_t *) node->op_params;
+            const int n_dims = pp[1], mode = pp[2], n_orig_ctx = pp[4];
+            const float freq_base = op_param_f(node, 5), freq_scale = op_param_f(node, 6), ext_factor = op_param_f(node, 7);
+            const float attn_factor = op_param_f(node, 8), beta_fast = op_param_f(node, 9), beta_slow = op_param_f(node, 10);
+            MI_ASSERT(n_dims <= a->ne[0] && n_dims % 2 == 0);
+            float corr[2];
+            rope_corr_dims(n_dims, n_orig_ctx, freq_base, beta_fast, beta_slow, corr);
+            mi_op_rope(desc(node), desc(a), (const int32_t *) b->data, n_dims, mode, freq_base, freq_scale, ext_factor,
+                       attn_factor, corr[0], corr[1], st);
+            break;
+        }
+        default:
+            fprintf(stderr, "%s: error: op not supported %s (%s)\\n", __func__, node->name, ggml_op_desc(node));
+            MI_ASSERT(!"unsupported op");
+    }
+    ctx->last_launches++;
+}
+
+// ---------------------------------------------------------------------------------------------
 // graph execution
 // ---------------------------------------------------------------------------------------------
 
@@ -541,8 +719,7 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
                 op_mul_mat(ctx, node);
                 break;
             default:
-                fprintf(stderr, "%s: error: op not supported %s (%s)\n", __func__, node->name, ggml_op_desc(node));
-                MI_ASSERT(!"unsupported op");
+                op_companion(ctx, node);
         }
         invalidate_activations(ctx, node);
     }
@@ -566,6 +743,7 @@ static void mi_backend_free(ggml_backend_t backend) {
         mi_device_guard g(ctx->device);
         MI_CHECK(hipStreamSynchronize(ctx->stream));
         if (ctx->scratch) MI_CHECK(hipFree(ctx->scratch));
+        if (ctx->tables) MI_CHECK(hipFree(ctx->tables));
         MI_CHECK(hipStreamDestroy(ctx->stream));
     }
     delete ctx;
@@ -763,6 +941,7 @@ ggml_backend_t ggml_backend_mi355x_init(int device) {
     {
         mi_device_guard g(device);
         MI_CHECK(hipStreamCreate(&ctx->stream));
+        op_tables(ctx);
     }
     const char * no_graphs = getenv("GGML_MI355X_DISABLE_GRAPHS");
     ctx->graph_capture = !(no_graphs && atoi(no_graphs) != 0);

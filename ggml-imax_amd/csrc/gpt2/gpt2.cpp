@@ -1,0 +1,448 @@
+// gpt2.cpp -- GPT-2 model driver over the ggml backend API (BASELINE config 4).
+//
+// Behaviour follows examples/gpt-2/main-backend.cpp of NAIST-Archlab/ggml-imax:
+//   file format + loader  :101-439   (legacy ggml magic, hparams, vocab, tensors by name,
+//                                     wte doubles as lm_head when the file has none :426-433)
+//   graph                 :442-717   (node-for-node the same ops, so a backend that passes the
+//                                     reference's test-backend-ops runs it unchanged)
+//   eval                  :728-786
+//   compute-buffer sizing :832-846   (worst case: n_batch tokens at the end of the context)
+// and the tokenizer of examples/common.cpp:272-329. Only the ggml API is used: the same source is
+// linked against this repo's runtime (product) and against the reference libggml (checker build in
+// oracle/, which gives the CPU logits).
+
+#include "gpt2-mi355x.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <regex>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr int kMaxNodes = 4096;  // GPT2_MAX_NODES
+
+struct layer_w {
+    ggml_tensor * ln_1_g, * ln_1_b, * ln_2_g, * ln_2_b;
+    ggml_tensor * c_attn_attn_w, * c_attn_attn_b, * c_attn_proj_w, * c_attn_proj_b;
+    ggml_tensor * c_mlp_fc_w, * c_mlp_fc_b, * c_mlp_proj_w, * c_mlp_proj_b;
+};
+
+struct vocab_t {
+    std::map<std::string, int32_t> token_to_id;
+    std::vector<std::string> id_to_token;
+};
+
+int64_t now_us() { return ggml_time_us(); }
+
+} // namespace
+
+struct gpt2_model {
+    gpt2_hparams_c hp = {50257, 1024, 768, 12, 12, 1, 1e-5f};
+    ggml_tensor * ln_f_g = nullptr, * ln_f_b = nullptr;
+    ggml_tensor * wte = nullptr, * wpe = nullptr, * lm_head = nullptr;
+    std::vector<layer_w> layers;
+    ggml_tensor * memory_k = nullptr, * memory_v = nullptr;
+    ggml_context * ctx_w = nullptr, * ctx_kv = nullptr;
+    ggml_backend_t backend = nullptr;
+    ggml_backend_buffer_t buffer_w = nullptr, buffer_kv = nullptr;
+    ggml_gallocr_t allocr = nullptr;
+    std::map<std::string, ggml_tensor *> tensors;
+    vocab_t vocab;
+    size_t weight_bytes = 0;
+    std::vector<uint8_t> graph_buf;
+    int last_nodes = 0;
+    int64_t us_build = 0, us_alloc = 0, us_compute = 0;
+};
+
+namespace {
+
+template <typename T> bool rd(std::ifstream & f, T & v) { return (bool) f.read((char *) &v, sizeof(T)); }
+
+bool load_file(gpt2_model & m, const char * fname, int n_ctx_override) {
+    std::ifstream fin(fname, std::ios::binary);
+    if (!fin) {
+        fprintf(stderr, "gpt2_model_load: failed to open '%s'\n", fname);
+        return false;
+    }
+    uint32_t magic = 0;
+    rd(fin, magic);
+    if (magic != GGML_FILE_MAGIC) {
+        fprintf(stderr, "gpt2_model_load: invalid model file '%s' (bad magic)\n", fname);
+        return false;
+    }
+    auto & hp = m.hp;
+    rd(fin, hp.n_vocab);
+    rd(fin, hp.n_ctx);
+    rd(fin, hp.n_embd);
+    rd(fin, hp.n_head);
+    rd(fin, hp.n_layer);
+    rd(fin, hp.ftype);
+    hp.ftype %= GGML_QNT_VERSION_FACTOR;
+
+    int32_t n_vocab = 0;
+    rd(fin, n_vocab);
+    if (n_vocab != hp.n_vocab) {
+        fprintf(stderr, "gpt2_model_load: invalid model file '%s' (bad vocab size %d != %d)\n", fname, n_vocab, hp.n_vocab);
+        return false;
+    }
+    m.vocab.id_to_token.resize(n_vocab);
+    for (int i = 0; i < n_vocab; i++) {
+        uint32_t len = 0;
+        rd(fin, len);
+        std::string w(len, '\0');
+        fin.read(&w[0], len);
+        m.vocab.token_to_id[w] = i;
+        m.vocab.id_to_token[i] = w;
+    }
+
+    const ggml_type wtype = ggml_ftype_to_ggml_type((ggml_ftype) hp.ftype);
+    if (wtype == GGML_TYPE_COUNT) {
+        fprintf(stderr, "gpt2_model_load: invalid model file '%s' (bad ftype value %d)\n", fname, hp.ftype);
+        return false;
+    }
+
+    // weights context + tensors (main-backend.cpp:186-297)
+    {
+        ggml_init_params ip = {ggml_tensor_overhead() * (size_t) (2 + 6 + 12 * hp.n_layer), nullptr, true};
+        m.ctx_w = ggml_init(ip);
+        if (!m.ctx_w) return false;
+        ggml_context * ctx = m.ctx_w;
+        const int E = hp.n_embd;
+        m.layers.resize(hp.n_layer);
+        m.ln_f_g = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, E);
+        m.ln_f_b = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, E);
+        m.wte = ggml_new_tensor_2d(ctx, wtype, E, hp.n_vocab);
+        m.wpe = ggml_new_tensor_2d(ctx, GGML_TYPE_F32, E, hp.n_ctx);
+        m.lm_head = ggml_new_tensor_2d(ctx, wtype, E, hp.n_vocab);
+        m.tensors["model/ln_f/g"] = m.ln_f_g;
+        m.tensors["model/ln_f/b"] = m.ln_f_b;
+        m.tensors["model/wte"] = m.wte;
+        m.tensors["model/wpe"] = m.wpe;
+        m.tensors["model/lm_head"] = m.lm_head;
+        for (int i = 0; i < hp.n_layer; i++) {
+            layer_w & L = m.layers[i];
+            L.ln_1_g = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, E);
+            L.ln_1_b = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, E);
+            L.ln_2_g = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, E);
+            L.ln_2_b = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, E);
+            L.c_attn_attn_w = ggml_new_tensor_2d(ctx, wtype, E, 3 * E);
+            L.c_attn_attn_b = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, 3 * E);
+            L.c_attn_proj_w = ggml_new_tensor_2d(ctx, wtype, E, E);
+            L.c_attn_proj_b = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, E);
+            L.c_mlp_fc_w = ggml_new_tensor_2d(ctx, wtype, E, 4 * E);
+            L.c_mlp_fc_b = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, 4 * E);
+            L.c_mlp_proj_w = ggml_new_tensor_2d(ctx, wtype, 4 * E, E);
+            L.c_mlp_proj_b = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, E);
+            const std::string p = "model/h" + std::to_string(i);
+            m.tensors[p + "/ln_1/g"] = L.ln_1_g;
+            m.tensors[p + "/ln_1/b"] = L.ln_1_b;
+            m.tensors[p + "/ln_2/g"] = L.ln_2_g;
+            m.tensors[p + "/ln_2/b"] = L.ln_2_b;
+            m.tensors[p + "/attn/c_attn/w"] = L.c_attn_attn_w;
+            m.tensors[p + "/attn/c_attn/b"] = L.c_attn_attn_b;
+            m.tensors[p + "/attn/c_proj/w"] = L.c_attn_proj_w;
+            m.tensors[p + "/attn/c_proj/b"] = L.c_attn_proj_b;
+            m.tensors[p + "/mlp/c_fc/w"] = L.c_mlp_fc_w;
+            m.tensors[p + "/mlp/c_fc/b"] = L.c_mlp_fc_b;
+            m.tensors[p + "/mlp/c_proj/w"] = L.c_mlp_proj_w;
+            m.tensors[p + "/mlp/c_proj/b"] = L.c_mlp_proj_b;
+        }
+    }
+    m.buffer_w = ggml_backend_alloc_ctx_tensors(m.ctx_w, m.backend);
+    if (!m.buffer_w) {
+        fprintf(stderr, "gpt2_model_load: weight buffer allocation failed\n");
+        return false;
+    }
+
+    if (n_ctx_override > 0) hp.n_ctx = n_ctx_override;
+
+    // KV memory, f32, n_layer*n_ctx*n_embd each (:306-343)
+    {
+        ggml_init_params ip = {ggml_tensor_overhead() * 2, nullptr, true};
+        m.ctx_kv = ggml_init(ip);
+        if (!m.ctx_kv) return false;
+        const int64_t n_elements = (int64_t) hp.n_embd * hp.n_layer * hp.n_ctx;
+        m.memory_k = ggml_new_tensor_1d(m.ctx_kv, GGML_TYPE_F32, n_elements);
+        m.memory_v = ggml_new_tensor_1d(m.ctx_kv, GGML_TYPE_F32, n_elements);
+        m.buffer_kv = ggml_backend_alloc_ctx_tensors(m.ctx_kv, m.backend);
+        if (!m.buffer_kv) {
+            fprintf(stderr, "gpt2_model_load: KV buffer allocation failed\n");
+            return false;
+        }
+    }
+
+    // tensors by name (:346-435)
+    bool has_lm_head = false;
+    std::vector<char> buf;
+    for (;;) {
+        int32_t n_dims = 0, length = 0, ttype = 0;
+        rd(fin, n_dims);
+        rd(fin, length);
+        rd(fin, ttype);
+        if (fin.eof()) break;
+        int32_t ne[2] = {1, 1};
+        int64_t nelements = 1;
+        for (int i = 0; i < n_dims; i++) {
+            rd(fin, ne[i]);
+            nelements *= ne[i];
+        }
+        std::string name(length, '\0');
+        fin.read(&name[0], length);
+        auto it = m.tensors.find(name);
+        if (it == m.tensors.end()) {
+            fprintf(stderr, "gpt2_model_load: unknown tensor '%s' in model file\n", name.c_str());
+            return false;
+        }
+        ggml_tensor * t = it->second;
+        ggml_set_name(t, name.c_str());
+        if (ggml_nelements(t) != nelements || t->ne[0] != ne[0] || t->ne[1] != ne[1]) {
+            fprintf(stderr, "gpt2_model_load: tensor '%s' has wrong shape in model file\n", name.c_str());
+            return false;
+        }
+        const size_t bpe = ggml_type_size((ggml_type) ttype);
+        if ((nelements * bpe) / ggml_blck_size(t->type) != ggml_nbytes(t)) {
+            fprintf(stderr, "gpt2_model_load: tensor '%s' has wrong size in model file\n", name.c_str());
+            return false;
+        }
+        const size_t nb = ggml_nbytes(t);
+        if (ggml_backend_buffer_is_host(m.buffer_w)) {
+            fin.read((char *) t->data, nb);
+        } else {
+            buf.resize(nb);
+            fin.read(buf.data(), nb);
+            ggml_backend_tensor_set(t, buf.data(), 0, nb);
+        }
+        if (!fin) {
+            fprintf(stderr, "gpt2_model_load: truncated model file at '%s'\n", name.c_str());
+            return false;
+        }
+        if (name == "model/wte" && !has_lm_head) m.lm_head = t;  // tied embedding
+        if (name == "model/lm_head") has_lm_head = true;
+        m.weight_bytes += nb;
+    }
+    return true;
+}
+
+// gpt2_graph, main-backend.cpp:442-717
+ggml_cgraph * build_graph(gpt2_model & m, int n_past, int N) {
+    const auto & hp = m.hp;
+    const int n_embd = hp.n_embd, n_layer = hp.n_layer, n_ctx = hp.n_ctx, n_head = hp.n_head;
+
+    const size_t buf_size = ggml_tensor_overhead() * kMaxNodes + ggml_graph_overhead_custom(kMaxNodes, false);
+    if (m.graph_buf.size() != buf_size) m.graph_buf.resize(buf_size);
+    ggml_init_params ip = {buf_size, m.graph_buf.data(), true};
+    ggml_context * ctx = ggml_init(ip);
+    ggml_cgraph * gf = ggml_new_graph_custom(ctx, kMaxNodes, false);
+
+    ggml_tensor * embd = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, N);
+    ggml_set_name(embd, "embd");
+    ggml_set_input(embd);
+    ggml_tensor * position = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, N);
+    ggml_set_name(position, "position");
+    ggml_set_input(position);
+
+    ggml_tensor * inpL = ggml_add(ctx, ggml_get_rows(ctx, m.wte, embd), ggml_get_rows(ctx, m.wpe, position));
+
+    const size_t esk = ggml_element_size(m.memory_k), esv = ggml_element_size(m.memory_v);
+    for (int il = 0; il < n_layer; ++il) {
+        const layer_w & L = m.layers[il];
+        ggml_tensor * cur = ggml_norm(ctx, inpL, hp.eps);
+        cur = ggml_add(ctx, ggml_mul(ctx, cur, L.ln_1_g), L.ln_1_b);
+
+        cur = ggml_mul_mat(ctx, L.c_attn_attn_w, cur);
+        cur = ggml_add(ctx, cur, L.c_attn_attn_b);
+
+        {
+            ggml_tensor * Qcur = ggml_view_2d(ctx, cur, n_embd, N, cur->nb[1], 0 * sizeof(float) * n_embd);
+            ggml_tensor * Kcur = ggml_view_2d(ctx, cur, n_embd, N, cur->nb[1], 1 * sizeof(float) * n_embd);
+            ggml_tensor * Vcur = ggml_view_2d(ctx, cur, n_embd, N, cur->nb[1], 2 * sizeof(float) * n_embd);
+
+            ggml_tensor * k = ggml_view_1d(ctx, m.memory_k, (int64_t) N * n_embd, (esk * n_embd) * (il * n_ctx + n_past));
+            ggml_tensor * v = ggml_view_1d(ctx, m.memory_v, (int64_t) N * n_embd, (esv * n_embd) * (il * n_ctx + n_past));
+            ggml_build_forward_expand(gf, ggml_cpy(ctx, Kcur, k));
+            ggml_build_forward_expand(gf, ggml_cpy(ctx, Vcur, v));
+
+            ggml_tensor * Q = ggml_permute(ctx, ggml_cont_3d(ctx, Qcur, n_embd / n_head, n_head, N), 0, 2, 1, 3);
+            ggml_tensor * K = ggml_permute(
+                ctx,
+                ggml_reshape_3d(ctx, ggml_view_1d(ctx, m.memory_k, (int64_t) (n_past + N) * n_embd, il * n_ctx * esk * n_embd),
+                                n_embd / n_head, n_head, n_past + N),
+                0, 2, 1, 3);
+            ggml_tensor * KQ = ggml_mul_mat(ctx, K, Q);
+            ggml_tensor * KQ_scaled = ggml_scale(ctx, KQ, 1.0f / sqrtf(float(n_embd) / n_head));
+            ggml_tensor * KQ_masked = ggml_diag_mask_inf(ctx, KQ_scaled, n_past);
+            ggml_tensor * KQ_soft_max = ggml_soft_max(ctx, KQ_masked);
+            ggml_tensor * V_trans = ggml_cont_3d(
+                ctx,
+                ggml_permute(ctx,
+                             ggml_reshape_3d(ctx,
+                                             ggml_view_1d(ctx, m.memory_v, (int64_t) (n_past + N) * n_embd, il * n_ctx * esv * n_embd),
+                                             n_embd / n_head, n_head, n_past + N),
+                             1, 2, 0, 3),
+                n_past + N, n_embd / n_head, n_head);
+            ggml_tensor * KQV = ggml_mul_mat(ctx, V_trans, KQ_soft_max);
+            ggml_tensor * KQV_merged = ggml_permute(ctx, KQV, 0, 2, 1, 3);
+            cur = ggml_cont_2d(ctx, KQV_merged, n_embd, N);
+        }
+
+        cur = ggml_mul_mat(ctx, L.c_attn_proj_w, cur);
+        cur = ggml_add(ctx, cur, L.c_attn_proj_b);
+        cur = ggml_add(ctx, cur, inpL);
+        ggml_tensor * inpFF = cur;
+
+        cur = ggml_norm(ctx, inpFF, hp.eps);
+        cur = ggml_add(ctx, ggml_mul(ctx, cur, L.ln_2_g), L.ln_2_b);
+        cur = ggml_mul_mat(ctx, L.c_mlp_fc_w, cur);
+        cur = ggml_add(ctx, cur, L.c_mlp_fc_b);
+        cur = ggml_gelu(ctx, cur);
+        cur = ggml_mul_mat(ctx, L.c_mlp_proj_w, cur);
+        cur = ggml_add(ctx, cur, L.c_mlp_proj_b);
+
+        inpL = ggml_add(ctx, cur, inpFF);
+    }
+
+    inpL = ggml_norm(ctx, inpL, hp.eps);
+    inpL = ggml_add(ctx, ggml_mul(ctx, inpL, m.ln_f_g), m.ln_f_b);
+    inpL = ggml_mul_mat(ctx, m.lm_head, inpL);
+    ggml_set_name(inpL, "logits");
+    ggml_set_output(inpL);
+    ggml_build_forward_expand(gf, inpL);
+    ggml_free(ctx);  // the context memory is graph_buf; the graph stays valid until the next build
+    return gf;
+}
+
+void split_words(std::string str, std::vector<std::string> & words) {
+    // examples/common.cpp:272-283
+    static const std::regex re(R"('s|'t|'re|'ve|'m|'ll|'d| ?[[:alpha:]]+| ?[[:digit:]]+| ?[^\s[:alpha:][:digit:]]+|\s+(?!\S)|\s+)");
+    std::smatch sm;
+    while (std::regex_search(str, sm, re)) {
+        for (auto x : sm) words.push_back(x);
+        str = sm.suffix();
+    }
+}
+
+} // namespace
+
+extern "C" {
+
+gpt2_model * gpt2_model_load(const char * fname, ggml_backend_t backend, int n_ctx, int n_batch) {
+    if (!backend) {
+        fprintf(stderr, "gpt2_model_load: no backend\n");
+        return nullptr;
+    }
+    auto * m = new gpt2_model();
+    m->backend = backend;
+    if (!load_file(*m, fname, n_ctx)) {
+        gpt2_model_free(m);
+        return nullptr;
+    }
+    m->allocr = ggml_gallocr_new(ggml_backend_get_default_buffer_type(backend));
+    const int n_tokens = std::min(m->hp.n_ctx, n_batch > 0 ? n_batch : 8);
+    ggml_cgraph * gf = build_graph(*m, m->hp.n_ctx - n_tokens, n_tokens);
+    if (!ggml_gallocr_reserve(m->allocr, gf)) {
+        fprintf(stderr, "gpt2_model_load: compute buffer reservation failed\n");
+        gpt2_model_free(m);
+        return nullptr;
+    }
+    return m;
+}
+
+void gpt2_model_free(gpt2_model * m) {
+    if (!m) return;
+    if (m->allocr) ggml_gallocr_free(m->allocr);
+    if (m->buffer_w) ggml_backend_buffer_free(m->buffer_w);
+    if (m->buffer_kv) ggml_backend_buffer_free(m->buffer_kv);
+    if (m->ctx_w) ggml_free(m->ctx_w);
+    if (m->ctx_kv) ggml_free(m->ctx_kv);
+    delete m;
+}
+
+void gpt2_model_hparams(const gpt2_model * m, gpt2_hparams_c * out) { *out = m->hp; }
+size_t gpt2_model_size(const gpt2_model * m) { return m->weight_bytes; }
+size_t gpt2_compute_buffer_size(const gpt2_model * m) { return ggml_gallocr_get_buffer_size(m->allocr, 0); }
+
+int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float * logits, int all_logits) {
+    // positions index wpe, which has the file's context length even when the KV cache is larger
+    if (N <= 0 || n_past < 0 || n_past + N > m->hp.n_ctx || n_past + N > m->wpe->ne[1]) {
+        fprintf(stderr, "gpt2_eval: bad token range (n_past %d, n_tokens %d, n_ctx %d, wpe rows %d)\n", n_past, N,
+                m->hp.n_ctx, (int) m->wpe->ne[1]);
+        return 1;
+    }
+    for (int i = 0; i < N; i++) {
+        if (tokens[i] < 0 || tokens[i] >= m->hp.n_vocab) {
+            fprintf(stderr, "gpt2_eval: token %d out of range\n", tokens[i]);
+            return 1;
+        }
+    }
+    const int64_t t0 = now_us();
+    ggml_cgraph * gf = build_graph(*m, n_past, N);
+    const int64_t t1 = now_us();
+    if (!ggml_gallocr_alloc_graph(m->allocr, gf)) {
+        fprintf(stderr, "gpt2_eval: graph allocation failed\n");
+        return 1;
+    }
+    ggml_tensor * embd = ggml_graph_get_tensor(gf, "embd");
+    ggml_backend_tensor_set(embd, tokens, 0, (size_t) N * ggml_element_size(embd));
+    ggml_tensor * position = ggml_graph_get_tensor(gf, "position");
+    std::vector<int32_t> pos(N);
+    for (int i = 0; i < N; i++) pos[i] = n_past + i;
+    ggml_backend_tensor_set(position, pos.data(), 0, (size_t) N * sizeof(int32_t));
+    const int64_t t2 = now_us();
+    if (ggml_backend_graph_compute(m->backend, gf) != GGML_STATUS_SUCCESS) {
+        fprintf(stderr, "gpt2_eval: graph compute failed\n");
+        return 1;
+    }
+    ggml_tensor * out = ggml_graph_get_tensor(gf, "logits");
+    const size_t nv = (size_t) m->hp.n_vocab;
+    if (all_logits) ggml_backend_tensor_get(out, logits, 0, sizeof(float) * nv * N);
+    else ggml_backend_tensor_get(out, logits, sizeof(float) * nv * (N - 1), sizeof(float) * nv);
+    const int64_t t3 = now_us();
+    m->last_nodes = gf->n_nodes;
+    m->us_build = t1 - t0;
+    m->us_alloc = t2 - t1;
+    m->us_compute = t3 - t2;
+    return 0;
+}
+
+const char * gpt2_token_text(const gpt2_model * m, int32_t id) {
+    if (id < 0 || id >= (int32_t) m->vocab.id_to_token.size()) return nullptr;
+    return m->vocab.id_to_token[id].c_str();
+}
+
+int gpt2_tokenize(const gpt2_model * m, const char * text, int32_t * out, int max_tokens) {
+    std::vector<std::string> words;
+    split_words(text, words);
+    // longest vocabulary prefix at each position (examples/common.cpp:322-340)
+    int n = 0;
+    for (const auto & w : words) {
+        for (int i = 0; i < (int) w.size();) {
+            for (int j = (int) w.size() - 1; j >= i; j--) {
+                auto it = m->vocab.token_to_id.find(w.substr(i, j - i + 1));
+                if (it != m->vocab.token_to_id.end()) {
+                    if (n < max_tokens) out[n] = it->second;
+                    n++;
+                    i = j + 1;
+                    break;
+                } else if (j == i) {
+                    fprintf(stderr, "gpt2_tokenize: unknown token '%s'\n", w.substr(i, 1).c_str());
+                    i++;
+                }
+            }
+        }
+    }
+    return n;
+}
+
+void gpt2_last_eval_stats(const gpt2_model * m, int * n_nodes, int64_t * us_build, int64_t * us_alloc, int64_t * us_compute) {
+    if (n_nodes) *n_nodes = m->last_nodes;
+    if (us_build) *us_build = m->us_build;
+    if (us_alloc) *us_alloc = m->us_alloc;
+    if (us_compute) *us_compute = m->us_compute;
+}
+
+} // extern "C"

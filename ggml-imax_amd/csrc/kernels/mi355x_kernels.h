@@ -86,6 +86,27 @@ bool mi_mmq_supported(int type, int64_t K, size_t nb01, size_t ycol);
 void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_q8 & act, const uint16_t * xh,
                     int64_t ncols, float * dst, size_t ycol, hipStream_t s);
 
+// ---- companion ops (ops.hip) ----
+// a tensor view as the element-wise kernels see it: f32 (type 0), f16 (1) or i32 (26) elements
+struct mi_tensor_desc {
+    char * data;
+    int type;
+    int64_t ne[4];
+    size_t nb[4];
+};
+enum mi_elt_op { MI_OP_ADD, MI_OP_MUL, MI_OP_SUB, MI_OP_DIV, MI_OP_SCALE, MI_OP_GELU, MI_OP_SILU, MI_OP_CPY };
+void mi_op_binary(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & b, int op, hipStream_t s);
+void mi_op_unary(const mi_tensor_desc & d, const mi_tensor_desc & a, int op, float p0, const uint16_t * table, hipStream_t s);
+void mi_op_cpy(const mi_tensor_desc & d, const mi_tensor_desc & a, hipStream_t s);
+void mi_op_get_rows(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & idx, hipStream_t s);
+void mi_op_diag_mask(const mi_tensor_desc & d, const mi_tensor_desc & a, int n_past, float value, hipStream_t s);
+void mi_op_norm(const mi_tensor_desc & d, const mi_tensor_desc & a, float eps, bool rms, hipStream_t s);
+// rope f32 forward, modes 0/2; corr = ggml_rope_yarn_corr_dims() computed on the host
+void mi_op_rope(const mi_tensor_desc & d, const mi_tensor_desc & a, const int32_t * pos, int n_dims, int mode, float freq_base,
+                float freq_scale, float ext_factor, float attn_factor, float corr0, float corr1, hipStream_t s);
+void mi_op_soft_max(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & mask, float scale,
+                    const uint16_t * exp_table, hipStream_t s);
+
 // f16 weights x f16-rounded activations
 void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s);
 // f32 x f32, both operands arbitrarily strided (src1 described by x, src0 by m.nb0x)

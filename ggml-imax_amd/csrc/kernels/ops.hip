@@ -1,0 +1,359 @@
+// ops.hip -- the non-matmul ops of the GPT-2 / LLaMA-style graphs on gfx950.
+//
+// All are memory- or launch-bound. Each follows the reference CPU forward's rounding sequence so
+// that results are bit-identical where the CPU order is reproducible:
+//   get_rows   src/ggml.c:12920 (f16) / :13006 (f32)       -- exact
+//   add / mul  src/ggml.c:8568 / :9687 (broadcast src1)      -- exact
+//   scale      src/ggml.c:12637                              -- exact
+//   norm       src/ggml.c:11353-11406 (double sums)          -- sums in double, then the same f32 ops
+//   rms_norm   src/ggml.c:11428-11478 (double sums)
+//   soft_max   src/ggml.c:13393-13508 (fp16 exp table, double sum, y *= (float)(1/sum))
+//   diag_mask  src/ggml.c:13301-13390
+//   gelu/silu  src/ggml.c:1966-1991 (fp16 lookup tables, built on the host with libm like the
+//              reference's ggml_init, src/ggml.c:2884-2898)
+//   rope       src/ggml.c:13719-13948 (modes 0 and 2)
+//   cpy/cont/dup src/ggml.c:8062, :12818 -- element i of src (row-major logical order) to
+//              element i of dst, with f32/f16 conversion (RNE)
+
+#include "mi355x_common.h"
+#include "mi355x_kernels.h"
+
+namespace {
+
+__device__ __forceinline__ void unflatten(int64_t i, const int64_t * ne, int64_t & i0, int64_t & i1, int64_t & i2, int64_t & i3) {
+    i0 = i % ne[0];
+    i /= ne[0];
+    i1 = i % ne[1];
+    i /= ne[1];
+    i2 = i % ne[2];
+    i3 = i / ne[2];
+}
+
+__device__ __forceinline__ size_t off4(const size_t * nb, int64_t i0, int64_t i1, int64_t i2, int64_t i3) {
+    return (size_t) i0 * nb[0] + (size_t) i1 * nb[1] + (size_t) i2 * nb[2] + (size_t) i3 * nb[3];
+}
+
+__device__ __forceinline__ float ld_f(const char * p, int type) {
+    return type == 1 ? mi_h2f(*(const uint16_t *) p) : *(const float *) p;
+}
+
+__device__ __forceinline__ void st_f(char * p, int type, float v) {
+    if (type == 1) *(uint16_t *) p = mi_f2h(v);
+    else *(float *) p = v;
+}
+
+// ---- element-wise ----------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_binary(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc b, int op, int64_t n) {
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        int64_t i0, i1, i2, i3;
+        unflatten(i, d.ne, i0, i1, i2, i3);
+        const float x = ld_f(a.data + off4(a.nb, i0, i1, i2, i3), a.type);
+        const float y = ld_f(b.data + off4(b.nb, i0 % b.ne[0], i1 % b.ne[1], i2 % b.ne[2], i3 % b.ne[3]), b.type);
+        float r;
+        switch (op) {
+            case MI_OP_ADD: r = x + y; break;
+            case MI_OP_MUL: r = x * y; break;
+            case MI_OP_SUB: r = x - y; break;
+            default: r = x / y; break;
+        }
+        st_f(d.data + off4(d.nb, i0, i1, i2, i3), d.type, r);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_unary(mi_tensor_desc d, mi_tensor_desc a, int op, float p0, const uint16_t * table, int64_t n) {
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        int64_t i0, i1, i2, i3;
+        unflatten(i, d.ne, i0, i1, i2, i3);
+        const float x = ld_f(a.data + off4(a.nb, i0, i1, i2, i3), a.type);
+        float r;
+        switch (op) {
+            case MI_OP_SCALE: r = x * p0; break;
+            case MI_OP_GELU:  // ggml_vec_gelu_f32 with GGML_GELU_FP16 (src/ggml.c:1978-1991)
+                r = x <= -10.0f ? 0.0f : (x >= 10.0f ? x : mi_h2f(table[mi_f2h(x)]));
+                break;
+            case MI_OP_SILU:  // ggml_vec_silu_f32 with GGML_SILU_FP16: table[fp16(x)]
+                r = mi_h2f(table[mi_f2h(x)]);
+                break;
+            case MI_OP_CPY:
+            default: r = x; break;
+        }
+        st_f(d.data + off4(d.nb, i0, i1, i2, i3), d.type, r);
+    }
+}
+
+// element i of src (in src's logical order) -> element i of dst (dst's logical order)
+__global__ __launch_bounds__(256) void k_cpy(mi_tensor_desc d, mi_tensor_desc a, int64_t n) {
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        int64_t i0, i1, i2, i3, j0, j1, j2, j3;
+        unflatten(i, a.ne, i0, i1, i2, i3);
+        unflatten(i, d.ne, j0, j1, j2, j3);
+        const char * sp = a.data + off4(a.nb, i0, i1, i2, i3);
+        char * dp = d.data + off4(d.nb, j0, j1, j2, j3);
+        if (a.type == d.type && a.type == 1) *(uint16_t *) dp = *(const uint16_t *) sp;
+        else st_f(dp, d.type, ld_f(sp, a.type));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_get_rows(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc idx, int64_t n) {
+    // dst row (i10, i11, i12) = src0 row (src1[i10, i11, i12], i11, i12)
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        const int64_t c = i % d.ne[0];
+        int64_t r = i / d.ne[0];
+        const int64_t i10 = r % idx.ne[0];
+        r /= idx.ne[0];
+        const int64_t i11 = r % idx.ne[1];
+        const int64_t i12 = r / idx.ne[1];
+        const int32_t i01 = *(const int32_t *) (idx.data + i10 * idx.nb[0] + i11 * idx.nb[1] + i12 * idx.nb[2]);
+        const float v = ld_f(a.data + c * a.nb[0] + (size_t) i01 * a.nb[1] + i11 * a.nb[2] + i12 * a.nb[3], a.type);
+        st_f(d.data + c * d.nb[0] + i10 * d.nb[1] + i11 * d.nb[2] + i12 * d.nb[3], d.type, v);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_diag_mask(mi_tensor_desc d, mi_tensor_desc a, int n_past, float value, int64_t n) {
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        int64_t i0, i1, i2, i3;
+        unflatten(i, d.ne, i0, i1, i2, i3);
+        float v = *(const float *) (a.data + off4(a.nb, i0, i1, i2, i3));
+        if (i0 >= n_past && i0 > n_past + i1) v = value;
+        *(float *) (d.data + off4(d.nb, i0, i1, i2, i3)) = v;
+    }
+}
+
+// ---- row reductions: one 256-thread workgroup per row ----------------------------------------
+
+__device__ __forceinline__ double block_sum_d(double v, double * sh) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) sh[wave] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int w = 0; w < (int) (blockDim.x >> 6); w++) t += sh[w];
+    return t;
+}
+
+__device__ __forceinline__ float block_max_f(float v, float * sh) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) sh[wave] = v;
+    __syncthreads();
+    float t = -INFINITY;
+    for (int w = 0; w < (int) (blockDim.x >> 6); w++) t = fmaxf(t, sh[w]);
+    return t;
+}
+
+// rows of src0 / dst are addressed by (i1, i2, i3); elements along ne0 with stride nb[0]
+__device__ __forceinline__ void row_coords(int64_t r, const int64_t * ne, int64_t & i1, int64_t & i2, int64_t & i3) {
+    i1 = r % ne[1];
+    r /= ne[1];
+    i2 = r % ne[2];
+    i3 = r / ne[2];
+}
+
+__global__ __launch_bounds__(256) void k_norm(mi_tensor_desc d, mi_tensor_desc a, float eps, int rms) {
+    __shared__ double shd[4];
+    int64_t i1, i2, i3;
+    row_coords(blockIdx.x, a.ne, i1, i2, i3);
+    const char * x = a.data + off4(a.nb, 0, i1, i2, i3);
+    char * y = d.data + off4(d.nb, 0, i1, i2, i3);
+    const int64_t n = a.ne[0];
+    if (rms) {
+        // src/ggml.c:11428-11478: sum(x*x) in double, mean, scale = 1/sqrtf(mean + eps)
+        double s = 0.0;
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const float v = *(const float *) (x + i * a.nb[0]);
+            s += (double) (v * v);
+        }
+        s = block_sum_d(s, shd);
+        const float mean = (float) (s / n);
+        const float scale = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(mean, eps)));
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            *(float *) (y + i * d.nb[0]) = *(const float *) (x + i * a.nb[0]) * scale;
+        }
+        return;
+    }
+    // src/ggml.c:11353-11406: mean in double -> float; v = x - mean; sum(v*v) in double
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += (double) *(const float *) (x + i * a.nb[0]);
+    s = block_sum_d(s, shd);
+    const float mean = (float) (s / n);
+    double s2 = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const float v = *(const float *) (x + i * a.nb[0]) - mean;
+        s2 += (double) (v * v);
+    }
+    s2 = block_sum_d(s2, shd);
+    const float variance = (float) (s2 / n);
+    const float scale = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(variance, eps)));
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const float v = *(const float *) (x + i * a.nb[0]) - mean;
+        *(float *) (y + i * d.nb[0]) = v * scale;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_soft_max(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc mask, float scale,
+                                                  const uint16_t * exp_table) {
+    __shared__ double shd[4];
+    __shared__ float shf[4];
+    int64_t i1, i2, i3;
+    row_coords(blockIdx.x, a.ne, i1, i2, i3);
+    const char * x = a.data + off4(a.nb, 0, i1, i2, i3);
+    char * y = d.data + off4(d.nb, 0, i1, i2, i3);
+    const int64_t n = a.ne[0];
+    // the mask row is broadcast over rows: (i1 % mask.ne1), as (i1 % ne01) in the reference
+    const char * mrow = mask.data ? mask.data + (size_t) (blockIdx.x % a.ne[1]) * mask.nb[1] : nullptr;
+    auto w_of = [&](int64_t i) {
+        // wp = x*scale; wp += slope*mask (two roundings, no contraction; slope = 1 as max_bias = 0)
+        float w = __fmul_rn(*(const float *) (x + i * a.nb[0]), scale);
+        if (mrow) w = __fadd_rn(w, ld_f(mrow + i * mask.nb[0], mask.type));
+        return w;
+    };
+    float mx = -INFINITY;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) mx = fmaxf(mx, w_of(i));
+    mx = block_max_f(mx, shf);
+    double sum = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const float w = w_of(i);
+        float val = 0.0f;
+        if (w != -INFINITY) {
+            val = mi_h2f(exp_table[mi_f2h(w - mx)]);
+            sum += (double) val;
+        }
+        *(float *) (y + i * d.nb[0]) = val;
+    }
+    sum = block_sum_d(sum, shd);
+    const float inv = (float) (1.0 / sum);
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) *(float *) (y + i * d.nb[0]) *= inv;
+}
+
+// rope f32 (src/ggml.c:13719-13948), modes 0 (adjacent pairs) and 2 (neox halves), forward.
+// One thread per rotated pair. theta follows the reference's running product theta *= theta_scale
+// (so each thread replays k multiplications), and cos/sin are rounded from double so they match a
+// correctly rounded libm.
+struct mi_rope_params {
+    int n_dims, mode;
+    float freq_scale, ext_factor, attn_factor, theta_scale, inv_ndims, corr0, corr1;
+};
+
+__device__ __forceinline__ void rope_yarn_dev(float theta_extrap, const mi_rope_params & r, int64_t i0, float & c, float & s) {
+    const float theta_interp = __fmul_rn(r.freq_scale, theta_extrap);
+    float theta = theta_interp;
+    float mscale = r.attn_factor;
+    if (r.ext_factor != 0.0f) {
+        const float y = ((float) (i0 / 2) - r.corr0) / fmaxf(0.001f, r.corr1 - r.corr0);
+        const float ramp_mix = (1.0f - fminf(1.0f, fmaxf(0.0f, y))) * r.ext_factor;
+        theta = __fadd_rn(__fmul_rn(theta_interp, 1.0f - ramp_mix), __fmul_rn(theta_extrap, ramp_mix));
+        mscale *= 1.0f + 0.1f * (float) log(1.0 / (double) r.freq_scale);
+    }
+    c = __fmul_rn((float) cos((double) theta), mscale);
+    s = __fmul_rn((float) sin((double) theta), mscale);
+}
+
+__global__ __launch_bounds__(256) void k_rope(mi_tensor_desc d, mi_tensor_desc a, const int32_t * pos, mi_rope_params r) {
+    const int64_t pairs = a.ne[0] / 2;
+    const int64_t nrows = a.ne[1] * a.ne[2] * a.ne[3];
+    const int64_t total = pairs * nrows;
+    for (int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t) gridDim.x * blockDim.x) {
+        const int64_t k = t % pairs;
+        int64_t row = t / pairs;
+        const int64_t i1 = row % a.ne[1];
+        row /= a.ne[1];
+        const int64_t i2 = row % a.ne[2];
+        const int64_t i3 = row / a.ne[2];
+        const float p = (float) pos[i2];
+        const char * src = a.data + off4(a.nb, 0, i1, i2, i3);
+        char * dst = d.data + off4(d.nb, 0, i1, i2, i3);
+        if (r.mode == 0) {
+            float theta = p;
+            for (int64_t j = 0; j < k; j++) theta = __fmul_rn(theta, r.theta_scale);
+            float c, s;
+            rope_yarn_dev(theta, r, 2 * k, c, s);
+            const float x0 = *(const float *) (src + 2 * k * a.nb[0]);
+            const float x1 = *(const float *) (src + (2 * k + 1) * a.nb[0]);
+            *(float *) (dst + 2 * k * d.nb[0]) = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s));
+            *(float *) (dst + (2 * k + 1) * d.nb[0]) = __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c));
+        } else {
+            const int64_t ic = 2 * k;
+            if (ic < r.n_dims) {
+                float theta = __fmul_rn(p, r.freq_scale);
+                for (int64_t j = 0; j < k; j++) theta = __fmul_rn(theta, r.theta_scale);
+                const float cur_rot = __fmul_rn(r.inv_ndims, (float) ic);
+                float c, s;
+                rope_yarn_dev(theta, r, (int64_t) cur_rot, c, s);
+                const int64_t i0 = ic / 2;
+                const int64_t h = r.n_dims / 2;
+                const float x0 = *(const float *) (src + i0 * a.nb[0]);
+                const float x1 = *(const float *) (src + (i0 + h) * a.nb[0]);
+                *(float *) (dst + i0 * d.nb[0]) = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s));
+                *(float *) (dst + (i0 + h) * d.nb[0]) = __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c));
+            } else {
+                *(float *) (dst + ic * d.nb[0]) = *(const float *) (src + ic * a.nb[0]);
+                *(float *) (dst + (ic + 1) * d.nb[0]) = *(const float *) (src + (ic + 1) * a.nb[0]);
+            }
+        }
+    }
+}
+
+unsigned grid_for(int64_t n) {
+    int64_t g = (n + 255) / 256;
+    return (unsigned) (g > 65536 ? 65536 : (g < 1 ? 1 : g));
+}
+
+} // namespace
+
+void mi_op_binary(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & b, int op, hipStream_t s) {
+    const int64_t n = d.ne[0] * d.ne[1] * d.ne[2] * d.ne[3];
+    hipLaunchKernelGGL(k_binary, dim3(grid_for(n)), dim3(256), 0, s, d, a, b, op, n);
+}
+
+void mi_op_unary(const mi_tensor_desc & d, const mi_tensor_desc & a, int op, float p0, const uint16_t * table, hipStream_t s) {
+    const int64_t n = d.ne[0] * d.ne[1] * d.ne[2] * d.ne[3];
+    hipLaunchKernelGGL(k_unary, dim3(grid_for(n)), dim3(256), 0, s, d, a, op, p0, table, n);
+}
+
+void mi_op_cpy(const mi_tensor_desc & d, const mi_tensor_desc & a, hipStream_t s) {
+    const int64_t n = a.ne[0] * a.ne[1] * a.ne[2] * a.ne[3];
+    hipLaunchKernelGGL(k_cpy, dim3(grid_for(n)), dim3(256), 0, s, d, a, n);
+}
+
+void mi_op_get_rows(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & idx, hipStream_t s) {
+    const int64_t n = d.ne[0] * d.ne[1] * d.ne[2] * d.ne[3];
+    hipLaunchKernelGGL(k_get_rows, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n);
+}
+
+void mi_op_diag_mask(const mi_tensor_desc & d, const mi_tensor_desc & a, int n_past, float value, hipStream_t s) {
+    const int64_t n = d.ne[0] * d.ne[1] * d.ne[2] * d.ne[3];
+    hipLaunchKernelGGL(k_diag_mask, dim3(grid_for(n)), dim3(256), 0, s, d, a, n_past, value, n);
+}
+
+void mi_op_norm(const mi_tensor_desc & d, const mi_tensor_desc & a, float eps, bool rms, hipStream_t s) {
+    const int64_t rows = a.ne[1] * a.ne[2] * a.ne[3];
+    hipLaunchKernelGGL(k_norm, dim3((unsigned) rows), dim3(256), 0, s, d, a, eps, rms ? 1 : 0);
+}
+
+void mi_op_soft_max(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & mask, float scale,
+                    const uint16_t * exp_table, hipStream_t s) {
+    const int64_t rows = a.ne[1] * a.ne[2] * a.ne[3];
+    hipLaunchKernelGGL(k_soft_max, dim3((unsigned) rows), dim3(256), 0, s, d, a, mask, scale, exp_table);
+}
+
+void mi_op_rope(const mi_tensor_desc & d, const mi_tensor_desc & a, const int32_t * pos, int n_dims, int mode, float freq_base,
+                float freq_scale, float ext_factor, float attn_factor, float corr0, float corr1, hipStream_t s) {
+    mi_rope_params r;
+    r.n_dims = n_dims;
+    r.mode = mode;
+    r.freq_scale = freq_scale;
+    r.ext_factor = ext_factor;
+    r.attn_factor = attn_factor;
+    r.theta_scale = powf(freq_base, -2.0f / n_dims);
+    r.inv_ndims = -1.f / n_dims;
+    r.corr0 = corr0;
+    r.corr1 = corr1;
+    const int64_t n = a.ne[0] / 2 * a.ne[1] * a.ne[2] * a.ne[3];
+    hipLaunchKernelGGL(k_rope, dim3(grid_for(n)), dim3(256), 0, s, d, a, pos, r);
+}

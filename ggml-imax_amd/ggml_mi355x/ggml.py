@@ -19,6 +19,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_ROOT, "lib")
 CORE_LIB = os.path.join(LIB_DIR, "libggml_core.so")
 BACKEND_LIB = os.path.join(LIB_DIR, "libggml_mi355x.so")
+GPT2_LIB = os.path.join(LIB_DIR, "libgpt2_mi355x.so")
 
 # enum ggml_type (include/ggml/ggml.h:348-381)
 GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
@@ -163,6 +164,16 @@ _SIGS = {
     "ggml_backend_mi355x_last_launch_count": ([c_void_p], c_int),
     "ggml_backend_mi355x_set_tuning": ([c_char_p, c_int], c_bool),
     "ggml_backend_mi355x_quantize_activations": ([c_void_p, c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p], c_bool),
+    # GPT-2 driver (include/gpt2-mi355x.h)
+    "gpt2_model_load": ([c_char_p, c_void_p, c_int, c_int], c_void_p),
+    "gpt2_model_free": ([c_void_p], None),
+    "gpt2_model_hparams": ([c_void_p, c_void_p], None),
+    "gpt2_model_size": ([c_void_p], c_size_t),
+    "gpt2_compute_buffer_size": ([c_void_p], c_size_t),
+    "gpt2_eval": ([c_void_p, c_int, c_void_p, c_int, c_void_p, c_int], c_int),
+    "gpt2_token_text": ([c_void_p, c_int32], c_char_p),
+    "gpt2_tokenize": ([c_void_p, c_char_p, c_void_p, c_int], c_int),
+    "gpt2_last_eval_stats": ([c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], None),
 }
 
 BACKEND_EXPORTS = [k for k in _SIGS if k.startswith("ggml_backend_mi355x") or k == "ggml_backend_is_mi355x"]
@@ -204,10 +215,10 @@ def runtime() -> Lib:
     """The MI355X runtime (core + backend). Fails loudly if it has not been built."""
     global _runtime
     if _runtime is None:
-        for p in (CORE_LIB, BACKEND_LIB):
+        for p in (CORE_LIB, BACKEND_LIB, GPT2_LIB):
             if not os.path.exists(p):
                 raise RuntimeError(f"{p} missing: run `make -C ggml-imax_amd` (or __graft_entry__.build())")
-        _runtime = Lib([CORE_LIB, BACKEND_LIB])
+        _runtime = Lib([CORE_LIB, BACKEND_LIB, GPT2_LIB])
     return _runtime
 
 

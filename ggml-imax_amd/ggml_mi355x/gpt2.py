@@ -1,0 +1,184 @@
+"""GPT-2 (BASELINE config 4): synthetic GPT-2-117M model files and a wrapper over include/gpt2-mi355x.h.
+
+No GPT-2 weights exist offline (the reference's download scripts need network), so models are
+synthetic and seeded, written in the legacy ggml format that examples/gpt-2/main-backend.cpp:101-439
+loads -- the layout examples/gpt-2/convert-ckpt-to-ggml.py:91-151 produces: magic, 6 int32 hparams,
+vocab (len + bytes), then per tensor (n_dims, name length, ftype, ne[0..], name, data), with "model/wte"
+and every ".../w" matrix in f16 and everything else f32. At 117M shapes the file holds 239.08 MB of
+tensor data, the figure the reference prints for the real model.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+
+import numpy as np
+
+from . import ggml as G
+
+GPT2_117M = dict(n_vocab=50257, n_ctx=1024, n_embd=768, n_head=12, n_layer=12)
+EOT = 50256
+
+
+class gpt2_hparams_c(ctypes.Structure):
+    _fields_ = [("n_vocab", ctypes.c_int32), ("n_ctx", ctypes.c_int32), ("n_embd", ctypes.c_int32),
+                ("n_head", ctypes.c_int32), ("n_layer", ctypes.c_int32), ("ftype", ctypes.c_int32),
+                ("eps", ctypes.c_float)]
+
+
+def synthetic_vocab(n_vocab: int, seed: int = 0) -> list[bytes]:
+    """Deterministic GPT-2-like vocabulary: printable bytes, ' '+char, then syllable words with and
+    without a leading space; the last id is <|endoftext|>."""
+    rng = np.random.default_rng(seed)
+    toks: list[bytes] = []
+    seen = set()
+
+    def add(t: bytes):
+        if t not in seen and len(toks) < n_vocab - 1:
+            seen.add(t)
+            toks.append(t)
+
+    for c in range(32, 127):
+        add(bytes([c]))
+    add(b"\n")
+    for c in b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789":
+        add(b" " + bytes([c]))
+    cons = [b"b", b"c", b"d", b"f", b"g", b"h", b"k", b"l", b"m", b"n", b"p", b"r", b"s", b"t", b"v", b"w",
+            b"th", b"st", b"ch", b"sh", b"tr", b"pl"]
+    vows = [b"a", b"e", b"i", b"o", b"u", b"ea", b"ou", b"y"]
+    while len(toks) < n_vocab - 1:
+        ns = int(rng.integers(1, 4))
+        w = b"".join(cons[int(rng.integers(len(cons)))] + vows[int(rng.integers(len(vows)))] for _ in range(ns))
+        if rng.random() < 0.3:
+            w += cons[int(rng.integers(len(cons)))]
+        add((b" " + w) if rng.random() < 0.6 else w)
+    toks.append(b"<|endoftext|>")
+    return toks
+
+
+def write_synthetic_model(path: str, seed: int = 117, ftype: int = 1, **hp) -> str:
+    """Write a seeded GPT-2 model (default 117M shapes) in the legacy ggml format; returns path.
+
+    Init follows GPT-2's: N(0, 0.02) matrices and embeddings, residual projections scaled by
+    1/sqrt(2*n_layer), layer norms near (1, 0), small biases.
+    """
+    h = dict(GPT2_117M)
+    h.update(hp)
+    E, L, V, C = h["n_embd"], h["n_layer"], h["n_vocab"], h["n_ctx"]
+    rng = np.random.default_rng(seed)
+    vocab = synthetic_vocab(V, seed)
+    tmp = path + ".tmp"
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(tmp, "wb") as f:
+        f.write(struct.pack("i", 0x67676D6C))
+        for k in ("n_vocab", "n_ctx", "n_embd", "n_head", "n_layer"):
+            f.write(struct.pack("i", h[k]))
+        f.write(struct.pack("i", ftype))
+        f.write(struct.pack("i", V))
+        for t in vocab:
+            f.write(struct.pack("i", len(t)))
+            f.write(t)
+
+        def tensor(name: str, data: np.ndarray):
+            is_mat = name == "model/wte" or name.endswith("/w")
+            cur = ftype if is_mat else 0
+            arr = data.astype(np.float16 if cur == 1 else np.float32)
+            nm = name.encode()
+            f.write(struct.pack("iii", arr.ndim, len(nm), cur))
+            for i in range(arr.ndim):
+                f.write(struct.pack("i", arr.shape[arr.ndim - 1 - i]))
+            f.write(nm)
+            arr.tofile(f)
+
+        def normal(shape, std):
+            return (rng.standard_normal(shape, dtype=np.float32) * np.float32(std))
+
+        tensor("model/wte", normal((V, E), 0.02))
+        tensor("model/wpe", normal((C, E), 0.01))
+        proj_std = 0.02 / np.sqrt(2 * L)
+        for i in range(L):
+            p = f"model/h{i}"
+            tensor(p + "/ln_1/g", 1.0 + normal((E,), 0.05))
+            tensor(p + "/ln_1/b", normal((E,), 0.02))
+            tensor(p + "/attn/c_attn/w", normal((3 * E, E), 0.02))
+            tensor(p + "/attn/c_attn/b", normal((3 * E,), 0.02))
+            tensor(p + "/attn/c_proj/w", normal((E, E), proj_std))
+            tensor(p + "/attn/c_proj/b", normal((E,), 0.02))
+            tensor(p + "/ln_2/g", 1.0 + normal((E,), 0.05))
+            tensor(p + "/ln_2/b", normal((E,), 0.02))
+            tensor(p + "/mlp/c_fc/w", normal((4 * E, E), 0.02))
+            tensor(p + "/mlp/c_fc/b", normal((4 * E,), 0.02))
+            tensor(p + "/mlp/c_proj/w", normal((E, 4 * E), proj_std))
+            tensor(p + "/mlp/c_proj/b", normal((E,), 0.02))
+        tensor("model/ln_f/g", 1.0 + normal((E,), 0.05))
+        tensor("model/ln_f/b", normal((E,), 0.02))
+    os.replace(tmp, path)
+    return path
+
+
+def default_model_path() -> str:
+    root = os.environ.get("GRAFT_REPO_ROOT") or os.path.dirname(G.PKG_ROOT)
+    return os.path.join(root, "models", "gpt2-117M-synth-f16.bin")
+
+
+def ensure_model(path: str | None = None, seed: int = 117) -> str:
+    path = path or default_model_path()
+    if not os.path.exists(path):
+        write_synthetic_model(path, seed=seed)
+    return path
+
+
+class Model:
+    """One loaded GPT-2 on a backend (gpt2_model_load); eval() returns logits as numpy."""
+
+    def __init__(self, lib: G.Lib, path: str, backend, n_ctx: int = 0, n_batch: int = 8):
+        if not lib.has("gpt2_model_load"):
+            raise RuntimeError("this library set has no GPT-2 driver (lib/libgpt2_mi355x.so)")
+        self.lib = lib
+        self.backend = backend
+        self.m = lib.gpt2_model_load(path.encode(), backend, n_ctx, n_batch)
+        if not self.m:
+            raise RuntimeError(f"gpt2_model_load({path}) failed")
+        hp = gpt2_hparams_c()
+        lib.gpt2_model_hparams(self.m, ctypes.byref(hp))
+        self.hp = hp
+        self.n_vocab = hp.n_vocab
+
+    def eval(self, n_past: int, tokens, all_logits: bool = False) -> np.ndarray:
+        tok = np.ascontiguousarray(np.asarray(tokens, dtype=np.int32))
+        n = len(tok)
+        out = np.empty((n if all_logits else 1, self.n_vocab), dtype=np.float32)
+        rc = self.lib.gpt2_eval(self.m, n_past, tok.ctypes.data, n, out.ctypes.data, 1 if all_logits else 0)
+        if rc != 0:
+            raise RuntimeError("gpt2_eval failed")
+        return out
+
+    def stats(self) -> dict:
+        n = ctypes.c_int()
+        b, a, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        self.lib.gpt2_last_eval_stats(self.m, ctypes.byref(n), ctypes.byref(b), ctypes.byref(a), ctypes.byref(c))
+        return {"nodes": n.value, "us_build": b.value, "us_alloc": a.value, "us_compute": c.value}
+
+    def tokenize(self, text: str) -> list[int]:
+        buf = np.empty(4096, dtype=np.int32)
+        n = self.lib.gpt2_tokenize(self.m, text.encode(), buf.ctypes.data, len(buf))
+        return buf[:min(n, len(buf))].tolist()
+
+    def token_text(self, i: int) -> bytes:
+        return self.lib.gpt2_token_text(self.m, i)
+
+    @property
+    def weight_bytes(self) -> int:
+        return self.lib.gpt2_model_size(self.m)
+
+    def free(self):
+        if self.m:
+            self.lib.gpt2_model_free(self.m)
+            self.m = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

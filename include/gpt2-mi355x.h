@@ -1,0 +1,54 @@
+// gpt2-mi355x.h -- GPT-2 decode driver over the ggml backend API (BASELINE config 4).
+//
+// The model code of examples/gpt-2/main-backend.cpp (NAIST-Archlab/ggml-imax) as a C library:
+// the same legacy-ggml file format (:102-439), the same graph (gpt2_graph :442-717) and the same
+// evaluation contract (gpt2_eval :728-786), but with the backend passed in by the caller, so one
+// build runs on ggml_backend_mi355x_init(dev) and on the reference CPU backend alike.
+#pragma once
+
+#include "ggml_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct gpt2_model;
+
+struct gpt2_hparams_c {
+    int32_t n_vocab;
+    int32_t n_ctx;    // KV-cache context (the -c override, main-backend.cpp:304)
+    int32_t n_embd;
+    int32_t n_head;
+    int32_t n_layer;
+    int32_t ftype;
+    float eps;
+};
+
+// gpt2_model_load (main-backend.cpp:101): weights and KV cache in `backend`'s default buffer type,
+// and a graph allocator reserved for the worst-case graph of n_batch tokens (:832-846).
+// n_ctx <= 0 keeps the file's context. Returns NULL (with a message on stderr) on failure.
+GGML_API struct gpt2_model * gpt2_model_load(const char * fname, ggml_backend_t backend, int n_ctx, int n_batch);
+GGML_API void gpt2_model_free(struct gpt2_model * model);
+GGML_API void gpt2_model_hparams(const struct gpt2_model * model, struct gpt2_hparams_c * out);
+GGML_API size_t gpt2_model_size(const struct gpt2_model * model);   // bytes of weight data read
+GGML_API size_t gpt2_compute_buffer_size(const struct gpt2_model * model);
+
+// gpt2_eval (main-backend.cpp:728): runs n_tokens tokens at positions n_past.. and writes the
+// logits of the last token (n_vocab floats), or of all tokens (n_tokens*n_vocab) if all_logits.
+// Returns 0 on success.
+GGML_API int gpt2_eval(struct gpt2_model * model, int n_past, const int32_t * tokens, int n_tokens, float * logits,
+                       int all_logits);
+
+// the vocabulary from the model file and the word-split + longest-match tokenizer of
+// examples/common.cpp:272-329. gpt2_tokenize returns the token count (may exceed max_tokens;
+// only max_tokens are written).
+GGML_API const char * gpt2_token_text(const struct gpt2_model * model, int32_t id);
+GGML_API int gpt2_tokenize(const struct gpt2_model * model, const char * text, int32_t * out, int max_tokens);
+
+// last-evaluated graph statistics: nodes, and wall-clock microseconds of build / alloc / compute
+GGML_API void gpt2_last_eval_stats(const struct gpt2_model * model, int * n_nodes, int64_t * us_build, int64_t * us_alloc,
+                                   int64_t * us_compute);
+
+#ifdef __cplusplus
+}
+#endif

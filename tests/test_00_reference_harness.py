@@ -37,6 +37,26 @@ def test_reference_backend_ops_mul_mat():
     assert "FAIL" not in out.replace("\x1b[1;31mFAIL", "FAIL").split("Backend name: MI355X0")[1].split("backends passed")[0] or rc == 0
 
 
+# the GPT-2 / LLaMA companion ops -- every case the reference's suite
+# holds for them that our supports_op accepts (GELU/SILU f32, f16/f32 CPY/DUP/CONT, GET_ROWS f16/f32,
+# RoPE modes 0/2, soft_max without ALiBi, ...); unsupported cases are reported "not supported"
+COMPANION_OPS = ["ADD", "MUL", "SUB", "DIV", "SCALE", "NORM", "RMS_NORM", "SOFT_MAX", "DIAG_MASK_INF", "UNARY", "GET_ROWS",
+                 "CPY", "DUP", "CONT", "ROPE"]
+
+
+@pytest.mark.parametrize("op", COMPANION_OPS)
+def test_reference_backend_ops_companion(op):
+    rc, out = _run([OPS, "test", "-o", op, "-b", "MI355X0"])
+    lines = out.replace("\x1b[1;31m", "").replace("\x1b[1;32m", "").replace("\x1b[0m", "").splitlines()
+    bad = [ln for ln in lines if "FAIL" in ln]
+    ok = [ln for ln in lines if ln.rstrip().endswith("OK")]
+    print(f"{op}: {len(ok)} OK, {len(bad)} FAIL")
+    print("\n".join(bad[:40]))
+    assert "Backend name: MI355X0" in out, out[-2000:]
+    assert rc == 0 and not bad, "\n".join(bad[:40]) or out[-3000:]
+    assert ok, f"no {op} case ran on MI355X0"
+
+
 def test_reference_backend_buffer():
     rc, out = _run([BUF])
     print(out[-3000:])

@@ -1,0 +1,166 @@
+"""GPT-2-117M end to end (BASELINE config 4): synthetic seeded f16 weights.
+
+Checkers (test infrastructure, oracle/Makefile `gpt2`):
+  * oracle/_ref/gpt-2-backend -- the reference's own examples/gpt-2/main-backend.cpp, unmodified,
+    on the reference CPU backend;
+  * oracle/_ref/libgpt2_ref.so / gpt-2-mi355x-ref -- this repo's GPT-2 driver linked against the
+    reference libggml, so the reference CPU ops compute the logits.
+
+CPU tests pin the driver to the reference program (identical generated text for a seed, i.e. same
+graph, tokenizer and sampler); GPU tests compare teacher-forced MI355X logits with the reference
+CPU logits: max |d| / max |ref| <= 1e-3 per step (BASELINE north_star "logits within 1e-3").
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+from ggml_mi355x import ggml as G
+from ggml_mi355x import gpt2
+
+REF = os.path.join(REPO, "oracle", "_ref")
+REF_BIN = os.path.join(REF, "gpt-2-backend")
+OUR_REF_BIN = os.path.join(REF, "gpt-2-mi355x-ref")
+REF_GGML = os.path.join(REF, "libggml_ref.so")
+REF_GPT2 = os.path.join(REF, "libgpt2_ref.so")
+OUR_BIN = os.path.join(REPO, "ggml-imax_amd", "bin", "gpt-2-mi355x")
+
+PROMPT = "Once upon a time the cat sat on the mat and the dog"
+LOGIT_TOL = 1e-3
+
+
+@pytest.fixture(scope="module")
+def model_path():
+    return gpt2.ensure_model()
+
+
+def _text(out: str) -> str:
+    # the generated text sits between the "first 8 tokens" line and the timing block
+    body = out.split("first 8 tokens:", 1)[1].split("\n", 1)[1]
+    return body.split("main:     load time", 1)[0].strip()
+
+
+def test_synthetic_model_format(model_path):
+    size = os.path.getsize(model_path)
+    assert size > 239 * 1024 * 1024
+    with open(model_path, "rb") as f:
+        hdr = np.frombuffer(f.read(32), dtype=np.int32)
+    assert hdr[0] == 0x67676D6C
+    assert list(hdr[1:7]) == [50257, 1024, 768, 12, 12, 1]
+
+
+@pytest.mark.skipif(not (os.path.exists(REF_BIN) and os.path.exists(OUR_REF_BIN)), reason="make -C oracle gpt2")
+def test_driver_matches_reference_program(model_path):
+    """Same seed + prompt: the reference program and our driver (both on reference CPU ops) print
+    the same tokens -- our graph, tokenizer and sampler mirror examples/gpt-2 exactly."""
+    args = ["-m", model_path, "-p", PROMPT, "-n", "24", "-s", "7", "-t", "4"]
+    ref = subprocess.run([REF_BIN] + args, capture_output=True, text=True, timeout=300)
+    ours = subprocess.run([OUR_REF_BIN] + args, capture_output=True, text=True, timeout=300)
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    assert ours.returncode == 0, ours.stderr[-2000:]
+    assert "model size  =   239.08 MB" in ref.stdout
+    assert "model size  =   239.08 MB" in ours.stdout
+    t_ref, t_ours = _text(ref.stdout), _text(ours.stdout)
+    assert len(t_ref) > len(PROMPT)
+    assert t_ref == t_ours
+
+
+def _ref_model(path):
+    ref = G.Lib([REF_GGML, REF_GPT2], isolated=True)
+    be = ref.ggml_backend_cpu_init()
+    ref.ggml_backend_cpu_set_n_threads(be, min(16, os.cpu_count() or 1))
+    return ref, be, gpt2.Model(ref, path, be, n_ctx=1024, n_batch=8)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+def test_reference_driver_tokenizer_roundtrip(model_path):
+    ref, be, m = _ref_model(model_path)
+    try:
+        toks = m.tokenize(PROMPT)
+        assert len(toks) > 4
+        assert b"".join(m.token_text(t) for t in toks).decode() == PROMPT
+        logits = m.eval(0, toks[:8])
+        assert logits.shape == (1, 50257) and np.isfinite(logits).all()
+    finally:
+        m.free()
+        ref.ggml_backend_free(be)
+
+
+def _rel_err(a, b):
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+def test_gpt2_logits_match_reference_cpu(model_path):
+    """Teacher-forced: prompt in batches of 8 (the reference's n_batch), then 24 single-token
+    decode steps fed from the reference's argmax; every step's logits within 1e-3."""
+    lib = G.runtime()
+    be = G.mi355x_backend(lib)
+    ours = gpt2.Model(lib, model_path, be, n_ctx=1024, n_batch=8)
+    ref, rbe, rm = _ref_model(model_path)
+    try:
+        toks = ours.tokenize(PROMPT)
+        n_past = 0
+        errs = []
+        for i in range(0, len(toks), 8):
+            chunk = toks[i:i + 8]
+            a = ours.eval(n_past, chunk, all_logits=True)
+            b = rm.eval(n_past, chunk, all_logits=True)
+            errs.append(_rel_err(a, b))
+            n_past += len(chunk)
+        nxt = int(np.argmax(b[-1]))
+        for _ in range(24):
+            a = ours.eval(n_past, [nxt])
+            b = rm.eval(n_past, [nxt])
+            errs.append(_rel_err(a, b))
+            n_past += 1
+            nxt = int(np.argmax(b[-1]))
+        print("max rel logit error per step:", ["%.2e" % e for e in errs])
+        assert max(errs) <= LOGIT_TOL, errs
+    finally:
+        ours.free()
+        rm.free()
+        lib.ggml_backend_free(be)
+        ref.ggml_backend_free(rbe)
+
+
+@pytest.mark.gpu
+def test_gpt2_cli_on_mi355x(model_path):
+    """The product CLI (-ngl 100 runs the whole graph on MI355X) generates and reports timing."""
+    p = subprocess.run([OUR_BIN, "-m", model_path, "-p", PROMPT, "-n", "32", "-s", "7", "-ngl", "100"],
+                       capture_output=True, text=True, timeout=300)
+    print(p.stdout[-1500:], p.stderr[-1500:])
+    assert p.returncode == 0
+    assert "using MI355X0 backend" in p.stderr
+    assert "per token" in p.stdout
+
+
+@pytest.mark.gpu
+def test_gpt2_long_context_decode(model_path):
+    """Positions up to the 1024-token context: attention over long KV (strided f32 mul_mats,
+    soft_max rows of 1000+) stays finite and close to the reference at the last step."""
+    lib = G.runtime()
+    be = G.mi355x_backend(lib)
+    ours = gpt2.Model(lib, model_path, be, n_ctx=1024, n_batch=512)
+    ref, rbe, rm = _ref_model(model_path)
+    try:
+        rng = np.random.default_rng(3)
+        toks = rng.integers(0, 50257, size=1000).astype(np.int32)
+        a = ours.eval(0, toks[:512], all_logits=False)
+        b = rm.eval(0, toks[:512], all_logits=False)
+        assert _rel_err(a, b) <= LOGIT_TOL
+        a = ours.eval(512, toks[512:1000], all_logits=False)
+        b = rm.eval(512, toks[512:1000], all_logits=False)
+        assert np.isfinite(a).all()
+        assert _rel_err(a, b) <= LOGIT_TOL
+        with pytest.raises(RuntimeError):
+            ours.eval(1000, toks[:100])  # past the 1024 positions of wpe
+    finally:
+        ours.free()
+        rm.free()
+        lib.ggml_backend_free(be)
+        ref.ggml_backend_free(rbe)
