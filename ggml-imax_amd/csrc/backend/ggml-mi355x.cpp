@@ -312,7 +312,8 @@ static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
             return is_f32(a) && is_f32(op);
         case GGML_OP_NORM:
         case GGML_OP_RMS_NORM:
-            return is_f32(a) && is_f32(op) && a->nb[0] == sizeof(float);
+            // rows longer than the kernel's LDS staging (12288 floats) stage in a contiguous dst
+            return is_f32(a) && is_f32(op) && a->nb[0] == sizeof(float) && (a->ne[0] <= 12288 || ggml_is_contiguous(op));
         case GGML_OP_SOFT_MAX: {
             float max_bias;
             memcpy(&max_bias, (const float *) op->op_params + 1, sizeof(float));
@@ -511,7 +512,13 @@ static float host_h2f(uint16_t h) {
 // the reference's fp16 lookup tables (src/ggml.c:2884-2898), same formulas and libm
 static const float kGeluCoefA = 0.044715f;
 static const float kSqrt2OverPi = 0.79788456080286535587989211986876f;
-static float gelu_ref(float x) { return 0.5f * x * (1.0f + tanhf(kSqrt2OverPi * x * (1.0f + kGeluCoefA * x * x))); }
+// ggml_gelu_f32 as the reference's gcc -O3 -mfma build evaluates it (read off its ggml_init):
+// (0.5f*x) * (1 + tanhf((SQRT_2_OVER_PI*x) * fmaf(GELU_COEF_A*x, x, 1))) -- one contraction
+static float gelu_ref(float x) {
+    const float inner = fmaf(kGeluCoefA * x, x, 1.0f);
+    const float arg = (kSqrt2OverPi * x) * inner;
+    return (0.5f * x) * (1.0f + tanhf(arg));
+}
 static float silu_ref(float x) { return x / (1.0f + expf(-x)); }
 
 static const uint16_t * op_tables(mi_backend_ctx * ctx) {

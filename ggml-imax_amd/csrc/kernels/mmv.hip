@@ -14,8 +14,7 @@
 //   Q8_0 x Q8_0  ggml_vec_dot_q8_0_q8_0  src/ggml-quants.c:4819+
 //   Q4_K x Q8_K  ggml_vec_dot_q4_K_q8_K  src/ggml-quants.c:7007-7502
 //   Q5_K x Q8_K  ggml_vec_dot_q5_K_q8_K  src/ggml-quants.c:7833-8378
-//   F16  x F16   ggml_vec_dot_f16        src/ggml.c:1674-1714
-//   F32  x F32   ggml_vec_dot_f32        src/ggml.c:1567-1608
+// (F16 and F32 live in mmv_ordered.hip: bit-exact CPU summation order.)
 
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
@@ -205,72 +204,6 @@ __global__ __launch_bounds__(256) void k_mmv_q0(const uint8_t * __restrict__ W, 
     mmv_store<NC>(g, dst, row, i11, i12, i13, acc, lane);
 }
 
-// ---------------------------------------------------------------- F16 x F16
-
-typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-
-template <int NC>
-__global__ __launch_bounds__(256) void k_mmv_f16(const uint8_t * __restrict__ W, const uint16_t * __restrict__ xh, float * __restrict__ dst, mmv_geom g) {
-    const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t) blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
-    if (row >= g.N) return;
-    int64_t i11, i12, i13, i02, i03;
-    mmv_coords(g, NC, i11, i12, i13, i02, i03);
-    const uint16_t * wrow = (const uint16_t *) (W + i02 * g.nb02 + i03 * g.nb03 + row * g.nb01);
-    const int64_t col0 = i11 + g.ne11 * (i12 + g.ne12 * i13);
-    float acc[NC];
-#pragma unroll
-    for (int c = 0; c < NC; c++) acc[c] = 0.0f;
-    const int64_t nv = g.K / 8;
-    for (int64_t v = lane; v < nv; v += 64) {
-        const uint4 w4 = *(const uint4 *) (wrow + v * 8);
-        const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            if (NC > 1 && i11 + c >= g.ne11) break;
-            const uint4 x4 = *(const uint4 *) (xh + (col0 + c) * g.K + v * 8);
-            const uint32_t xv[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                h2_t a, b;
-                __builtin_memcpy(&a, &wv[i], 4);
-                __builtin_memcpy(&b, &xv[i], 4);
-                acc[c] = __builtin_amdgcn_fdot2(a, b, acc[c], false);
-            }
-        }
-    }
-    // K tail (K % 8)
-    for (int64_t k = nv * 8 + lane; k < g.K; k += 64) {
-        const float w = mi_h2f(wrow[k]);
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            if (NC > 1 && i11 + c >= g.ne11) break;
-            acc[c] += w * mi_h2f(xh[(col0 + c) * g.K + k]);
-        }
-    }
-    mmv_store<NC>(g, dst, row, i11, i12, i13, acc, lane);
-}
-
-// ---------------------------------------------------------------- F32 x F32 (strided)
-
-// one wave per output element; src1 column described by mi_src_cols (nb10 == 4)
-__global__ __launch_bounds__(256) void k_mm_f32(const uint8_t * __restrict__ W, mi_src_cols x, float * __restrict__ dst, mmv_geom g) {
-    const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t) blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
-    if (row >= g.N) return;
-    const int64_t y = blockIdx.y;
-    const int64_t i11 = y % g.ne11;
-    const int64_t z = y / g.ne11;
-    const int64_t i12 = z % g.ne12, i13 = z / g.ne12;
-    const int64_t i02 = i12 / g.r2, i03 = i13 / g.r3;
-    const float * w = (const float *) (W + i02 * g.nb02 + i03 * g.nb03 + row * g.nb01);
-    const float * xc = (const float *) (x.base + i11 * x.nb1 + i12 * x.nb2 + i13 * x.nb3);
-    float acc = 0.0f;
-    for (int64_t k = lane; k < g.K; k += 64) acc = __builtin_fmaf(w[k], xc[k], acc);
-    acc = mi_wave_sum(acc);
-    if (lane == 0) *(float *) ((char *) dst + i11 * g.nb1 + i12 * g.nb2 + i13 * g.nb3 + row * sizeof(float)) = acc;
-}
-
 mmv_geom make_geom(const mi_mm_desc & m, int NC) {
     mmv_geom g;
     g.K = m.K;
@@ -320,16 +253,4 @@ void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s) {
         case 8:  MI_MMV_SWITCH(k_mmv_q0, true); break;   // Q8_0
         default: break;
     }
-}
-
-void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s) {
-    const int nc = m.ne11 >= 5 ? 8 : (int) m.ne11;
-    const uint16_t * act_or_x = xh;
-    MI_MMV_SWITCH(k_mmv_f16);
-}
-
-void mi_mul_mat_f32(const mi_mm_desc & m, const mi_src_cols & x, hipStream_t s) {
-    const mmv_geom g = make_geom(m, 1);
-    const dim3 grid((unsigned) ((m.N + kRowsPerBlock - 1) / kRowsPerBlock), (unsigned) (m.ne11 * m.ne12 * m.ne13));
-    hipLaunchKernelGGL(k_mm_f32, grid, dim3(256), 0, s, (const uint8_t *) m.W, x, m.dst, g);
 }

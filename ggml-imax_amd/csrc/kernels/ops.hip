@@ -18,6 +18,19 @@
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
 
+// Bit-exactness with the CPU needs every multiply and add rounded separately unless written as
+// __fmaf_rn: HIP's __fmul_rn/__fadd_rn are plain operators defined in a header (so this file's
+// pragma does not reach them) that -ffp-contract=fast would fuse; mul_rn/add_rn below are
+// written under the pragma instead. (__fsqrt_rn is the approximate native sqrt; sqrtf and '/'
+// are correctly rounded under hipcc's default -fhip-fp32-correctly-rounded-divide-sqrt.)
+#pragma clang fp contract(off)
+
+namespace {
+__device__ __forceinline__ float mul_rn(float a, float b) { return a * b; }
+__device__ __forceinline__ float add_rn(float a, float b) { return a + b; }
+__device__ __forceinline__ float sub_rn(float a, float b) { return a - b; }
+} // namespace
+
 namespace {
 
 __device__ __forceinline__ void unflatten(int64_t i, const int64_t * ne, int64_t & i0, int64_t & i1, int64_t & i2, int64_t & i3) {
@@ -122,18 +135,6 @@ __global__ __launch_bounds__(256) void k_diag_mask(mi_tensor_desc d, mi_tensor_d
 
 // ---- row reductions: one 256-thread workgroup per row ----------------------------------------
 
-__device__ __forceinline__ double block_sum_d(double v, double * sh) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0) sh[wave] = v;
-    __syncthreads();
-    double t = 0.0;
-    for (int w = 0; w < (int) (blockDim.x >> 6); w++) t += sh[w];
-    return t;
-}
-
 __device__ __forceinline__ float block_max_f(float v, float * sh) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
@@ -154,81 +155,118 @@ __device__ __forceinline__ void row_coords(int64_t r, const int64_t * ne, int64_
     i3 = r / ne[2];
 }
 
-__global__ __launch_bounds__(256) void k_norm(mi_tensor_desc d, mi_tensor_desc a, float eps, int rms) {
-    __shared__ double shd[4];
-    int64_t i1, i2, i3;
-    row_coords(blockIdx.x, a.ne, i1, i2, i3);
-    const char * x = a.data + off4(a.nb, 0, i1, i2, i3);
-    char * y = d.data + off4(d.nb, 0, i1, i2, i3);
-    const int64_t n = a.ne[0];
-    if (rms) {
-        // src/ggml.c:11428-11478: sum(x*x) in double, mean, scale = 1/sqrtf(mean + eps)
-        double s = 0.0;
-        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const float v = *(const float *) (x + i * a.nb[0]);
-            s += (double) (v * v);
-        }
-        s = block_sum_d(s, shd);
-        const float mean = (float) (s / n);
-        const float scale = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(mean, eps)));
-        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-            *(float *) (y + i * d.nb[0]) = *(const float *) (x + i * a.nb[0]) * scale;
-        }
-        return;
+// The CPU accumulates row sums one element at a time in double (ggml_float); double addition is
+// not associative, so the only order that reproduces its bits is the sequential one. The row is
+// staged in a float buffer (LDS when it fits, else the dst row) and one lane runs the chain.
+// SQ: sum of (double)(v*v) with v*v rounded in float first, as the CPU writes it.
+template <bool SQ>
+__device__ __forceinline__ double seq_sum_d(const float * buf, int64_t n) {
+    double s0 = 0.0;
+    int64_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        const float4 v = *(const float4 *) (buf + i);
+        s0 += (double) (SQ ? mul_rn(v.x, v.x) : v.x);
+        s0 += (double) (SQ ? mul_rn(v.y, v.y) : v.y);
+        s0 += (double) (SQ ? mul_rn(v.z, v.z) : v.z);
+        s0 += (double) (SQ ? mul_rn(v.w, v.w) : v.w);
     }
-    // src/ggml.c:11353-11406: mean in double -> float; v = x - mean; sum(v*v) in double
-    double s = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += (double) *(const float *) (x + i * a.nb[0]);
-    s = block_sum_d(s, shd);
-    const float mean = (float) (s / n);
-    double s2 = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const float v = *(const float *) (x + i * a.nb[0]) - mean;
-        s2 += (double) (v * v);
-    }
-    s2 = block_sum_d(s2, shd);
-    const float variance = (float) (s2 / n);
-    const float scale = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(variance, eps)));
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const float v = *(const float *) (x + i * a.nb[0]) - mean;
-        *(float *) (y + i * d.nb[0]) = v * scale;
-    }
+    for (; i < n; i++) s0 += (double) (SQ ? mul_rn(buf[i], buf[i]) : buf[i]);
+    return s0;
 }
 
-__global__ __launch_bounds__(256) void k_soft_max(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc mask, float scale,
-                                                  const uint16_t * exp_table) {
-    __shared__ double shd[4];
-    __shared__ float shf[4];
+constexpr int kRowLds = 12288;  // floats staged in LDS (48 KB); longer rows stage in dst
+
+__global__ __launch_bounds__(256) void k_norm(mi_tensor_desc d, mi_tensor_desc a, float eps, int rms) {
+    __shared__ __attribute__((aligned(16))) float lds[kRowLds];
+    __shared__ float sh_scale, sh_mean;
     int64_t i1, i2, i3;
     row_coords(blockIdx.x, a.ne, i1, i2, i3);
     const char * x = a.data + off4(a.nb, 0, i1, i2, i3);
     char * y = d.data + off4(d.nb, 0, i1, i2, i3);
     const int64_t n = a.ne[0];
+    // staging buffer: LDS, or the dst row when it is contiguous f32 and the row is long
+    const bool in_lds = n <= kRowLds;
+    float * buf = in_lds ? lds : (float *) y;
+    const bool aligned = in_lds || ((uintptr_t) y % 16 == 0);
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) buf[i] = *(const float *) (x + i * a.nb[0]);
+    __syncthreads();
+    if (rms) {
+        // src/ggml.c:11428-11478: sum += (double)(x*x); mean = sum/n; y = x * (1/sqrtf(mean+eps))
+        if (threadIdx.x == 0) {
+            double s = 0.0;
+            if (aligned) s = seq_sum_d<true>(buf, n);
+            else for (int64_t i = 0; i < n; i++) s += (double) mul_rn(buf[i], buf[i]);
+            const float mean = (float) (s / n);
+            sh_scale = 1.0f / sqrtf(add_rn(mean, eps));
+        }
+        __syncthreads();
+        const float scale = sh_scale;
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) *(float *) (y + i * d.nb[0]) = mul_rn(buf[i], scale);
+        return;
+    }
+    // src/ggml.c:11353-11406: mean = (float)(sum x / n); v = x - mean; sum2 += (double)(v*v)
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        if (aligned) s = seq_sum_d<false>(buf, n);
+        else for (int64_t i = 0; i < n; i++) s += (double) buf[i];
+        sh_mean = (float) (s / n);
+    }
+    __syncthreads();
+    const float mean = sh_mean;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) buf[i] = sub_rn(buf[i], mean);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s2 = 0.0;
+        if (aligned) s2 = seq_sum_d<true>(buf, n);
+        else for (int64_t i = 0; i < n; i++) s2 += (double) mul_rn(buf[i], buf[i]);
+        const float variance = (float) (s2 / n);
+        sh_scale = 1.0f / sqrtf(add_rn(variance, eps));
+    }
+    __syncthreads();
+    const float scale = sh_scale;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) *(float *) (y + i * d.nb[0]) = mul_rn(buf[i], scale);
+}
+
+// src/ggml.c:13393-13508: w = x*scale (+ mask); max; val = table_exp[fp16(w - max)] (0 for -inf);
+// sum += (double)val in order; y = val * (float)(1/sum)
+__global__ __launch_bounds__(256) void k_soft_max(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc mask, float scale,
+                                                  const uint16_t * exp_table) {
+    __shared__ __attribute__((aligned(16))) float lds[kRowLds];
+    __shared__ float shf[4];
+    __shared__ float sh_inv;
+    int64_t i1, i2, i3;
+    row_coords(blockIdx.x, a.ne, i1, i2, i3);
+    const char * x = a.data + off4(a.nb, 0, i1, i2, i3);
+    char * y = d.data + off4(d.nb, 0, i1, i2, i3);
+    const int64_t n = a.ne[0];
+    const bool in_lds = n <= kRowLds;
+    float * buf = in_lds ? lds : (float *) y;
+    const bool aligned = in_lds || ((uintptr_t) y % 16 == 0);
     // the mask row is broadcast over rows: (i1 % mask.ne1), as (i1 % ne01) in the reference
     const char * mrow = mask.data ? mask.data + (size_t) (blockIdx.x % a.ne[1]) * mask.nb[1] : nullptr;
-    auto w_of = [&](int64_t i) {
-        // wp = x*scale; wp += slope*mask (two roundings, no contraction; slope = 1 as max_bias = 0)
-        float w = __fmul_rn(*(const float *) (x + i * a.nb[0]), scale);
-        if (mrow) w = __fadd_rn(w, ld_f(mrow + i * mask.nb[0], mask.type));
-        return w;
-    };
     float mx = -INFINITY;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) mx = fmaxf(mx, w_of(i));
-    mx = block_max_f(mx, shf);
-    double sum = 0.0;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const float w = w_of(i);
-        float val = 0.0f;
-        if (w != -INFINITY) {
-            val = mi_h2f(exp_table[mi_f2h(w - mx)]);
-            sum += (double) val;
-        }
-        *(float *) (y + i * d.nb[0]) = val;
+        float w = mul_rn(*(const float *) (x + i * a.nb[0]), scale);
+        if (mrow) w = add_rn(w, ld_f(mrow + i * mask.nb[0], mask.type));  // slope = 1 (max_bias = 0)
+        buf[i] = w;
+        mx = fmaxf(mx, w);
     }
-    sum = block_sum_d(sum, shd);
-    const float inv = (float) (1.0 / sum);
+    mx = block_max_f(mx, shf);  // includes the barrier that publishes buf
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const float w = buf[i];
+        buf[i] = w == -INFINITY ? 0.0f : mi_h2f(exp_table[mi_f2h(sub_rn(w, mx))]);
+    }
     __syncthreads();
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) *(float *) (y + i * d.nb[0]) *= inv;
+    if (threadIdx.x == 0) {
+        // adding the 0.0 of masked entries leaves a double sum unchanged, as skipping them does
+        double sum = 0.0;
+        if (aligned) sum = seq_sum_d<false>(buf, n);
+        else for (int64_t i = 0; i < n; i++) sum += (double) buf[i];
+        sh_inv = (float) (1.0 / sum);
+    }
+    __syncthreads();
+    const float inv = sh_inv;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) *(float *) (y + i * d.nb[0]) = mul_rn(buf[i], inv);
 }
 
 // rope f32 (src/ggml.c:13719-13948), modes 0 (adjacent pairs) and 2 (neox halves), forward.
@@ -241,17 +279,17 @@ struct mi_rope_params {
 };
 
 __device__ __forceinline__ void rope_yarn_dev(float theta_extrap, const mi_rope_params & r, int64_t i0, float & c, float & s) {
-    const float theta_interp = __fmul_rn(r.freq_scale, theta_extrap);
+    const float theta_interp = mul_rn(r.freq_scale, theta_extrap);
     float theta = theta_interp;
     float mscale = r.attn_factor;
     if (r.ext_factor != 0.0f) {
         const float y = ((float) (i0 / 2) - r.corr0) / fmaxf(0.001f, r.corr1 - r.corr0);
         const float ramp_mix = (1.0f - fminf(1.0f, fmaxf(0.0f, y))) * r.ext_factor;
-        theta = __fadd_rn(__fmul_rn(theta_interp, 1.0f - ramp_mix), __fmul_rn(theta_extrap, ramp_mix));
+        theta = add_rn(mul_rn(theta_interp, 1.0f - ramp_mix), mul_rn(theta_extrap, ramp_mix));
         mscale *= 1.0f + 0.1f * (float) log(1.0 / (double) r.freq_scale);
     }
-    c = __fmul_rn((float) cos((double) theta), mscale);
-    s = __fmul_rn((float) sin((double) theta), mscale);
+    c = mul_rn((float) cos((double) theta), mscale);
+    s = mul_rn((float) sin((double) theta), mscale);
 }
 
 __global__ __launch_bounds__(256) void k_rope(mi_tensor_desc d, mi_tensor_desc a, const int32_t * pos, mi_rope_params r) {
@@ -270,27 +308,27 @@ __global__ __launch_bounds__(256) void k_rope(mi_tensor_desc d, mi_tensor_desc a
         char * dst = d.data + off4(d.nb, 0, i1, i2, i3);
         if (r.mode == 0) {
             float theta = p;
-            for (int64_t j = 0; j < k; j++) theta = __fmul_rn(theta, r.theta_scale);
+            for (int64_t j = 0; j < k; j++) theta = mul_rn(theta, r.theta_scale);
             float c, s;
             rope_yarn_dev(theta, r, 2 * k, c, s);
             const float x0 = *(const float *) (src + 2 * k * a.nb[0]);
             const float x1 = *(const float *) (src + (2 * k + 1) * a.nb[0]);
-            *(float *) (dst + 2 * k * d.nb[0]) = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s));
-            *(float *) (dst + (2 * k + 1) * d.nb[0]) = __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c));
+            *(float *) (dst + 2 * k * d.nb[0]) = sub_rn(mul_rn(x0, c), mul_rn(x1, s));
+            *(float *) (dst + (2 * k + 1) * d.nb[0]) = add_rn(mul_rn(x0, s), mul_rn(x1, c));
         } else {
             const int64_t ic = 2 * k;
             if (ic < r.n_dims) {
-                float theta = __fmul_rn(p, r.freq_scale);
-                for (int64_t j = 0; j < k; j++) theta = __fmul_rn(theta, r.theta_scale);
-                const float cur_rot = __fmul_rn(r.inv_ndims, (float) ic);
+                float theta = mul_rn(p, r.freq_scale);
+                for (int64_t j = 0; j < k; j++) theta = mul_rn(theta, r.theta_scale);
+                const float cur_rot = mul_rn(r.inv_ndims, (float) ic);
                 float c, s;
                 rope_yarn_dev(theta, r, (int64_t) cur_rot, c, s);
                 const int64_t i0 = ic / 2;
                 const int64_t h = r.n_dims / 2;
                 const float x0 = *(const float *) (src + i0 * a.nb[0]);
                 const float x1 = *(const float *) (src + (i0 + h) * a.nb[0]);
-                *(float *) (dst + i0 * d.nb[0]) = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s));
-                *(float *) (dst + (i0 + h) * d.nb[0]) = __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c));
+                *(float *) (dst + i0 * d.nb[0]) = sub_rn(mul_rn(x0, c), mul_rn(x1, s));
+                *(float *) (dst + (i0 + h) * d.nb[0]) = add_rn(mul_rn(x0, s), mul_rn(x1, c));
             } else {
                 *(float *) (dst + ic * d.nb[0]) = *(const float *) (src + ic * a.nb[0]);
                 *(float *) (dst + (ic + 1) * d.nb[0]) = *(const float *) (src + (ic + 1) * a.nb[0]);

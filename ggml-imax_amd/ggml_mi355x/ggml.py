@@ -282,3 +282,24 @@ def mul_mat_once(lib: Lib, backend, wtype: int, wq: np.ndarray, K: int, N: int, 
             return tensor_get(lib, y)
         finally:
             lib.ggml_backend_buffer_free(buf)
+
+
+def graph_once(lib: Lib, backend, build, n_tensors: int = 64):
+    """Build a graph with `build(ctx) -> (feeds, out)` (feeds: list of (tensor, ndarray)), allocate
+    it on `backend`, upload the feeds, compute, and return `out` as a float32/raw array."""
+    overhead = lib.ggml_tensor_overhead() * n_tensors + lib.ggml_graph_overhead()
+    with Context(lib, overhead, no_alloc=True) as c:
+        feeds, out = build(c.ctx)
+        g = lib.ggml_new_graph(c.ctx)
+        lib.ggml_build_forward_expand(g, out)
+        buf = lib.ggml_backend_alloc_ctx_tensors(c.ctx, backend)
+        assert buf, "buffer allocation failed"
+        try:
+            for t, arr in feeds:
+                tensor_set(lib, t, arr)
+            st = lib.ggml_backend_graph_compute(backend, g)
+            assert st == GGML_STATUS_SUCCESS, st
+            o = out.contents
+            return tensor_get(lib, out, np.float16 if o.type == GGML_TYPE_F16 else np.float32)
+        finally:
+            lib.ggml_backend_buffer_free(buf)

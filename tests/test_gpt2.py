@@ -8,7 +8,9 @@ Checkers (test infrastructure, oracle/Makefile `gpt2`):
 
 CPU tests pin the driver to the reference program (identical generated text for a seed, i.e. same
 graph, tokenizer and sampler); GPU tests compare teacher-forced MI355X logits with the reference
-CPU logits: max |d| / max |ref| <= 1e-3 per step (BASELINE north_star "logits within 1e-3").
+CPU logits. BASELINE's bar is max |d| / max |ref| <= 1e-3; on the decode path (prompt batches of
+<= 8 tokens, then single tokens) the MI355X logits are bit-identical to the CPU's, and the product
+CLI on MI355X samples exactly the text the reference program samples on the CPU.
 """
 import os
 import subprocess
@@ -105,22 +107,26 @@ def test_gpt2_logits_match_reference_cpu(model_path):
     try:
         toks = ours.tokenize(PROMPT)
         n_past = 0
-        errs = []
+        errs, same = [], []
         for i in range(0, len(toks), 8):
             chunk = toks[i:i + 8]
             a = ours.eval(n_past, chunk, all_logits=True)
             b = rm.eval(n_past, chunk, all_logits=True)
             errs.append(_rel_err(a, b))
+            same.append(float(np.mean(a == b)))
             n_past += len(chunk)
         nxt = int(np.argmax(b[-1]))
         for _ in range(24):
             a = ours.eval(n_past, [nxt])
             b = rm.eval(n_past, [nxt])
             errs.append(_rel_err(a, b))
+            same.append(float(np.mean(a == b)))
             n_past += 1
             nxt = int(np.argmax(b[-1]))
         print("max rel logit error per step:", ["%.2e" % e for e in errs])
+        print("fraction of bit-identical logits per step:", ["%.4f" % f for f in same])
         assert max(errs) <= LOGIT_TOL, errs
+        assert min(same) == 1.0, "decode-path logits are expected to be bit-identical to the CPU's"
     finally:
         ours.free()
         rm.free()
@@ -137,6 +143,19 @@ def test_gpt2_cli_on_mi355x(model_path):
     assert p.returncode == 0
     assert "using MI355X0 backend" in p.stderr
     assert "per token" in p.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="make -C oracle gpt2")
+def test_gpt2_cli_on_mi355x_samples_reference_text(model_path):
+    """Seeded sampling on MI355X (-ngl 100) prints the same text as the reference program
+    (examples/gpt-2/main-backend.cpp) on the reference CPU: the logits are bit-identical."""
+    args = ["-m", model_path, "-p", PROMPT, "-n", "48", "-s", "11", "-t", "8"]
+    ref = subprocess.run([REF_BIN] + args, capture_output=True, text=True, timeout=300)
+    ours = subprocess.run([OUR_BIN] + args + ["-ngl", "100"], capture_output=True, text=True, timeout=300)
+    assert ref.returncode == 0 and ours.returncode == 0, (ref.stderr[-1000:], ours.stderr[-1000:])
+    print(_text(ours.stdout))
+    assert _text(ours.stdout) == _text(ref.stdout)
 
 
 @pytest.mark.gpu

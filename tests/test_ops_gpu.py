@@ -1,0 +1,201 @@
+"""Companion ops at GPT-2 / LLaMA shapes vs the reference CPU backend
+(oracle/_ref/libggml_ref.so) itself, bit for bit where the CPU's rounding sequence is reproducible.
+
+The reference's test-backend-ops (tests/test_00_reference_harness.py) checks these ops with NMSE
+thresholds; here the same graphs run on MI355X and on the reference CPU and the outputs must be
+identical bits: norms and soft_max run the CPU's sequential double sums, lookup tables are built
+with the reference build's own contraction choices, and no multiply-add is fused unless the CPU
+fuses it. RoPE is the exception (cos/sin from the device math library): tolerance-checked.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from ggml_mi355x import ggml as G
+from ggml_mi355x import synth
+
+REF_LIB = os.path.join(REPO, "oracle", "_ref", "libggml_ref.so")
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not os.path.exists(REF_LIB), reason="make -C oracle ref")]
+
+F32, F16, I32 = G.GGML_TYPE_F32, G.GGML_TYPE_F16, G.GGML_TYPE_I32
+
+
+@pytest.fixture(scope="module")
+def libs():
+    rt = G.runtime()
+    be = G.mi355x_backend(rt)
+    ref = G.Lib([REF_LIB], isolated=True)
+    cpu = ref.ggml_backend_cpu_init()
+    yield rt, be, ref, cpu
+    ref.ggml_backend_free(cpu)
+    rt.ggml_backend_free(be)
+
+
+def both(libs, build):
+    rt, be, ref, cpu = libs
+    return G.graph_once(rt, be, lambda c: build(rt, c)), G.graph_once(ref, cpu, lambda c: build(ref, c))
+
+
+def ulp_diff(a, b):
+    ai = a.view(np.int32).astype(np.int64)
+    bi = b.view(np.int32).astype(np.int64)
+    return np.abs(ai - bi)
+
+
+def assert_exact(a, b, name, allow_ulp1_frac=0.0):
+    assert a.shape == b.shape
+    fin = np.isfinite(b)
+    assert np.array_equal(np.isfinite(a), fin), f"{name}: inf/nan pattern differs"
+    d = ulp_diff(a[fin], b[fin])
+    n_bad = int(np.sum(d > 0))
+    print(f"{name}: {n_bad}/{d.size} elements differ (max {int(d.max()) if d.size else 0} ulp)")
+    if allow_ulp1_frac == 0.0:
+        assert n_bad == 0
+    else:
+        assert int(d.max()) <= 1 and n_bad <= allow_ulp1_frac * d.size
+
+
+def rnd(seed, n, scale=1.0):
+    return (synth.uniform(seed, n) * np.float32(scale)).astype(np.float32)
+
+
+@pytest.mark.parametrize("ne0,ne1", [(768, 1), (768, 8), (3072, 5), (4096, 3)])
+def test_norm_exact(libs, ne0, ne1):
+    x = rnd(1, ne0 * ne1, 3.0) + np.float32(0.5)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_2d(c, F32, ne0, ne1)
+        return [(t, x)], L.ggml_norm(c, t, 1e-5)
+
+    a, b = both(libs, build)
+    assert_exact(a, b, "norm")
+
+
+@pytest.mark.parametrize("ne0,ne1", [(4096, 1), (4096, 7)])
+def test_rms_norm_exact(libs, ne0, ne1):
+    x = rnd(2, ne0 * ne1, 2.0)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_2d(c, F32, ne0, ne1)
+        return [(t, x)], L.ggml_rms_norm(c, t, 1e-6)
+
+    a, b = both(libs, build)
+    assert_exact(a, b, "rms_norm")
+
+
+@pytest.mark.parametrize("n_kv,N", [(1, 1), (13, 1), (40, 8), (1000, 1), (512, 16)])
+def test_gpt2_attention_softmax_exact(libs, n_kv, N):
+    """scale -> diag_mask_inf(n_past) -> soft_max as in gpt2_graph (main-backend.cpp:572-584)."""
+    H = 12
+    n_past = n_kv - N
+    x = rnd(3, n_kv * N * H, 4.0)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_3d(c, F32, n_kv, N, H)
+        s = L.ggml_scale(c, t, 1.0 / 8.0)
+        m = L.ggml_diag_mask_inf(c, s, n_past)
+        return [(t, x)], L.ggml_soft_max(c, m)
+
+    a, b = both(libs, build)
+    assert_exact(a, b, "scale+diag_mask_inf+soft_max")
+
+
+def test_gelu_exact(libs):
+    # every f16 input value of the lookup table plus the clamp regions
+    h = np.arange(65536, dtype=np.uint16).view(np.float16).astype(np.float32)
+    h = h[np.isfinite(h)]
+    x = np.concatenate([h, rnd(4, 30000, 12.0)]).astype(np.float32)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_1d(c, F32, len(x))
+        return [(t, x)], L.ggml_gelu(c, t)
+
+    a, b = both(libs, build)
+    assert_exact(a, b, "gelu")
+
+
+def test_silu_exact(libs):
+    x = rnd(5, 50000, 9.0)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_1d(c, F32, len(x))
+        return [(t, x)], L.ggml_silu(c, t)
+
+    a, b = both(libs, build)
+    assert_exact(a, b, "silu")
+
+
+@pytest.mark.parametrize("src_type", [F16, F32])
+def test_get_rows_plus_add_exact(libs, src_type):
+    """get_rows(wte f16) + get_rows(wpe f32) as the GPT-2 embedding (main-backend.cpp:475-478)."""
+    E, V, N = 768, 997, 9
+    w = rnd(6, E * V, 0.1)
+    wv = w.astype(np.float16) if src_type == F16 else w
+    p = rnd(7, E * 64, 0.1)
+    ids = np.array([5, 996, 0, 17, 17, 300, 2, 9, 500], dtype=np.int32)
+    pos = np.arange(N, dtype=np.int32) + 3
+
+    def build(L, c):
+        wt = L.ggml_new_tensor_2d(c, src_type, E, V)
+        pt = L.ggml_new_tensor_2d(c, F32, E, 64)
+        it = L.ggml_new_tensor_1d(c, I32, N)
+        qt = L.ggml_new_tensor_1d(c, I32, N)
+        out = L.ggml_add(c, L.ggml_get_rows(c, wt, it), L.ggml_get_rows(c, pt, qt))
+        return [(wt, wv), (pt, p), (it, ids), (qt, pos)], out
+
+    a, b = both(libs, build)
+    assert_exact(a, b, "get_rows+add")
+
+
+def test_layernorm_affine_exact(libs):
+    """norm -> mul(g) -> add(b) with row broadcast, as every GPT-2 layer norm."""
+    E, N = 768, 6
+    x = rnd(8, E * N, 2.0)
+    g = rnd(9, E, 1.0) + np.float32(1.0)
+    bb = rnd(10, E, 0.1)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_2d(c, F32, E, N)
+        gt = L.ggml_new_tensor_1d(c, F32, E)
+        bt = L.ggml_new_tensor_1d(c, F32, E)
+        return [(t, x), (gt, g), (bt, bb)], L.ggml_add(c, L.ggml_mul(c, L.ggml_norm(c, t, 1e-5), gt), bt)
+
+    a, b = both(libs, build)
+    assert_exact(a, b, "norm+mul+add")
+
+
+def test_permute_cont_cpy_exact(libs):
+    """cont(permute(reshape)) of the V cache (main-backend.cpp:586-594) and f32 -> f16 cpy."""
+    D, H, T = 64, 12, 37
+    x = rnd(11, D * H * T, 1.0)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_3d(c, F32, D, H, T)
+        p = L.ggml_cont(c, L.ggml_permute(c, t, 1, 2, 0, 3))
+        h = L.ggml_new_tensor_3d(c, F16, T, D, H)
+        return [(t, x)], L.ggml_cpy(c, p, h)
+
+    a, b = both(libs, build)
+    assert np.array_equal(a.view(np.uint16), b.view(np.uint16))
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_rope_close(libs, mode):
+    """RoPE (LLaMA mode 0, NeoX mode 2): cos/sin come from libm on the CPU and from the device's
+    math library here, so this is a tolerance check (and exact counts are reported)."""
+    D, H, T = 128, 8, 11
+    x = rnd(12, D * H * T, 1.0)
+    pos = (np.arange(T, dtype=np.int32) * 37 + 5).astype(np.int32)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_3d(c, F32, D, H, T)
+        pt = L.ggml_new_tensor_1d(c, I32, T)
+        return [(t, x), (pt, pos)], L.ggml_rope(c, t, pt, D, mode, 0)
+
+    a, b = both(libs, build)
+    d = ulp_diff(a, b)
+    print(f"rope mode {mode}: {int(np.sum(d > 0))}/{d.size} differ, max abs {float(np.max(np.abs(a - b))):.2e}")
+    assert np.max(np.abs(a - b)) <= 1e-5 * max(1.0, float(np.max(np.abs(b))))
