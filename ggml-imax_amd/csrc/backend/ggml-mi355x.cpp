@@ -24,6 +24,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #define MI_CHECK(call)                                                                                  \
@@ -574,9 +575,9 @@ static void op_companion(mi_backend_ctx * ctx, ggml_tensor * node) {
         case GGML_OP_MUL: mi_op_binary(desc(node), desc(a), desc(b), MI_OP_MUL, st); break;
         case GGML_OP_DIV: mi_op_binary(desc(node), desc(a), desc(b), MI_OP_DIV, st); break;
         case GGML_OP_SCALE: mi_op_unary(desc(node), desc(a), MI_OP_SCALE, op_param_f(node, 0), nullptr, st); break;
-        case GGML_OP_NORM: mi_op_norm(desc(node), desc(a), op_param_f(node, 0), false, st); break;
-        case GGML_OP_RMS_NORM: mi_op_norm(desc(node), desc(a), op_param_f(node, 0), true, st); break;
-        case GGML_OP_SOFT_MAX: mi_op_soft_max(desc(node), desc(a), desc(b), op_param_f(node, 0), op_tables(ctx), st); break;
+        case GGML_OP_NORM: mi_op_norm(desc(node), desc(a), op_param_f(node, 0), false, nullptr, nullptr, st); break;
+        case GGML_OP_RMS_NORM: mi_op_norm(desc(node), desc(a), op_param_f(node, 0), true, nullptr, nullptr, st); break;
+        case GGML_OP_SOFT_MAX: mi_op_soft_max(desc(node), desc(a), desc(b), op_param_f(node, 0), op_tables(ctx), 1.0f, -1, st); break;
         case GGML_OP_DIAG_MASK_INF:
             mi_op_diag_mask(desc(node), desc(a), ((const int32_t *) node->op_params)[0], -INFINITY, st);
             break;
@@ -706,6 +707,207 @@ static int run_fused_group(mi_backend_ctx * ctx, ggml_cgraph * cgraph, int i) {
     return last;
 }
 
+// ---- node fusion (same results: each fused step is rounded exactly as its own node would be) ----
+//
+// Patterns of the GPT-2 / LLaMA graphs (examples/gpt-2/main-backend.cpp:442-717):
+//   NORM|RMS_NORM -> MUL(., g[E]) -> ADD(., b[E])             one k_norm launch
+//   MUL_MAT(F16, few cols) -> ADD(., bias[N]) [-> ADD(., resid) | -> GELU]   one GEMV launch
+//   SCALE -> DIAG_MASK_INF -> SOFT_MAX                          one k_soft_max launch
+// An intermediate may be skipped only if the next node is its sole consumer and it is not a graph
+// output; views of a tensor count as consumers of it.
+
+struct mi_uses {
+    std::unordered_map<const ggml_tensor *, int> n;
+    int of(const ggml_tensor * t) const {
+        auto it = n.find(t);
+        return it == n.end() ? 0 : it->second;
+    }
+};
+
+static void count_uses(const ggml_cgraph * g, mi_uses & u) {
+    u.n.clear();
+    for (int i = 0; i < g->n_nodes; i++) {
+        const ggml_tensor * t = g->nodes[i];
+        for (int s = 0; s < GGML_MAX_SRC; s++) {
+            const ggml_tensor * src = t->src[s];
+            if (!src) continue;
+            u.n[src]++;
+            if (src->view_src) u.n[src->view_src]++;
+        }
+        if (t->view_src) u.n[t->view_src]++;
+    }
+}
+
+static int next_node(const ggml_cgraph * g, int i) {
+    for (int j = i + 1; j < g->n_nodes; j++) {
+        if (!is_noop(g->nodes[j])) return j;
+    }
+    return -1;
+}
+
+static bool private_intermediate(const ggml_tensor * t, const mi_uses & u) {
+    return u.of(t) == 1 && !(t->flags & GGML_TENSOR_FLAG_OUTPUT);
+}
+
+// a fused kernel may write `out` over an input only when both are the same elements (each lane
+// reads its element before writing it); any other overlap would race across workgroups
+static bool safe_alias(const ggml_tensor * out, const ggml_tensor * in) {
+    if (!in || !overlaps(out, in)) return true;
+    return out->data == in->data && ggml_are_same_shape(out, in) && memcmp(out->nb, in->nb, sizeof(out->nb)) == 0;
+}
+
+static bool is_vec_f32(const ggml_tensor * t, int64_t n) {
+    return t && t->type == GGML_TYPE_F32 && t->ne[0] == n && t->ne[1] == 1 && t->ne[2] == 1 && t->ne[3] == 1 &&
+           t->nb[0] == sizeof(float);
+}
+
+// ADD(x, other) or ADD(other, x): returns `other`, or null
+static const ggml_tensor * add_operand(const ggml_tensor * add, const ggml_tensor * x) {
+    if (add->op != GGML_OP_ADD) return nullptr;
+    if (add->src[0] == x) return add->src[1];
+    if (add->src[1] == x) return add->src[0];
+    return nullptr;
+}
+
+static int try_fuse_norm(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
+    ggml_tensor * norm = g->nodes[i];
+    const int64_t E = norm->ne[0];
+    const int j = next_node(g, i);
+    if (j < 0 || !private_intermediate(norm, u)) return -1;
+    ggml_tensor * mul = g->nodes[j];
+    if (mul->op != GGML_OP_MUL || mul->src[0] != norm || !is_vec_f32(mul->src[1], E) || !ggml_are_same_shape(mul, norm)) return -1;
+    ggml_tensor * out = mul;
+    const float * bias = nullptr;
+    int last = j;
+    const int k = next_node(g, j);
+    if (k >= 0 && private_intermediate(mul, u)) {
+        ggml_tensor * add = g->nodes[k];
+        if (add->op == GGML_OP_ADD && add->src[0] == mul && is_vec_f32(add->src[1], E) && ggml_are_same_shape(add, mul)) {
+            out = add;
+            bias = (const float *) add->src[1]->data;
+            last = k;
+        }
+    }
+    if (out->type != GGML_TYPE_F32 || out->nb[0] != sizeof(float)) return -1;
+    if (!safe_alias(out, norm->src[0]) || overlaps(out, mul->src[1]) || (bias && overlaps(out, g->nodes[last]->src[1]))) return -1;
+    mi_op_norm(desc(out), desc(norm->src[0]), op_param_f(norm, 0), norm->op == GGML_OP_RMS_NORM,
+               (const float *) mul->src[1]->data, bias, ctx->stream);
+    ctx->last_launches++;
+    return last;
+}
+
+static int try_fuse_softmax(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
+    ggml_tensor * sc = g->nodes[i];
+    const int j = next_node(g, i);
+    if (j < 0 || !private_intermediate(sc, u)) return -1;
+    ggml_tensor * dm = g->nodes[j];
+    if (dm->op != GGML_OP_DIAG_MASK_INF || dm->src[0] != sc) return -1;
+    const int k = next_node(g, j);
+    if (k < 0 || !private_intermediate(dm, u)) return -1;
+    ggml_tensor * sm = g->nodes[k];
+    if (sm->op != GGML_OP_SOFT_MAX || sm->src[0] != dm || sm->src[1] != nullptr || op_param_f(sm, 1) != 0.0f) return -1;
+    const ggml_tensor * a = sc->src[0];
+    if (a->type != GGML_TYPE_F32 || !ggml_is_contiguous(a) || !ggml_are_same_shape(a, sm)) return -1;
+    if (!safe_alias(sm, a)) return -1;
+    const int n_past = ((const int32_t *) dm->op_params)[0];
+    mi_op_soft_max(desc(sm), desc(a), desc(nullptr), op_param_f(sm, 0), op_tables(ctx), op_param_f(sc, 0), n_past, ctx->stream);
+    ctx->last_launches++;
+    return k;
+}
+
+static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
+    ggml_tensor * mm = g->nodes[i];
+    const ggml_tensor * w = mm->src[0];
+    const ggml_tensor * x = mm->src[1];
+    if (w->type != GGML_TYPE_F16 || x->type != GGML_TYPE_F32) return -1;
+    if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1 || x->ne[1] > 8) return -1;
+    if (w->nb[0] != 2 || w->nb[1] % 16 != 0 || (uintptr_t) w->data % 16 != 0 || x->nb[0] != sizeof(float)) return -1;
+    if (!mi_mul_mat_f16_fused_supported(w->ne[0], x->ne[1])) return -1;
+    const int64_t N = w->ne[1];
+    mi_f16_epilogue e;
+    const ggml_tensor * bias_t = nullptr, * res_t = nullptr;
+    ggml_tensor * out = mm;
+    int last = i;
+    int j = next_node(g, i);
+    if (j >= 0 && private_intermediate(mm, u)) {
+        ggml_tensor * add = g->nodes[j];
+        const ggml_tensor * bias = add_operand(add, mm);
+        if (bias && is_vec_f32(bias, N) && ggml_are_same_shape(add, mm) && add->nb[0] == sizeof(float)) {
+            e.bias = (const float *) bias->data;
+            bias_t = bias;
+            out = add;
+            last = j;
+            const int k = next_node(g, j);
+            if (k >= 0 && private_intermediate(add, u)) {
+                ggml_tensor * n2 = g->nodes[k];
+                const ggml_tensor * res = add_operand(n2, add);
+                if (res && res != add && res->type == GGML_TYPE_F32 && ggml_are_same_shape(res, add) && res->nb[0] == sizeof(float) &&
+                    n2->nb[0] == sizeof(float) && ggml_are_same_shape(n2, add)) {
+                    e.resid = (const char *) res->data;
+                    e.resid_nb1 = res->nb[1];
+                    res_t = res;
+                    out = n2;
+                    last = k;
+                } else if (n2->op == GGML_OP_UNARY && ggml_get_unary_op(n2) == GGML_UNARY_OP_GELU && n2->src[0] == add &&
+                           n2->type == GGML_TYPE_F32 && n2->nb[0] == sizeof(float) && ggml_are_same_shape(n2, add)) {
+                    e.gelu_table = op_tables(ctx) + 65536;
+                    out = n2;
+                    last = k;
+                }
+            }
+        }
+    }
+    if (out->type != GGML_TYPE_F32 || out->nb[0] != sizeof(float)) return -1;
+    // every workgroup reads all of X and W; resid/bias are read per element. When the graph
+    // allocator has placed `out` over X (X's last reader is this mul_mat), X is first converted
+    // into the backend's scratch so no workgroup can see it overwritten.
+    if (overlaps(out, w)) return -1;
+    if (bias_t && overlaps(out, bias_t)) return -1;
+    if (res_t && !safe_alias(out, res_t)) return -1;
+    const uint16_t * xh = nullptr;
+    if (overlaps(out, x)) {
+        uint16_t * tmp = (uint16_t *) scratch_take(ctx, act_bytes(2, w->ne[0], x->ne[1]));
+        mi_convert_f16(src_cols(x), w->ne[0], tmp, ctx->stream);
+        ctx->last_launches++;
+        xh = tmp;
+    }
+    mi_mul_mat_f16_fused(w->data, w->nb[1], w->ne[0], N, src_cols(x), xh, x->ne[1], (float *) out->data, out->nb[1], e, ctx->stream);
+    ctx->last_launches++;
+    return last;
+}
+
+static bool is_copy(const ggml_tensor * t) {
+    return (t->op == GGML_OP_CPY || t->op == GGML_OP_DUP || t->op == GGML_OP_CONT) && is_f16_or_f32(t->src[0]) && is_f16_or_f32(t) &&
+           ggml_nelements(t) == ggml_nelements(t->src[0]);
+}
+
+// consecutive independent copies (GPT-2: K -> cache, V -> cache, cont(Q)) as one launch
+static int try_fuse_copies(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
+    std::vector<ggml_tensor *> grp = {g->nodes[i]};
+    if (!is_copy(grp[0])) return -1;
+    int last = i;
+    for (int j = next_node(g, i); j >= 0 && (int) grp.size() < kMiMaxCopies; j = next_node(g, j)) {
+        ggml_tensor * n = g->nodes[j];
+        if (!is_copy(n)) break;
+        bool indep = true;
+        for (ggml_tensor * m : grp) {
+            if (overlaps(n->src[0], m) || overlaps(n, m->src[0]) || overlaps(n, m)) indep = false;
+        }
+        if (!indep) break;
+        grp.push_back(n);
+        last = j;
+    }
+    if (grp.size() < 2) return -1;
+    mi_tensor_desc d[kMiMaxCopies], a[kMiMaxCopies];
+    for (size_t k = 0; k < grp.size(); k++) {
+        d[k] = desc(grp[k]);
+        a[k] = desc(grp[k]->src[0]);
+    }
+    mi_op_cpy_multi(d, a, (int) grp.size(), ctx->stream);
+    ctx->last_launches++;
+    return last;
+}
+
 static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * cgraph) {
     auto * ctx = (mi_backend_ctx *) backend->context;
     mi_device_guard g(ctx->device);
@@ -714,9 +916,30 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
     ctx->act_cache.clear();
     ctx->last_launches = 0;
     static const bool no_fuse = getenv("GGML_MI355X_NO_FUSED_MMV") != nullptr;
+    static const bool no_node_fusion = getenv("GGML_MI355X_NO_NODE_FUSION") != nullptr;
+    mi_uses uses;
+    if (!no_node_fusion) count_uses(cgraph, uses);
     for (int i = 0; i < cgraph->n_nodes; i++) {
         ggml_tensor * node = cgraph->nodes[i];
         if (is_noop(node)) continue;
+        int last = -1;
+        if (!no_node_fusion) {
+            switch (node->op) {
+                case GGML_OP_NORM:
+                case GGML_OP_RMS_NORM: last = try_fuse_norm(ctx, cgraph, i, uses); break;
+                case GGML_OP_SCALE: last = try_fuse_softmax(ctx, cgraph, i, uses); break;
+                case GGML_OP_MUL_MAT: last = try_fuse_f16_gemv(ctx, cgraph, i, uses); break;
+                case GGML_OP_CPY:
+                case GGML_OP_DUP:
+                case GGML_OP_CONT: last = try_fuse_copies(ctx, cgraph, i); break;
+                default: break;
+            }
+        }
+        if (last >= 0) {
+            for (int k = i; k <= last; k++) invalidate_activations(ctx, cgraph->nodes[k]);
+            i = last;
+            continue;
+        }
         switch (node->op) {
             case GGML_OP_MUL_MAT:
                 if (!no_fuse && fused_mv_eligible(node)) {

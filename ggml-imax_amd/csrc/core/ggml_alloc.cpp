@@ -166,12 +166,22 @@ struct plan_entry {
 
 } // namespace
 
+// per graph position (node i / leaf i) placement of the last full plan: reused as long as a new
+// graph has the same shape of positions and every tensor fits its planned slot -- the reserve()
+// of a worst-case graph followed by cheap per-step assignment, as ggml-alloc.c:668-737 does
+struct slot {
+    int buffer_id;   // -1: the position needs no memory
+    size_t offset;
+    size_t size;
+};
+
 struct ggml_gallocr {
     std::vector<ggml_backend_buffer_type_t> bufts;
     std::vector<ggml_backend_buffer_t> buffers;
     std::vector<size_t> planned;  // planned size per buffer
     std::vector<int> node_buffer_ids;
     std::vector<int> leaf_buffer_ids;
+    std::vector<slot> node_slots, leaf_slots;
 };
 
 static ggml_tensor * base_of(ggml_tensor * t) { return t->view_src ? t->view_src : t; }
@@ -239,7 +249,30 @@ static std::vector<size_t> plan_graph(ggml_gallocr * ga, ggml_cgraph * g, std::u
     }
     std::vector<size_t> sizes(nb);
     for (int i = 0; i < nb; i++) sizes[i] = arenas[i].high;
+    auto slot_of = [&](ggml_tensor * t) -> slot {
+        auto it = out.find(t);
+        if (it == out.end()) return {-1, 0, 0};
+        return {it->second.buffer_id, it->second.offset, size_of(t, it->second.buffer_id)};
+    };
+    ga->node_slots.resize(g->n_nodes);
+    ga->leaf_slots.resize(g->n_leafs);
+    for (int i = 0; i < g->n_nodes; i++) ga->node_slots[i] = slot_of(g->nodes[i]);
+    for (int i = 0; i < g->n_leafs; i++) ga->leaf_slots[i] = slot_of(g->leafs[i]);
     return sizes;
+}
+
+// every tensor needing memory sits at a position whose planned slot holds it
+static bool slots_fit(ggml_gallocr * ga, ggml_cgraph * g) {
+    if ((int) ga->node_slots.size() != g->n_nodes || (int) ga->leaf_slots.size() != g->n_leafs || ga->buffers.empty()) return false;
+    auto fits = [&](ggml_tensor * t, const slot & sl) {
+        const bool needs = t->data == NULL && t->view_src == NULL;
+        if (!needs) return sl.buffer_id < 0 || t->data != NULL || t->view_src != NULL;
+        return sl.buffer_id >= 0 && ga->buffers[sl.buffer_id] != NULL &&
+               ggml_backend_buft_get_alloc_size(ga->bufts[sl.buffer_id], t) <= sl.size;
+    };
+    for (int i = 0; i < g->n_leafs; i++) if (!fits(g->leafs[i], ga->leaf_slots[i])) return false;
+    for (int i = 0; i < g->n_nodes; i++) if (!fits(g->nodes[i], ga->node_slots[i])) return false;
+    return true;
 }
 
 extern "C" {
@@ -290,6 +323,29 @@ bool ggml_gallocr_reserve_n(ggml_gallocr_t galloc, struct ggml_cgraph * graph, c
 bool ggml_gallocr_reserve(ggml_gallocr_t galloc, struct ggml_cgraph * graph) { return ggml_gallocr_reserve_n(galloc, graph, NULL, NULL); }
 
 bool ggml_gallocr_alloc_graph(ggml_gallocr_t galloc, struct ggml_cgraph * graph) {
+    auto init_view = [&](ggml_tensor * t) {
+        if (t->view_src && t->buffer == NULL && t->view_src->buffer != NULL) ggml_backend_view_init(t->view_src->buffer, t);
+    };
+    if (slots_fit(galloc, graph)) {
+        // fast path: same positions, every tensor fits its planned slot
+        for (int i = 0; i < (int) galloc->buffers.size(); i++) {
+            if (galloc->buffers[i]) ggml_backend_buffer_reset(galloc->buffers[i]);
+        }
+        auto put = [&](ggml_tensor * t, const slot & sl) {
+            if (sl.buffer_id < 0 || t->data != NULL || t->view_src != NULL) return;
+            ggml_backend_buffer_t buf = galloc->buffers[sl.buffer_id];
+            ggml_backend_tensor_alloc(buf, t, (char *) ggml_backend_buffer_get_base(buf) + sl.offset);
+        };
+        for (int i = 0; i < graph->n_leafs; i++) put(graph->leafs[i], galloc->leaf_slots[i]);
+        for (int i = 0; i < graph->n_nodes; i++) put(graph->nodes[i], galloc->node_slots[i]);
+        for (int i = 0; i < graph->n_nodes; i++) {
+            ggml_tensor * n = graph->nodes[i];
+            for (int s = 0; s < GGML_MAX_SRC; s++) if (n->src[s]) init_view(n->src[s]);
+            init_view(n);
+        }
+        for (int i = 0; i < graph->n_leafs; i++) init_view(graph->leafs[i]);
+        return true;
+    }
     std::unordered_map<ggml_tensor *, plan_entry> plan;
     const std::vector<size_t> sizes = plan_graph(galloc, graph, plan);
     for (size_t i = 0; i < sizes.size(); i++) {
@@ -306,9 +362,6 @@ bool ggml_gallocr_alloc_graph(ggml_gallocr_t galloc, struct ggml_cgraph * graph)
         if (it == plan.end() || t->data != NULL) return;
         ggml_backend_buffer_t buf = galloc->buffers[it->second.buffer_id];
         ggml_backend_tensor_alloc(buf, t, (char *) ggml_backend_buffer_get_base(buf) + it->second.offset);
-    };
-    auto init_view = [&](ggml_tensor * t) {
-        if (t->view_src && t->buffer == NULL && t->view_src->buffer != NULL) ggml_backend_view_init(t->view_src->buffer, t);
     };
     for (int i = 0; i < graph->n_leafs; i++) assign(graph->leafs[i]);
     for (int i = 0; i < graph->n_nodes; i++) {

@@ -56,7 +56,8 @@ struct gpt2_model {
     size_t weight_bytes = 0;
     std::vector<uint8_t> graph_buf;
     int last_nodes = 0;
-    int64_t us_build = 0, us_alloc = 0, us_compute = 0;
+    int64_t us_build = 0, us_alloc = 0, us_inputs = 0, us_compute = 0;
+    std::vector<int32_t> tok, pos;  // input staging, alive until the next eval
 };
 
 namespace {
@@ -386,12 +387,16 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
         fprintf(stderr, "gpt2_eval: graph allocation failed\n");
         return 1;
     }
+    const int64_t t1b = now_us();
+    // inputs go in on the backend's queue, ordered before the graph (ggml_backend_tensor_set_async,
+    // ggml-backend.h): no host round trip per input
     ggml_tensor * embd = ggml_graph_get_tensor(gf, "embd");
-    ggml_backend_tensor_set(embd, tokens, 0, (size_t) N * ggml_element_size(embd));
     ggml_tensor * position = ggml_graph_get_tensor(gf, "position");
-    std::vector<int32_t> pos(N);
-    for (int i = 0; i < N; i++) pos[i] = n_past + i;
-    ggml_backend_tensor_set(position, pos.data(), 0, (size_t) N * sizeof(int32_t));
+    m->pos.resize(N);
+    m->tok.assign(tokens, tokens + N);
+    for (int i = 0; i < N; i++) m->pos[i] = n_past + i;
+    ggml_backend_tensor_set_async(m->backend, embd, m->tok.data(), 0, (size_t) N * ggml_element_size(embd));
+    ggml_backend_tensor_set_async(m->backend, position, m->pos.data(), 0, (size_t) N * sizeof(int32_t));
     const int64_t t2 = now_us();
     if (ggml_backend_graph_compute(m->backend, gf) != GGML_STATUS_SUCCESS) {
         fprintf(stderr, "gpt2_eval: graph compute failed\n");
@@ -404,7 +409,8 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
     const int64_t t3 = now_us();
     m->last_nodes = gf->n_nodes;
     m->us_build = t1 - t0;
-    m->us_alloc = t2 - t1;
+    m->us_alloc = t1b - t1;
+    m->us_inputs = t2 - t1b;
     m->us_compute = t3 - t2;
     return 0;
 }
@@ -438,10 +444,12 @@ int gpt2_tokenize(const gpt2_model * m, const char * text, int32_t * out, int ma
     return n;
 }
 
-void gpt2_last_eval_stats(const gpt2_model * m, int * n_nodes, int64_t * us_build, int64_t * us_alloc, int64_t * us_compute) {
+void gpt2_last_eval_stats(const gpt2_model * m, int * n_nodes, int64_t * us_build, int64_t * us_alloc, int64_t * us_inputs,
+                          int64_t * us_compute) {
     if (n_nodes) *n_nodes = m->last_nodes;
     if (us_build) *us_build = m->us_build;
     if (us_alloc) *us_alloc = m->us_alloc;
+    if (us_inputs) *us_inputs = m->us_inputs;
     if (us_compute) *us_compute = m->us_compute;
 }
 

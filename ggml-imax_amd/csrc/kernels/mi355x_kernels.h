@@ -98,14 +98,33 @@ enum mi_elt_op { MI_OP_ADD, MI_OP_MUL, MI_OP_SUB, MI_OP_DIV, MI_OP_SCALE, MI_OP_
 void mi_op_binary(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & b, int op, hipStream_t s);
 void mi_op_unary(const mi_tensor_desc & d, const mi_tensor_desc & a, int op, float p0, const uint16_t * table, hipStream_t s);
 void mi_op_cpy(const mi_tensor_desc & d, const mi_tensor_desc & a, hipStream_t s);
+// several independent copies (element i of a[c] -> element i of d[c]) in one launch
+constexpr int kMiMaxCopies = 4;
+void mi_op_cpy_multi(const mi_tensor_desc * d, const mi_tensor_desc * a, int count, hipStream_t s);
 void mi_op_get_rows(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & idx, hipStream_t s);
 void mi_op_diag_mask(const mi_tensor_desc & d, const mi_tensor_desc & a, int n_past, float value, hipStream_t s);
-void mi_op_norm(const mi_tensor_desc & d, const mi_tensor_desc & a, float eps, bool rms, hipStream_t s);
+// norm / rms_norm; g, b (optional, 1-D over ne0): the graph's following mul(., g) and add(., b)
+void mi_op_norm(const mi_tensor_desc & d, const mi_tensor_desc & a, float eps, bool rms, const float * g, const float * b,
+                hipStream_t s);
 // rope f32 forward, modes 0/2; corr = ggml_rope_yarn_corr_dims() computed on the host
 void mi_op_rope(const mi_tensor_desc & d, const mi_tensor_desc & a, const int32_t * pos, int n_dims, int mode, float freq_base,
                 float freq_scale, float ext_factor, float attn_factor, float corr0, float corr1, hipStream_t s);
+// soft_max (max_bias 0); n_past >= 0 fuses the preceding scale(pre_scale) + diag_mask_inf(n_past)
 void mi_op_soft_max(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & mask, float scale,
-                    const uint16_t * exp_table, hipStream_t s);
+                    const uint16_t * exp_table, float pre_scale, int n_past, hipStream_t s);
+
+// Decode-regime F16 mul_mat (2-D weights, few f32 src1 columns of contiguous K) that converts the
+// activations itself and applies the graph's following bias add / residual add / GELU.
+struct mi_f16_epilogue {
+    const float * bias = nullptr;        // [N] f32, or null
+    const char * resid = nullptr;        // [N, ncols] f32 (row stride resid_nb1), or null
+    size_t resid_nb1 = 0;
+    const uint16_t * gelu_table = nullptr;  // fp16 GELU table (applied after bias), or null
+};
+bool mi_mul_mat_f16_fused_supported(int64_t K, int64_t ncols);
+// xh: optional f16 [ncols][K] activations already converted (then x is not read)
+void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh,
+                          int64_t ncols, float * dst, size_t ycol, const mi_f16_epilogue & e, hipStream_t s);
 
 // f16 weights x f16-rounded activations
 void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s);

@@ -17,6 +17,8 @@
 // These kernels carry GPT-2's f16 projections in decode (few columns) and the attention's KQ and
 // KQV products, so GPT-2 logits follow the CPU bit for bit through every dot product.
 
+#include <algorithm>
+
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
 
@@ -159,6 +161,139 @@ __global__ __launch_bounds__(256) void k_mm_f32_ord(const uint8_t * __restrict__
     }
 }
 
+// Decode-regime F16 GEMV with the activation conversion and the graph's epilogue fused in:
+//   - each workgroup converts its NC f32 activation columns to f16 in LDS (RNE, as the CPU's
+//     ggml_fp32_to_fp16_row, src/ggml.c:610-612), so no separate conversion launch;
+//   - weights stream through a two-deep register prefetch of kU 16-byte steps per lane, so a
+//     quad keeps up to 2*kU loads in flight instead of one per dependent FMA step (kU = 32 when
+//     the matrix has too few rows to fill the chip with waves, 8 otherwise);
+//   - epilogue (EPI): 1 = + bias[row], 2 = + bias[row] + resid, 3 = gelu(. + bias[row]) via the
+//     fp16 table -- the graph's following ADD / ADD / GELU nodes, each rounded as the CPU does.
+
+template <int NC, int EPI, int kU>
+__global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                   mi_src_cols x, const uint16_t * __restrict__ xh, int64_t ncols,
+                                                   float * __restrict__ dst, size_t ycol, mi_f16_epilogue e) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][K]
+    const int q = threadIdx.x & 3;
+    const int rpb = blockDim.x >> 2;
+    const int64_t row = (int64_t) blockIdx.x * rpb + (threadIdx.x >> 2);
+    const bool live = row < N;
+    const int64_t i11 = (int64_t) blockIdx.y * NC;
+    int nc = (int) (ncols - i11);
+    nc = nc > NC ? NC : nc;
+
+    // stage the activations: 16-byte loads, unrolled so each lane has its loads in flight at once
+    if (xh) {
+        // already converted (f16 [ncols][K] in scratch)
+        for (int c = 0; c < nc; c++) {
+            const uint4 * src = (const uint4 *) (xh + (i11 + c) * K);
+            uint4 * xd = (uint4 *) (xs + c * K);
+#pragma unroll 4
+            for (int64_t k = threadIdx.x; k < (K >> 3); k += blockDim.x) xd[k] = src[k];
+        }
+    } else if ((x.nb1 % 16) == 0 && ((uintptr_t) x.base % 16) == 0) {
+        const int64_t K4 = K >> 2;  // K % 8 == 0
+        for (int c = 0; c < nc; c++) {
+            const float4 * xc = (const float4 *) (x.base + (i11 + c) * x.nb1);
+            uint2 * xd = (uint2 *) (xs + c * K);
+#pragma unroll 8
+            for (int64_t k = threadIdx.x; k < K4; k += blockDim.x) {
+                const float4 v = xc[k];
+                xd[k] = make_uint2((uint32_t) mi_f2h(v.x) | ((uint32_t) mi_f2h(v.y) << 16),
+                                   (uint32_t) mi_f2h(v.z) | ((uint32_t) mi_f2h(v.w) << 16));
+            }
+        }
+    } else {
+        for (int c = 0; c < nc; c++) {
+            const float * xc = (const float *) (x.base + (i11 + c) * x.nb1);
+#pragma unroll 8
+            for (int64_t k = threadIdx.x; k < K; k += blockDim.x) xs[c * K + k] = mi_f2h(xc[k]);
+        }
+    }
+    __syncthreads();
+
+    const uint16_t * wrow = (const uint16_t *) (W + (live ? row : 0) * nb01);
+    float acc[NC][8];
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc[c][l] = 0.0f;
+
+    const int64_t nsteps = K >> 5;  // whole 32-element steps
+    auto step_compute = [&](const uint4 & wv4, int64_t st) {
+        float w[8];
+        h8_to_f(wv4, w);
+        const int64_t i = st * 32 + 8 * q;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (c < nc) {
+                float xv[8];
+                h8_to_f(*(const uint4 *) (xs + c * K + i), xv);
+#pragma unroll
+                for (int l = 0; l < 8; l++) acc[c][l] = __fmaf_rn(w[l], xv[l], acc[c][l]);
+            }
+        }
+    };
+    if (nsteps > 0) {
+        uint4 cur[kU], nxt[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) cur[u] = *(const uint4 *) (wrow + (u < nsteps ? u : nsteps - 1) * 32 + 8 * q);
+        for (int64_t s0 = 0; s0 < nsteps; s0 += kU) {
+            const int64_t s1 = s0 + kU;
+            if (s1 < nsteps) {
+#pragma unroll
+                for (int u = 0; u < kU; u++) nxt[u] = *(const uint4 *) (wrow + (s1 + u < nsteps ? s1 + u : nsteps - 1) * 32 + 8 * q);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                if (s0 + u < nsteps) step_compute(cur[u], s0 + u);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++) cur[u] = nxt[u];
+        }
+    }
+    const int64_t np = nsteps * 32;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const float r = quad_reduce_avx(acc[c]);
+        if (q == 0 && live && c < nc) {
+            double sd = (double) r;
+            for (int64_t i = np; i < K; i++) sd += (double) mul_rn(mi_h2f(wrow[i]), mi_h2f(xs[c * K + i]));
+            float v = (float) sd;
+            if (EPI >= 1) v = add_rn(v, e.bias[row]);
+            if (EPI == 2) v = add_rn(v, *(const float *) (e.resid + (i11 + c) * e.resid_nb1 + row * sizeof(float)));
+            if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
+            *(float *) ((char *) dst + (i11 + c) * ycol + row * sizeof(float)) = v;
+        }
+    }
+}
+
+template <int NC, int U>
+void launch_f16_x_u(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
+                    float * dst, size_t ycol, const mi_f16_epilogue & e, hipStream_t s, int threads) {
+    const int rpb = threads / 4;
+    const dim3 grid((unsigned) ((N + rpb - 1) / rpb), (unsigned) ((ncols + NC - 1) / NC));
+    const size_t lds = (size_t) NC * K * sizeof(uint16_t);
+    const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
+    switch (epi) {
+        case 0: hipLaunchKernelGGL((k_mmv_f16_x<NC, 0, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e); break;
+        case 1: hipLaunchKernelGGL((k_mmv_f16_x<NC, 1, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e); break;
+        case 2: hipLaunchKernelGGL((k_mmv_f16_x<NC, 2, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e); break;
+        default: hipLaunchKernelGGL((k_mmv_f16_x<NC, 3, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e); break;
+    }
+}
+
+template <int NC>
+void launch_f16_x(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
+                  float * dst, size_t ycol, const mi_f16_epilogue & e, hipStream_t s) {
+    // 64-lane workgroups (16 rows) while that still leaves >= 2 workgroups per CU, else 256;
+    // deep prefetch when there are few rows (a few thousand quads cannot hide HBM latency)
+    const int threads = N >= 16 * 1024 ? 256 : 64;
+    if (N * ((ncols + NC - 1) / NC) <= 8192) launch_f16_x_u<NC, 32>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s, threads);
+    else launch_f16_x_u<NC, 8>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s, threads);
+}
+
 ord_geom make_ord_geom(const mi_mm_desc & m, int NC) {
     ord_geom g;
     g.K = m.K;
@@ -199,4 +334,19 @@ void mi_mul_mat_f32(const mi_mm_desc & m, const mi_src_cols & x, hipStream_t s) 
     const ord_geom g = make_ord_geom(m, 1);
     const dim3 grid((unsigned) ((m.N + kQuadsPerBlock - 1) / kQuadsPerBlock), (unsigned) (m.ne11 * m.ne12 * m.ne13));
     hipLaunchKernelGGL(k_mm_f32_ord, grid, dim3(256), 0, s, (const uint8_t *) m.W, x, m.dst, g);
+}
+
+bool mi_mul_mat_f16_fused_supported(int64_t K, int64_t ncols) { return ncols >= 1 && K >= 8 && K % 8 == 0 && K <= 32768; }
+
+void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh,
+                          int64_t ncols, float * dst, size_t ycol, const mi_f16_epilogue & e, hipStream_t s) {
+    // columns per workgroup: up to 4, with the f16 activations within 64 KB of LDS
+    const int64_t cap = 32768 / K;
+    const int nc = (int) std::min<int64_t>(std::min<int64_t>(ncols, 4), std::max<int64_t>(cap, 1));
+    switch (nc) {
+        case 1: launch_f16_x<1>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s); break;
+        case 2: launch_f16_x<2>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s); break;
+        case 3: launch_f16_x<3>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s); break;
+        default: launch_f16_x<4>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s); break;
+    }
 }

@@ -33,13 +33,16 @@ __device__ __forceinline__ float sub_rn(float a, float b) { return a - b; }
 
 namespace {
 
-__device__ __forceinline__ void unflatten(int64_t i, const int64_t * ne, int64_t & i0, int64_t & i1, int64_t & i2, int64_t & i3) {
-    i0 = i % ne[0];
-    i /= ne[0];
-    i1 = i % ne[1];
-    i /= ne[1];
-    i2 = i % ne[2];
-    i3 = i / ne[2];
+// element index -> coordinates; 32-bit division (the launchers keep element counts below 2^32)
+__device__ __forceinline__ void unflatten(int64_t i64, const int64_t * ne, int64_t & i0, int64_t & i1, int64_t & i2, int64_t & i3) {
+    uint32_t i = (uint32_t) i64;
+    const uint32_t n0 = (uint32_t) ne[0], n1 = (uint32_t) ne[1], n2 = (uint32_t) ne[2];
+    i0 = i % n0;
+    i /= n0;
+    i1 = i % n1;
+    i /= n1;
+    i2 = i % n2;
+    i3 = i / n2;
 }
 
 __device__ __forceinline__ size_t off4(const size_t * nb, int64_t i0, int64_t i1, int64_t i2, int64_t i3) {
@@ -62,7 +65,8 @@ __global__ __launch_bounds__(256) void k_binary(mi_tensor_desc d, mi_tensor_desc
         int64_t i0, i1, i2, i3;
         unflatten(i, d.ne, i0, i1, i2, i3);
         const float x = ld_f(a.data + off4(a.nb, i0, i1, i2, i3), a.type);
-        const float y = ld_f(b.data + off4(b.nb, i0 % b.ne[0], i1 % b.ne[1], i2 % b.ne[2], i3 % b.ne[3]), b.type);
+        const float y = ld_f(b.data + off4(b.nb, (uint32_t) i0 % (uint32_t) b.ne[0], (uint32_t) i1 % (uint32_t) b.ne[1],
+                                          (uint32_t) i2 % (uint32_t) b.ne[2], (uint32_t) i3 % (uint32_t) b.ne[3]), b.type);
         float r;
         switch (op) {
             case MI_OP_ADD: r = x + y; break;
@@ -98,6 +102,27 @@ __global__ __launch_bounds__(256) void k_unary(mi_tensor_desc d, mi_tensor_desc 
 // element i of src (in src's logical order) -> element i of dst (dst's logical order)
 __global__ __launch_bounds__(256) void k_cpy(mi_tensor_desc d, mi_tensor_desc a, int64_t n) {
     for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        int64_t i0, i1, i2, i3, j0, j1, j2, j3;
+        unflatten(i, a.ne, i0, i1, i2, i3);
+        unflatten(i, d.ne, j0, j1, j2, j3);
+        const char * sp = a.data + off4(a.nb, i0, i1, i2, i3);
+        char * dp = d.data + off4(d.nb, j0, j1, j2, j3);
+        if (a.type == d.type && a.type == 1) *(uint16_t *) dp = *(const uint16_t *) sp;
+        else st_f(dp, d.type, ld_f(sp, a.type));
+    }
+}
+
+// up to kMaxCopies independent copies in one launch (blockIdx.y selects the copy)
+struct mi_cpy_batch {
+    mi_tensor_desc d[kMiMaxCopies], a[kMiMaxCopies];
+    int64_t n[kMiMaxCopies];
+};
+
+__global__ __launch_bounds__(256) void k_cpy_multi(mi_cpy_batch b) {
+    const int c = blockIdx.y;
+    const mi_tensor_desc & d = b.d[c];
+    const mi_tensor_desc & a = b.a[c];
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < b.n[c]; i += (int64_t) gridDim.x * blockDim.x) {
         int64_t i0, i1, i2, i3, j0, j1, j2, j3;
         unflatten(i, a.ne, i0, i1, i2, i3);
         unflatten(i, d.ne, j0, j1, j2, j3);
@@ -155,117 +180,149 @@ __device__ __forceinline__ void row_coords(int64_t r, const int64_t * ne, int64_
     i3 = r / ne[2];
 }
 
-// The CPU accumulates row sums one element at a time in double (ggml_float); double addition is
-// not associative, so the only order that reproduces its bits is the sequential one. The row is
-// staged in a float buffer (LDS when it fits, else the dst row) and one lane runs the chain.
-// SQ: sum of (double)(v*v) with v*v rounded in float first, as the CPU writes it.
+// The CPU accumulates row sums one element at a time in double (ggml_float) and then rounds
+// sum/n to float. A parallel double sum S differs from that sequential sum by at most
+// 2 n 2^-53 A (A = sum |term|; both are within n 2^-53 A of the exact sum), so whenever
+// (S - B)/n and (S + B)/n (B = 4 n 2^-53 A) round to the same float -- all but ~1e-5 of rows --
+// that float IS the CPU's result (division and rounding are monotonic). Otherwise one lane
+// replays the CPU's sequential chain. Rows are staged in a float buffer (LDS when they fit, else
+// the dst row).
+template <bool SQ> __device__ __forceinline__ float sum_term(float v) { return SQ ? mul_rn(v, v) : v; }
+
 template <bool SQ>
-__device__ __forceinline__ double seq_sum_d(const float * buf, int64_t n) {
-    double s0 = 0.0;
-    int64_t i = 0;
-    for (; i + 4 <= n; i += 4) {
-        const float4 v = *(const float4 *) (buf + i);
-        s0 += (double) (SQ ? mul_rn(v.x, v.x) : v.x);
-        s0 += (double) (SQ ? mul_rn(v.y, v.y) : v.y);
-        s0 += (double) (SQ ? mul_rn(v.z, v.z) : v.z);
-        s0 += (double) (SQ ? mul_rn(v.w, v.w) : v.w);
+__device__ float row_mean_cpu_order(const float * buf, int64_t n, double * shd) {
+    double s = 0.0, a = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const double t = (double) sum_term<SQ>(buf[i]);
+        s += t;
+        a += fabs(t);
     }
-    for (; i < n; i++) s0 += (double) (SQ ? mul_rn(buf[i], buf[i]) : buf[i]);
-    return s0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        s += __shfl_xor(s, off, 64);
+        a += __shfl_xor(a, off, 64);
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = (int) (blockDim.x >> 6);
+    if (lane == 0) {
+        shd[wave] = s;
+        shd[4 + wave] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double S = 0.0, A = 0.0;
+        for (int w = 0; w < nw; w++) {
+            S += shd[w];
+            A += shd[4 + w];
+        }
+        const double B = 4.0 * (double) n * A * 0x1p-53 + 0x1p-1074;
+        const float lo = (float) ((S - B) / (double) n);
+        const float hi = (float) ((S + B) / (double) n);
+        float r;
+        if (lo == hi) {
+            r = lo == 0.0f ? 0.0f : lo;  // the CPU's chain starts at +0.0
+        } else {
+            double q = 0.0;
+            int64_t i = 0;
+            for (; i + 8 <= n; i += 8) {
+                float v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) v[k] = buf[i + k];
+#pragma unroll
+                for (int k = 0; k < 8; k++) q += (double) sum_term<SQ>(v[k]);
+            }
+            for (; i < n; i++) q += (double) sum_term<SQ>(buf[i]);
+            r = (float) (q / (double) n);
+        }
+        shd[8] = (double) r;
+    }
+    __syncthreads();
+    const float r = (float) shd[8];
+    __syncthreads();  // shd is reused by the caller's next reduction
+    return r;
 }
 
 constexpr int kRowLds = 12288;  // floats staged in LDS (48 KB); longer rows stage in dst
 
-__global__ __launch_bounds__(256) void k_norm(mi_tensor_desc d, mi_tensor_desc a, float eps, int rms) {
+// norm / rms_norm, optionally followed by the graph's  mul(., g)  and  add(., b)  with 1-D g, b
+// broadcast over rows (each rounded separately, as the CPU's separate MUL and ADD nodes).
+__global__ __launch_bounds__(256) void k_norm(mi_tensor_desc d, mi_tensor_desc a, float eps, int rms, const float * g,
+                                              const float * bias) {
     __shared__ __attribute__((aligned(16))) float lds[kRowLds];
-    __shared__ float sh_scale, sh_mean;
+    __shared__ double shd[9];
     int64_t i1, i2, i3;
     row_coords(blockIdx.x, a.ne, i1, i2, i3);
     const char * x = a.data + off4(a.nb, 0, i1, i2, i3);
     char * y = d.data + off4(d.nb, 0, i1, i2, i3);
     const int64_t n = a.ne[0];
-    // staging buffer: LDS, or the dst row when it is contiguous f32 and the row is long
-    const bool in_lds = n <= kRowLds;
-    float * buf = in_lds ? lds : (float *) y;
-    const bool aligned = in_lds || ((uintptr_t) y % 16 == 0);
+    float * buf = n <= kRowLds ? lds : (float *) y;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) buf[i] = *(const float *) (x + i * a.nb[0]);
     __syncthreads();
+    float scale;
     if (rms) {
         // src/ggml.c:11428-11478: sum += (double)(x*x); mean = sum/n; y = x * (1/sqrtf(mean+eps))
-        if (threadIdx.x == 0) {
-            double s = 0.0;
-            if (aligned) s = seq_sum_d<true>(buf, n);
-            else for (int64_t i = 0; i < n; i++) s += (double) mul_rn(buf[i], buf[i]);
-            const float mean = (float) (s / n);
-            sh_scale = 1.0f / sqrtf(add_rn(mean, eps));
-        }
+        const float mean = row_mean_cpu_order<true>(buf, n, shd);
+        scale = 1.0f / sqrtf(add_rn(mean, eps));
+    } else {
+        // src/ggml.c:11353-11406: mean = (float)(sum x / n); v = x - mean; sum2 += (double)(v*v)
+        const float mean = row_mean_cpu_order<false>(buf, n, shd);
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) buf[i] = sub_rn(buf[i], mean);
         __syncthreads();
-        const float scale = sh_scale;
-        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) *(float *) (y + i * d.nb[0]) = mul_rn(buf[i], scale);
-        return;
+        const float variance = row_mean_cpu_order<true>(buf, n, shd);
+        scale = 1.0f / sqrtf(add_rn(variance, eps));
     }
-    // src/ggml.c:11353-11406: mean = (float)(sum x / n); v = x - mean; sum2 += (double)(v*v)
-    if (threadIdx.x == 0) {
-        double s = 0.0;
-        if (aligned) s = seq_sum_d<false>(buf, n);
-        else for (int64_t i = 0; i < n; i++) s += (double) buf[i];
-        sh_mean = (float) (s / n);
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        float v = mul_rn(buf[i], scale);
+        if (g) v = mul_rn(v, g[i]);
+        if (bias) v = add_rn(v, bias[i]);
+        *(float *) (y + i * d.nb[0]) = v;
     }
-    __syncthreads();
-    const float mean = sh_mean;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) buf[i] = sub_rn(buf[i], mean);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double s2 = 0.0;
-        if (aligned) s2 = seq_sum_d<true>(buf, n);
-        else for (int64_t i = 0; i < n; i++) s2 += (double) mul_rn(buf[i], buf[i]);
-        const float variance = (float) (s2 / n);
-        sh_scale = 1.0f / sqrtf(add_rn(variance, eps));
-    }
-    __syncthreads();
-    const float scale = sh_scale;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) *(float *) (y + i * d.nb[0]) = mul_rn(buf[i], scale);
 }
 
 // src/ggml.c:13393-13508: w = x*scale (+ mask); max; val = table_exp[fp16(w - max)] (0 for -inf);
-// sum += (double)val in order; y = val * (float)(1/sum)
+// sum += (double)val; y = val * (float)(1/sum). The vals are fp16 numbers in [0, 1] (multiples of
+// 2^-24), so every double partial sum is exact and a tree reduction equals the CPU's chain.
+// Optionally fused with the graph's preceding  scale(pre_scale)  and  diag_mask_inf(n_past)
+// (n_past < 0: none), applied in the CPU's order before soft_max's own scale.
 __global__ __launch_bounds__(256) void k_soft_max(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc mask, float scale,
-                                                  const uint16_t * exp_table) {
+                                                  const uint16_t * exp_table, float pre_scale, int n_past) {
     __shared__ __attribute__((aligned(16))) float lds[kRowLds];
     __shared__ float shf[4];
-    __shared__ float sh_inv;
+    __shared__ double shd[4];
     int64_t i1, i2, i3;
     row_coords(blockIdx.x, a.ne, i1, i2, i3);
     const char * x = a.data + off4(a.nb, 0, i1, i2, i3);
     char * y = d.data + off4(d.nb, 0, i1, i2, i3);
     const int64_t n = a.ne[0];
-    const bool in_lds = n <= kRowLds;
-    float * buf = in_lds ? lds : (float *) y;
-    const bool aligned = in_lds || ((uintptr_t) y % 16 == 0);
+    float * buf = n <= kRowLds ? lds : (float *) y;
     // the mask row is broadcast over rows: (i1 % mask.ne1), as (i1 % ne01) in the reference
     const char * mrow = mask.data ? mask.data + (size_t) (blockIdx.x % a.ne[1]) * mask.nb[1] : nullptr;
     float mx = -INFINITY;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        float w = mul_rn(*(const float *) (x + i * a.nb[0]), scale);
+        float w = *(const float *) (x + i * a.nb[0]);
+        if (n_past >= 0) {
+            w = mul_rn(w, pre_scale);
+            if (i >= n_past && i > n_past + i1) w = -INFINITY;
+        }
+        w = mul_rn(w, scale);
         if (mrow) w = add_rn(w, ld_f(mrow + i * mask.nb[0], mask.type));  // slope = 1 (max_bias = 0)
         buf[i] = w;
         mx = fmaxf(mx, w);
     }
     mx = block_max_f(mx, shf);  // includes the barrier that publishes buf
+    double s = 0.0;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
         const float w = buf[i];
-        buf[i] = w == -INFINITY ? 0.0f : mi_h2f(exp_table[mi_f2h(sub_rn(w, mx))]);
+        const float v = w == -INFINITY ? 0.0f : mi_h2f(exp_table[mi_f2h(sub_rn(w, mx))]);
+        buf[i] = v;
+        s += (double) v;
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) shd[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        // adding the 0.0 of masked entries leaves a double sum unchanged, as skipping them does
-        double sum = 0.0;
-        if (aligned) sum = seq_sum_d<false>(buf, n);
-        else for (int64_t i = 0; i < n; i++) sum += (double) buf[i];
-        sh_inv = (float) (1.0 / sum);
-    }
-    __syncthreads();
-    const float inv = sh_inv;
+    double sum = 0.0;
+    for (int w = 0; w < (int) (blockDim.x >> 6); w++) sum += shd[w];
+    const float inv = (float) (1.0 / sum);
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) *(float *) (y + i * d.nb[0]) = mul_rn(buf[i], inv);
 }
 
@@ -338,6 +395,7 @@ __global__ __launch_bounds__(256) void k_rope(mi_tensor_desc d, mi_tensor_desc a
 }
 
 unsigned grid_for(int64_t n) {
+    if (n >= (int64_t) 1 << 32) abort();  // element-wise kernels index with 32 bits
     int64_t g = (n + 255) / 256;
     return (unsigned) (g > 65536 ? 65536 : (g < 1 ? 1 : g));
 }
@@ -369,15 +427,16 @@ void mi_op_diag_mask(const mi_tensor_desc & d, const mi_tensor_desc & a, int n_p
     hipLaunchKernelGGL(k_diag_mask, dim3(grid_for(n)), dim3(256), 0, s, d, a, n_past, value, n);
 }
 
-void mi_op_norm(const mi_tensor_desc & d, const mi_tensor_desc & a, float eps, bool rms, hipStream_t s) {
+void mi_op_norm(const mi_tensor_desc & d, const mi_tensor_desc & a, float eps, bool rms, const float * g, const float * b,
+                hipStream_t s) {
     const int64_t rows = a.ne[1] * a.ne[2] * a.ne[3];
-    hipLaunchKernelGGL(k_norm, dim3((unsigned) rows), dim3(256), 0, s, d, a, eps, rms ? 1 : 0);
+    hipLaunchKernelGGL(k_norm, dim3((unsigned) rows), dim3(256), 0, s, d, a, eps, rms ? 1 : 0, g, b);
 }
 
 void mi_op_soft_max(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & mask, float scale,
-                    const uint16_t * exp_table, hipStream_t s) {
+                    const uint16_t * exp_table, float pre_scale, int n_past, hipStream_t s) {
     const int64_t rows = a.ne[1] * a.ne[2] * a.ne[3];
-    hipLaunchKernelGGL(k_soft_max, dim3((unsigned) rows), dim3(256), 0, s, d, a, mask, scale, exp_table);
+    hipLaunchKernelGGL(k_soft_max, dim3((unsigned) rows), dim3(256), 0, s, d, a, mask, scale, exp_table, pre_scale, n_past);
 }
 
 void mi_op_rope(const mi_tensor_desc & d, const mi_tensor_desc & a, const int32_t * pos, int n_dims, int mode, float freq_base,
@@ -394,4 +453,16 @@ void mi_op_rope(const mi_tensor_desc & d, const mi_tensor_desc & a, const int32_
     r.corr1 = corr1;
     const int64_t n = a.ne[0] / 2 * a.ne[1] * a.ne[2] * a.ne[3];
     hipLaunchKernelGGL(k_rope, dim3(grid_for(n)), dim3(256), 0, s, d, a, pos, r);
+}
+
+void mi_op_cpy_multi(const mi_tensor_desc * d, const mi_tensor_desc * a, int count, hipStream_t s) {
+    mi_cpy_batch b;
+    int64_t nmax = 1;
+    for (int c = 0; c < count; c++) {
+        b.d[c] = d[c];
+        b.a[c] = a[c];
+        b.n[c] = a[c].ne[0] * a[c].ne[1] * a[c].ne[2] * a[c].ne[3];
+        nmax = b.n[c] > nmax ? b.n[c] : nmax;
+    }
+    hipLaunchKernelGGL(k_cpy_multi, dim3(grid_for(nmax), (unsigned) count), dim3(256), 0, s, b);
 }

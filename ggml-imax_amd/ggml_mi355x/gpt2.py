@@ -156,9 +156,9 @@ class Model:
 
     def stats(self) -> dict:
         n = ctypes.c_int()
-        b, a, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        self.lib.gpt2_last_eval_stats(self.m, ctypes.byref(n), ctypes.byref(b), ctypes.byref(a), ctypes.byref(c))
-        return {"nodes": n.value, "us_build": b.value, "us_alloc": a.value, "us_compute": c.value}
+        b, a, i, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        self.lib.gpt2_last_eval_stats(self.m, ctypes.byref(n), ctypes.byref(b), ctypes.byref(a), ctypes.byref(i), ctypes.byref(c))
+        return {"nodes": n.value, "us_build": b.value, "us_alloc": a.value, "us_inputs": i.value, "us_compute": c.value}
 
     def tokenize(self, text: str) -> list[int]:
         buf = np.empty(4096, dtype=np.int32)

@@ -45,9 +45,10 @@ GGML_API int gpt2_eval(struct gpt2_model * model, int n_past, const int32_t * to
 GGML_API const char * gpt2_token_text(const struct gpt2_model * model, int32_t id);
 GGML_API int gpt2_tokenize(const struct gpt2_model * model, const char * text, int32_t * out, int max_tokens);
 
-// last-evaluated graph statistics: nodes, and wall-clock microseconds of build / alloc / compute
+// last-evaluated graph statistics: nodes, and wall-clock microseconds of graph build / graph
+// allocation / input upload / compute (incl. reading the logits back)
 GGML_API void gpt2_last_eval_stats(const struct gpt2_model * model, int * n_nodes, int64_t * us_build, int64_t * us_alloc,
-                                   int64_t * us_compute);
+                                   int64_t * us_inputs, int64_t * us_compute);
 
 #ifdef __cplusplus
 }

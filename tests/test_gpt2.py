@@ -171,11 +171,13 @@ def test_gpt2_long_context_decode(model_path):
         toks = rng.integers(0, 50257, size=1000).astype(np.int32)
         a = ours.eval(0, toks[:512], all_logits=False)
         b = rm.eval(0, toks[:512], all_logits=False)
-        assert _rel_err(a, b) <= LOGIT_TOL
+        e1 = _rel_err(a, b)
         a = ours.eval(512, toks[512:1000], all_logits=False)
         b = rm.eval(512, toks[512:1000], all_logits=False)
+        e2 = _rel_err(a, b)
+        print(f"long context: rel logit error {e1:.2e} (512-token prompt), {e2:.2e} (488 more)")
         assert np.isfinite(a).all()
-        assert _rel_err(a, b) <= LOGIT_TOL
+        assert e1 <= LOGIT_TOL and e2 <= LOGIT_TOL
         with pytest.raises(RuntimeError):
             ours.eval(1000, toks[:100])  # past the 1024 positions of wpe
     finally:

@@ -74,6 +74,26 @@ def test_norm_exact(libs, ne0, ne1):
     assert_exact(a, b, "norm")
 
 
+def test_norm_tie_rows_take_sequential_path(libs):
+    """Rows whose mean sits exactly on a float rounding midpoint: the certified parallel path
+    cannot decide them and the kernel must replay the CPU's sequential double sum."""
+    rows = []
+    for k in range(16):
+        r = np.zeros(8, np.float32)
+        r[0] = np.float32(1.0 + k * 2.0**-20)
+        r[1] = np.float32(2.0**-24)   # sum/8 = 0.125 + 2^-27: halfway between two floats
+        r[2 + k % 6] = np.float32(-(2.0**-30)) if k % 2 else np.float32(0.0)
+        rows.append(r)
+    x = np.concatenate(rows)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_2d(c, F32, 8, 16)
+        return [(t, x)], L.ggml_norm(c, t, 1e-5)
+
+    a, b = both(libs, build)
+    assert_exact(a, b, "norm (tie rows)")
+
+
 @pytest.mark.parametrize("ne0,ne1", [(4096, 1), (4096, 7)])
 def test_rms_norm_exact(libs, ne0, ne1):
     x = rnd(2, ne0 * ne1, 2.0)
