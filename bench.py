@@ -114,6 +114,68 @@ def _cpu_model():
     return "unknown"
 
 
+GPT2_PROMPT = "Once upon a time the cat sat on the mat and the dog ran away from the big red house"
+
+
+def gpt2_bench(lib, backend, n_decode=128, n_batch=8):
+    """BASELINE config 4: GPT-2-117M f16 (synthetic seeded weights, legacy ggml file) on MI355X.
+    Prompt in n_batch chunks, then n_decode greedy single-token steps, logits read back each step
+    (as examples/gpt-2/main-backend.cpp's gpt2_eval does). Returns decode tokens/s and the
+    reference program's ms/token definition (predict time / n_past, prompt tokens included)."""
+    from ggml_mi355x import gpt2
+    path = gpt2.ensure_model()
+    m = gpt2.Model(lib, path, backend, n_ctx=1024, n_batch=n_batch)
+    try:
+        toks = m.tokenize(GPT2_PROMPT)
+        n_past, t_pred = 0, 0.0
+        t0 = time.perf_counter()
+        for i in range(0, len(toks), n_batch):
+            lg = m.eval(n_past, toks[i:i + n_batch])
+            n_past += len(toks[i:i + n_batch])
+        t_prompt = time.perf_counter() - t0
+        nxt = int(np.argmax(lg[-1]))
+        for _ in range(8):  # warm-up decode steps (not timed), then restart the context
+            lg = m.eval(n_past, [nxt])
+            nxt = int(np.argmax(lg[-1]))
+        n_past = len(toks)
+        t0 = time.perf_counter()
+        for _ in range(n_decode):
+            lg = m.eval(n_past, [nxt])
+            n_past += 1
+            nxt = int(np.argmax(lg[-1]))
+        t_dec = time.perf_counter() - t0
+        st = m.stats()
+        t_pred = t_prompt + t_dec
+        return {"model": "GPT-2-117M f16 (synthetic seeded weights, 239.08 MB)", "decode_tokens_per_s": round(n_decode / t_dec, 1),
+                "ms_per_decode_token": round(t_dec / n_decode * 1e3, 4),
+                "prompt_tokens": len(toks), "prompt_tokens_per_s": round(len(toks) / t_prompt, 1),
+                "ms_per_token_reference_definition": round(t_pred / n_past * 1e3, 4),
+                "graph_nodes": st["nodes"], "kernel_launches_per_token": lib.ggml_backend_mi355x_last_launch_count(backend),
+                "host_us_per_token": {k: st[k] for k in ("us_build", "us_alloc", "us_inputs")},
+                "parity": "decode-path logits bit-identical to the reference CPU (tests/test_gpt2.py)"}
+    finally:
+        m.free()
+
+
+def gpt2_cpu_baseline(threads, n_predict=64):
+    """The reference's own examples/gpt-2/main-backend.cpp (oracle/_ref/gpt-2-backend, built from
+    the reference sources) on the same synthetic model, CPU backend: its printed ms per token."""
+    import re
+    import subprocess
+    exe = os.path.join(REPO, "oracle", "_ref", "gpt-2-backend")
+    if not os.path.exists(exe):
+        return None
+    from ggml_mi355x import gpt2
+    p = subprocess.run([exe, "-m", gpt2.ensure_model(), "-p", GPT2_PROMPT, "-n", str(n_predict), "-s", "1", "-t", str(threads)],
+                       capture_output=True, text=True, timeout=600)
+    mt = re.search(r"predict time =\s*([\d.]+) ms /\s*([\d.]+) ms per token", p.stdout)
+    if p.returncode != 0 or not mt:
+        return None
+    ms_tok = float(mt.group(2))
+    return {"value": round(1e3 / ms_tok, 1), "unit": "tokens/s", "ms_per_token": ms_tok, "cores": threads, "kind": "reference",
+            "sample": f"examples/gpt-2/main-backend.cpp (reference program) -n {n_predict} -t {threads}: predict time / n_past"}
+
+
 def event_time_per_step(torch, wl, stream_ptr, iters=20):
     """HIP-event duration of one step on the backend's own stream (ms)."""
     s = torch.cuda.ExternalStream(stream_ptr)
@@ -155,6 +217,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-gpt2", action="store_true")
+    ap.add_argument("--gpt2-tokens", type=int, default=128)
     args = ap.parse_args()
 
     import torch
@@ -206,7 +270,7 @@ def main():
     launches = max(launches, 1)
     bytes_per_launch = R * ub / launches
     achieved = bytes_per_launch / (step_ms / 1e3 / launches) / 1e9
-    traffic = load_traffic("k_mmv_kq_stream")
+    traffic = load_traffic("k_mmv_stream")
 
     result = {
         "metric": "Q4_K 4096x4096 mul_mat GB/s-effective (+ GPT-2 tokens/s), 1 GPU",
@@ -260,8 +324,14 @@ def main():
             w3.free()
         result["sweep"] = sweep
 
+    if rank == 0 and world == 1 and not args.no_gpt2:
+        # BASELINE config 4 (the metric's "+ GPT-2 tokens/s" half)
+        result["gpt2"] = gpt2_bench(lib, backend, args.gpt2_tokens)
+
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(t, K, N, B, args.cpu_seconds)
+        if "gpt2" in result:
+            result["gpt2"]["cpu_baseline"] = gpt2_cpu_baseline(int(os.environ.get("BENCH_CPU_THREADS", min(16, os.cpu_count() or 1))))
 
     wl.free()
     lib.ggml_backend_free(backend)

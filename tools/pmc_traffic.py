@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--tag", default="r01")
     ap.add_argument("bench_args", nargs="*")
     a = ap.parse_args()
-    bench_args = a.bench_args or ["--steps", "5", "--warmup", "2", "--no-cpu", "--no-sweep"]
+    bench_args = a.bench_args or ["--steps", "5", "--warmup", "2", "--no-cpu", "--no-sweep", "--no-gpt2"]
     out = os.path.join(REPO, "gpurun_out", f"pmc_{a.tag}")
     fetch = run_pass("FETCH_SIZE", out + "_fetch", bench_args)
     write = run_pass("WRITE_SIZE", out + "_write", bench_args)
