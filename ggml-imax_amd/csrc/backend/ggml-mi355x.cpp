@@ -724,23 +724,27 @@ struct mi_uses {
     }
 };
 
+// uses(X) = edges (consumer node, src == X) + views of X; a view V of X that is itself consumed
+// counts once for X (as the view) and once per consumer for V
 static void count_uses(const ggml_cgraph * g, mi_uses & u) {
     u.n.clear();
     for (int i = 0; i < g->n_nodes; i++) {
         const ggml_tensor * t = g->nodes[i];
         for (int s = 0; s < GGML_MAX_SRC; s++) {
-            const ggml_tensor * src = t->src[s];
-            if (!src) continue;
-            u.n[src]++;
-            if (src->view_src) u.n[src->view_src]++;
+            if (t->src[s]) u.n[t->src[s]]++;
         }
         if (t->view_src) u.n[t->view_src]++;
     }
 }
 
+// nodes already executed inside another node's fused kernel (set per graph by plan_attention)
+static thread_local const std::vector<uint8_t> * tl_absorbed = nullptr;
+
+static bool absorbed(int j) { return tl_absorbed && j < (int) tl_absorbed->size() && (*tl_absorbed)[j]; }
+
 static int next_node(const ggml_cgraph * g, int i) {
     for (int j = i + 1; j < g->n_nodes; j++) {
-        if (!is_noop(g->nodes[j])) return j;
+        if (!is_noop(g->nodes[j]) && !absorbed(j)) return j;
     }
     return -1;
 }
@@ -769,33 +773,6 @@ static const ggml_tensor * add_operand(const ggml_tensor * add, const ggml_tenso
     return nullptr;
 }
 
-static int try_fuse_norm(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
-    ggml_tensor * norm = g->nodes[i];
-    const int64_t E = norm->ne[0];
-    const int j = next_node(g, i);
-    if (j < 0 || !private_intermediate(norm, u)) return -1;
-    ggml_tensor * mul = g->nodes[j];
-    if (mul->op != GGML_OP_MUL || mul->src[0] != norm || !is_vec_f32(mul->src[1], E) || !ggml_are_same_shape(mul, norm)) return -1;
-    ggml_tensor * out = mul;
-    const float * bias = nullptr;
-    int last = j;
-    const int k = next_node(g, j);
-    if (k >= 0 && private_intermediate(mul, u)) {
-        ggml_tensor * add = g->nodes[k];
-        if (add->op == GGML_OP_ADD && add->src[0] == mul && is_vec_f32(add->src[1], E) && ggml_are_same_shape(add, mul)) {
-            out = add;
-            bias = (const float *) add->src[1]->data;
-            last = k;
-        }
-    }
-    if (out->type != GGML_TYPE_F32 || out->nb[0] != sizeof(float)) return -1;
-    if (!safe_alias(out, norm->src[0]) || overlaps(out, mul->src[1]) || (bias && overlaps(out, g->nodes[last]->src[1]))) return -1;
-    mi_op_norm(desc(out), desc(norm->src[0]), op_param_f(norm, 0), norm->op == GGML_OP_RMS_NORM,
-               (const float *) mul->src[1]->data, bias, ctx->stream);
-    ctx->last_launches++;
-    return last;
-}
-
 static int try_fuse_softmax(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
     ggml_tensor * sc = g->nodes[i];
     const int j = next_node(g, i);
@@ -815,10 +792,13 @@ static int try_fuse_softmax(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const 
     return k;
 }
 
-static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
+// pro / pro_x: the src1 of this mul_mat is the output of a norm chain (norm -> mul g -> add b)
+// that the kernel computes itself from pro_x
+static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u,
+                             const mi_norm_prologue * pro = nullptr, const ggml_tensor * pro_x = nullptr) {
     ggml_tensor * mm = g->nodes[i];
     const ggml_tensor * w = mm->src[0];
-    const ggml_tensor * x = mm->src[1];
+    const ggml_tensor * x = pro_x ? pro_x : mm->src[1];
     if (w->type != GGML_TYPE_F16 || x->type != GGML_TYPE_F32) return -1;
     if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1 || x->ne[1] > 8) return -1;
     if (w->nb[0] != 2 || w->nb[1] % 16 != 0 || (uintptr_t) w->data % 16 != 0 || x->nb[0] != sizeof(float)) return -1;
@@ -865,15 +845,225 @@ static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const
     if (bias_t && overlaps(out, bias_t)) return -1;
     if (res_t && !safe_alias(out, res_t)) return -1;
     const uint16_t * xh = nullptr;
+    if (pro && (overlaps(out, x) || (x->nb[1] % sizeof(float)) != 0)) return -1;
     if (overlaps(out, x)) {
         uint16_t * tmp = (uint16_t *) scratch_take(ctx, act_bytes(2, w->ne[0], x->ne[1]));
         mi_convert_f16(src_cols(x), w->ne[0], tmp, ctx->stream);
         ctx->last_launches++;
         xh = tmp;
     }
-    mi_mul_mat_f16_fused(w->data, w->nb[1], w->ne[0], N, src_cols(x), xh, x->ne[1], (float *) out->data, out->nb[1], e, ctx->stream);
+    const mi_norm_prologue none;
+    mi_mul_mat_f16_fused(w->data, w->nb[1], w->ne[0], N, src_cols(x), xh, x->ne[1], (float *) out->data, out->nb[1], e,
+                         pro ? *pro : none, ctx->stream);
     ctx->last_launches++;
     return last;
+}
+
+static int try_fuse_norm(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
+    ggml_tensor * norm = g->nodes[i];
+    const int64_t E = norm->ne[0];
+    const int j = next_node(g, i);
+    if (j < 0 || !private_intermediate(norm, u)) return -1;
+    ggml_tensor * mul = g->nodes[j];
+    if (mul->op != GGML_OP_MUL || mul->src[0] != norm || !is_vec_f32(mul->src[1], E) || !ggml_are_same_shape(mul, norm)) return -1;
+    ggml_tensor * out = mul;
+    const float * bias = nullptr;
+    int last = j;
+    const int k = next_node(g, j);
+    if (k >= 0 && private_intermediate(mul, u)) {
+        ggml_tensor * add = g->nodes[k];
+        if (add->op == GGML_OP_ADD && add->src[0] == mul && is_vec_f32(add->src[1], E) && ggml_are_same_shape(add, mul)) {
+            out = add;
+            bias = (const float *) add->src[1]->data;
+            last = k;
+        }
+    }
+    if (out->type != GGML_TYPE_F32 || out->nb[0] != sizeof(float)) return -1;
+    // norm chain feeding an F16 GEMV as its only consumer: one kernel for all of it
+    const int m = next_node(g, last);
+    if (m >= 0 && private_intermediate(out, u) && g->nodes[m]->op == GGML_OP_MUL_MAT && g->nodes[m]->src[1] == out &&
+        norm->src[0]->type == GGML_TYPE_F32 && norm->src[0]->nb[0] == sizeof(float) && ggml_are_same_shape(norm->src[0], out)) {
+        mi_norm_prologue pro;
+        pro.g = (const float *) mul->src[1]->data;
+        pro.b = bias;
+        pro.eps = op_param_f(norm, 0);
+        pro.mode = norm->op == GGML_OP_RMS_NORM ? 2 : 1;
+        const int r = try_fuse_f16_gemv(ctx, g, m, u, &pro, norm->src[0]);
+        if (r >= 0) return r;
+    }
+    if (!safe_alias(out, norm->src[0]) || overlaps(out, mul->src[1]) || (bias && overlaps(out, g->nodes[last]->src[1]))) return -1;
+    mi_op_norm(desc(out), desc(norm->src[0]), op_param_f(norm, 0), norm->op == GGML_OP_RMS_NORM,
+               (const float *) mul->src[1]->data, bias, ctx->stream);
+    ctx->last_launches++;
+    return last;
+}
+
+// ---- attention subgraph (examples/gpt-2/main-backend.cpp:552-608) -----------------------------
+//   KQ = mul_mat(K, permute(cont(Q))); scale; diag_mask_inf; soft_max;
+//   KQV = mul_mat(cont(permute(V)), soft_max); cont(permute(KQV))
+// becomes one k_attn_ordered launch at the KQV node; the conts of Q and V and the KQ chain are
+// absorbed (they only feed this block), reading Q, K, V through their source strides.
+
+struct mi_attn_plan {
+    int kqv;  // node index of KQV
+    const ggml_tensor * merged;  // the absorbed cont node the kernel writes
+    mi_attn_desc d;
+    // Q is read through its source strides at the KQV node. The graph allocator considers that
+    // source dead after the (absorbed) cont of Q, so `merged` may have been placed over it: then
+    // Q is copied to the backend's scratch at the cont's position instead.
+    int q_copy_at = -1;          // node index of the cont of Q, or -1
+    mi_tensor_desc q_src;        // Q through its source strides, [D, N, H]
+};
+
+// byte range [lo, hi) touched by a strided [ne0, ne1, ne2] view
+static void strided_range(const char * base, const int64_t * ne, const size_t * nb, int n, const char ** lo, const char ** hi) {
+    size_t span = 4;
+    for (int k = 0; k < n; k++) span += (size_t) (ne[k] - 1) * nb[k];
+    *lo = base;
+    *hi = base + span;
+}
+
+static int node_index(const ggml_cgraph * g, const ggml_tensor * t, const std::unordered_map<const ggml_tensor *, int> & idx) {
+    auto it = idx.find(t);
+    return it == idx.end() ? -1 : it->second;
+}
+
+// virtual strides of a PERMUTE view P of a CONT node C, read through C's source
+static bool permute_of_cont_strides(const ggml_tensor * P, size_t nb[3], const char ** base) {
+    if (P->op != GGML_OP_PERMUTE || P->ne[3] != 1) return false;
+    const ggml_tensor * C = P->src[0];
+    if (!C || C->op != GGML_OP_CONT || C->type != GGML_TYPE_F32) return false;
+    const ggml_tensor * S = C->src[0];
+    if (!S || S->type != GGML_TYPE_F32 || S->nb[0] != sizeof(float)) return false;
+    size_t vc[4];
+    if (ggml_are_same_shape(S, C)) {
+        for (int k = 0; k < 4; k++) vc[k] = S->nb[k];
+    } else if (S->ne[2] == 1 && S->ne[3] == 1 && C->ne[3] == 1 && C->ne[0] * C->ne[1] == S->ne[0] && C->ne[2] == S->ne[1]) {
+        vc[0] = sizeof(float);
+        vc[1] = (size_t) C->ne[0] * sizeof(float);
+        vc[2] = S->nb[1];
+        vc[3] = 0;
+    } else {
+        return false;
+    }
+    const int32_t * ax = (const int32_t *) P->op_params;
+    size_t vp[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 4; k++) {
+        if (ax[k] < 0 || ax[k] > 3) return false;
+        vp[ax[k]] = vc[k];
+    }
+    for (int k = 0; k < 3; k++) nb[k] = vp[k];
+    *base = (const char *) S->data;
+    return true;
+}
+
+static void plan_attention(const ggml_cgraph * g, const mi_uses & u, std::vector<uint8_t> & absorbed_nodes,
+                           std::vector<mi_attn_plan> & plans) {
+    plans.clear();
+    absorbed_nodes.assign(g->n_nodes, 0);
+    std::unordered_map<const ggml_tensor *, int> idx;
+    for (int i = 0; i < g->n_nodes; i++) idx[g->nodes[i]] = i;
+    static const bool dbg = getenv("GGML_MI355X_DEBUG_FUSION") != nullptr;
+#define MI_ATTN_SKIP(why) { if (dbg && kqv->src[1] && kqv->src[1]->op == GGML_OP_SOFT_MAX) fprintf(stderr, "attn plan: node %d: %s\n", j, why); continue; }
+    for (int j = 0; j < g->n_nodes; j++) {
+        const ggml_tensor * kqv = g->nodes[j];
+        if (kqv->op != GGML_OP_MUL_MAT || kqv->type != GGML_TYPE_F32) continue;
+        const ggml_tensor * vt = kqv->src[0];
+        const ggml_tensor * sm = kqv->src[1];
+        if (!vt || vt->op != GGML_OP_CONT || vt->type != GGML_TYPE_F32 || u.of(vt) != 1) MI_ATTN_SKIP("check 1")
+        const ggml_tensor * vsrc = vt->src[0];
+        if (!vsrc || vsrc->type != GGML_TYPE_F32 || !ggml_are_same_shape(vsrc, vt)) MI_ATTN_SKIP("check 2")
+        if (sm->op != GGML_OP_SOFT_MAX || sm->src[1] || op_param_f(sm, 1) != 0.0f || u.of(sm) != 1) MI_ATTN_SKIP("check 3")
+        const ggml_tensor * dm = sm->src[0];
+        if (dm->op != GGML_OP_DIAG_MASK_INF || u.of(dm) != 1) MI_ATTN_SKIP("check 4")
+        const ggml_tensor * sc = dm->src[0];
+        if (sc->op != GGML_OP_SCALE || u.of(sc) != 1) MI_ATTN_SKIP("check 5")
+        const ggml_tensor * kq = sc->src[0];
+        if (kq->op != GGML_OP_MUL_MAT || kq->type != GGML_TYPE_F32 || u.of(kq) != 1) MI_ATTN_SKIP("check 6")
+        const ggml_tensor * K = kq->src[0];
+        const ggml_tensor * Qp = kq->src[1];
+        if (K->type != GGML_TYPE_F32 || K->ne[3] != 1 || Qp->type != GGML_TYPE_F32 || u.of(Qp) != 1) MI_ATTN_SKIP("check 7")
+        const ggml_tensor * qc = Qp->src[0];
+        if (!qc || u.of(qc) != 2) continue;  // the permute view only (src + view_src)
+        // KQV consumer: permute -> cont (merged, contiguous)
+        int jp = -1, jm = -1;
+        for (int k = j + 1; k < g->n_nodes && jm < 0; k++) {
+            const ggml_tensor * n = g->nodes[k];
+            if (jp < 0 && n->op == GGML_OP_PERMUTE && n->src[0] == kqv) jp = k;
+            else if (jp >= 0 && n->op == GGML_OP_CONT && n->src[0] == g->nodes[jp]) jm = k;
+        }
+        if (jp < 0 || jm < 0 || u.of(kqv) != 2 || u.of(g->nodes[jp]) != 1) MI_ATTN_SKIP("check 8")
+        const ggml_tensor * P2 = g->nodes[jp];
+        const ggml_tensor * M = g->nodes[jm];
+        if (M->type != GGML_TYPE_F32 || !ggml_is_contiguous(M) || P2->ne[3] != 1) MI_ATTN_SKIP("check 9")
+
+        mi_attn_desc d;
+        const char * qbase = nullptr;
+        if (!permute_of_cont_strides(Qp, d.q_nb, &qbase)) MI_ATTN_SKIP("check 10")
+        d.q = qbase;
+        d.D = (int) K->ne[0];
+        d.n_kv = (int) K->ne[1];
+        d.H = (int) Qp->ne[2];
+        d.N = (int) Qp->ne[1];
+        if (Qp->ne[0] != K->ne[0] || K->ne[2] == 0 || d.H % K->ne[2] != 0) MI_ATTN_SKIP("check 11")
+        d.r2 = d.H / (int) K->ne[2];
+        if (vt->ne[0] != d.n_kv || vt->ne[1] != d.D || vt->ne[2] != K->ne[2]) MI_ATTN_SKIP("check 12")
+        if (!mi_attn_supported(d.D, d.n_kv)) MI_ATTN_SKIP("check 13")
+        d.k = (const char *) K->data;
+        d.v = (const char *) vsrc->data;
+        for (int k = 0; k < 3; k++) {
+            d.k_nb[k] = K->nb[k];
+            d.v_nb[k] = vsrc->nb[k];
+        }
+        // KQV (d, t, h) -> merged: linear index in P2's (permuted) order, M contiguous
+        const int32_t * ax = (const int32_t *) P2->op_params;
+        const size_t c[4] = {1, (size_t) P2->ne[0], (size_t) (P2->ne[0] * P2->ne[1]), (size_t) (P2->ne[0] * P2->ne[1] * P2->ne[2])};
+        bool ok = true;
+        for (int k = 0; k < 3; k++) {
+            if (ax[k] < 0 || ax[k] > 3) ok = false;
+            else d.o_nb[k] = c[ax[k]] * sizeof(float);
+        }
+        if (!ok) MI_ATTN_SKIP("check 14")
+        d.out = (char *) M->data;
+        d.n_past = ((const int32_t *) dm->op_params)[0];
+        d.pre_scale = op_param_f(sc, 0);
+        d.sm_scale = op_param_f(sm, 0);
+        const int absorbed_ids[] = {node_index(g, vt, idx), node_index(g, qc, idx), node_index(g, kq, idx), node_index(g, sc, idx),
+                                    node_index(g, dm, idx), node_index(g, sm, idx), jm};
+        bool all = true;
+        for (int a : absorbed_ids) all &= a >= 0;
+        if (!all) MI_ATTN_SKIP("check 15")
+        // the fused kernel writes M while other workgroups still read Q, K, V
+        const char * mlo = (const char *) M->data;
+        const char * mhi = mlo + ggml_nbytes(M);
+        const char * lo, * hi;
+        const int64_t kne[3] = {K->ne[0], K->ne[1], K->ne[2]};
+        strided_range(d.k, kne, d.k_nb, 3, &lo, &hi);
+        if (lo < mhi && mlo < hi) MI_ATTN_SKIP("check 16")
+        const int64_t vne[3] = {vsrc->ne[0], vsrc->ne[1], vsrc->ne[2]};
+        strided_range(d.v, vne, d.v_nb, 3, &lo, &hi);
+        if (lo < mhi && mlo < hi) MI_ATTN_SKIP("check 17")
+        mi_attn_plan pl;
+        pl.kqv = j;
+        pl.merged = M;
+        pl.d = d;
+        const int64_t qne[3] = {d.D, d.N, d.H};
+        strided_range(d.q, qne, d.q_nb, 3, &lo, &hi);
+        if (lo < mhi && mlo < hi) {
+            pl.q_copy_at = node_index(g, qc, idx);
+            pl.q_src.data = (char *) d.q;
+            pl.q_src.type = GGML_TYPE_F32;
+            for (int k = 0; k < 3; k++) {
+                pl.q_src.ne[k] = qne[k];
+                pl.q_src.nb[k] = d.q_nb[k];
+            }
+            pl.q_src.ne[3] = 1;
+            pl.q_src.nb[3] = 0;
+        }
+        for (int a : absorbed_ids) absorbed_nodes[a] = 1;
+        plans.push_back(pl);
+    }
+#undef MI_ATTN_SKIP
 }
 
 static bool is_copy(const ggml_tensor * t) {
@@ -917,21 +1107,62 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
     ctx->last_launches = 0;
     static const bool no_fuse = getenv("GGML_MI355X_NO_FUSED_MMV") != nullptr;
     static const bool no_node_fusion = getenv("GGML_MI355X_NO_NODE_FUSION") != nullptr;
+    // bit mask of enabled node fusions (debug/A-B): 1 norm, 2 softmax, 4 f16 GEMV, 8 copies, 16 attention
+    static const int fuse_mask = getenv("GGML_MI355X_FUSE_MASK") ? atoi(getenv("GGML_MI355X_FUSE_MASK")) : 0xff;
     mi_uses uses;
-    if (!no_node_fusion) count_uses(cgraph, uses);
+    std::vector<uint8_t> absorbed_nodes;
+    std::vector<mi_attn_plan> attn;
+    if (!no_node_fusion) {
+        count_uses(cgraph, uses);
+        if (fuse_mask & 16) plan_attention(cgraph, uses, absorbed_nodes, attn);
+    }
+    size_t q_copy_bytes = 0;
+    for (const auto & pl : attn) {
+        if (pl.q_copy_at >= 0) q_copy_bytes += ((size_t) pl.d.D * pl.d.N * pl.d.H * sizeof(float) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+    }
+    if (q_copy_bytes) {
+        scratch_reserve(ctx, graph_scratch_bytes(cgraph) + q_copy_bytes);
+        for (auto & pl : attn) {
+            if (pl.q_copy_at < 0) continue;
+            char * q = (char *) scratch_take(ctx, (size_t) pl.d.D * pl.d.N * pl.d.H * sizeof(float));
+            pl.d.q = q;
+            pl.d.q_nb[0] = sizeof(float);
+            pl.d.q_nb[1] = (size_t) pl.d.D * sizeof(float);
+            pl.d.q_nb[2] = (size_t) pl.d.D * pl.d.N * sizeof(float);
+        }
+    }
+    tl_absorbed = &absorbed_nodes;
+    size_t next_attn = 0;
     for (int i = 0; i < cgraph->n_nodes; i++) {
         ggml_tensor * node = cgraph->nodes[i];
-        if (is_noop(node)) continue;
+        if (absorbed(i) && q_copy_bytes) {
+            for (const auto & pl : attn) {
+                if (pl.q_copy_at != i) continue;
+                mi_tensor_desc dq = pl.q_src;
+                dq.data = (char *) pl.d.q;
+                for (int k = 0; k < 3; k++) dq.nb[k] = pl.d.q_nb[k];
+                mi_op_cpy(dq, pl.q_src, ctx->stream);
+                ctx->last_launches++;
+            }
+        }
+        if (is_noop(node) || absorbed(i)) continue;
+        if (next_attn < attn.size() && attn[next_attn].kqv == i) {
+            mi_attn_ordered(attn[next_attn].d, op_tables(ctx), ctx->stream);
+            ctx->last_launches++;
+            invalidate_activations(ctx, attn[next_attn].merged);  // written here, at the KQV node
+            next_attn++;
+            continue;
+        }
         int last = -1;
         if (!no_node_fusion) {
             switch (node->op) {
                 case GGML_OP_NORM:
-                case GGML_OP_RMS_NORM: last = try_fuse_norm(ctx, cgraph, i, uses); break;
-                case GGML_OP_SCALE: last = try_fuse_softmax(ctx, cgraph, i, uses); break;
-                case GGML_OP_MUL_MAT: last = try_fuse_f16_gemv(ctx, cgraph, i, uses); break;
+                case GGML_OP_RMS_NORM: last = (fuse_mask & 1) ? try_fuse_norm(ctx, cgraph, i, uses) : -1; break;
+                case GGML_OP_SCALE: last = (fuse_mask & 2) ? try_fuse_softmax(ctx, cgraph, i, uses) : -1; break;
+                case GGML_OP_MUL_MAT: last = (fuse_mask & 4) ? try_fuse_f16_gemv(ctx, cgraph, i, uses) : -1; break;
                 case GGML_OP_CPY:
                 case GGML_OP_DUP:
-                case GGML_OP_CONT: last = try_fuse_copies(ctx, cgraph, i); break;
+                case GGML_OP_CONT: last = (fuse_mask & 8) ? try_fuse_copies(ctx, cgraph, i) : -1; break;
                 default: break;
             }
         }
@@ -953,6 +1184,7 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
         }
         invalidate_activations(ctx, node);
     }
+    tl_absorbed = nullptr;
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fprintf(stderr, "%s: kernel launch failed: %s\n", __func__, hipGetErrorString(err));

@@ -227,22 +227,25 @@ static std::vector<size_t> plan_graph(ggml_gallocr * ga, ggml_cgraph * g, std::u
     std::unordered_map<ggml_tensor *, bool> pinned;
     for (auto & kv : out) pinned[kv.first] = true;
 
-    // 2) nodes in order; free bases after their last consumer
-    std::vector<std::vector<ggml_tensor *>> free_at(g->n_nodes);
+    // 2) nodes in order; a base is released kFreeDelay nodes after its last consumer, so the
+    //    outputs of the next few nodes never land on it. A backend that executes a short chain
+    //    of nodes as one kernel (ggml-mi355x.cpp node fusion) then never finds the chain's output
+    //    placed over the chain's inputs.
+    constexpr int kFreeDelay = 4;
+    std::vector<std::vector<ggml_tensor *>> release_at(g->n_nodes + kFreeDelay + 1);
     for (int i = 0; i < g->n_nodes; i++) {
         ggml_tensor * n = g->nodes[i];
         for (int s = 0; s < GGML_MAX_SRC; s++) if (n->src[s]) place(base_of(n->src[s]));
         place(n);
-        ggml_tensor * b = base_of(n);
-        if (needs_alloc(b) || out.count(b)) {
-            // nodes that are outputs (or the final node) live to the end
+        for (ggml_tensor * p : release_at[i]) {
+            const plan_entry e = out[p];
+            arenas[e.buffer_id].release(e.offset, size_of(p, e.buffer_id));
         }
         for (int s = 0; s < GGML_MAX_SRC; s++) {
             ggml_tensor * p = n->src[s] ? base_of(n->src[s]) : nullptr;
             if (!p || !out.count(p) || pinned.count(p) || (p->flags & GGML_TENSOR_FLAG_OUTPUT)) continue;
             if (last_use[p] == i) {
-                const plan_entry e = out[p];
-                arenas[e.buffer_id].release(e.offset, size_of(p, e.buffer_id));
+                release_at[i + kFreeDelay].push_back(p);
                 pinned[p] = true;  // never release twice
             }
         }

@@ -121,10 +121,37 @@ struct mi_f16_epilogue {
     size_t resid_nb1 = 0;
     const uint16_t * gelu_table = nullptr;  // fp16 GELU table (applied after bias), or null
 };
+// optional prologue: src1 = add(mul(norm|rms_norm(x, eps), g), b) computed in the kernel from x
+struct mi_norm_prologue {
+    const float * g = nullptr;  // [K] or null
+    const float * b = nullptr;  // [K] or null
+    float eps = 0.0f;
+    int mode = 0;               // 0 none, 1 norm, 2 rms_norm
+};
 bool mi_mul_mat_f16_fused_supported(int64_t K, int64_t ncols);
 // xh: optional f16 [ncols][K] activations already converted (then x is not read)
 void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh,
-                          int64_t ncols, float * dst, size_t ycol, const mi_f16_epilogue & e, hipStream_t s);
+                          int64_t ncols, float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro,
+                          hipStream_t s);
+
+// attention of the GPT-2 graph (KQ, scale, causal mask, soft_max, KQV, merge) in one launch,
+// bit-identical to the separate nodes. Strides in bytes; element (i0, i1, i2) at base + sum i*nb.
+struct mi_attn_desc {
+    const char * q;   // Q [D, N, H]
+    size_t q_nb[3];
+    const char * k;   // K [D, n_kv, Hk]
+    size_t k_nb[3];
+    const char * v;   // V_trans [n_kv, D, Hk]
+    size_t v_nb[3];
+    char * out;       // KQV (d, t, h) destination
+    size_t o_nb[3];
+    int D, N, H, n_kv, r2;  // r2 = H / Hk
+    int n_past;             // diag_mask_inf n_past
+    float pre_scale;        // ggml_scale factor
+    float sm_scale;         // soft_max scale (op_params[0])
+};
+bool mi_attn_supported(int D, int n_kv);
+void mi_attn_ordered(const mi_attn_desc & a, const uint16_t * exp_table, hipStream_t s);
 
 // f16 weights x f16-rounded activations
 void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s);

@@ -22,17 +22,7 @@
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
 
-// Bit-exactness with the CPU needs every multiply and add rounded separately unless written as
-// __fmaf_rn: HIP's __fmul_rn/__fadd_rn are plain operators defined in a header (so this file's
-// pragma does not reach them) that -ffp-contract=fast would fuse; mul_rn/add_rn below are
-// written under the pragma instead.
-#pragma clang fp contract(off)
-
-namespace {
-__device__ __forceinline__ float mul_rn(float a, float b) { return a * b; }
-__device__ __forceinline__ float add_rn(float a, float b) { return a + b; }
-__device__ __forceinline__ float sub_rn(float a, float b) { return a - b; }
-} // namespace
+#include "cpu_order.h"
 
 namespace {
 
@@ -173,8 +163,10 @@ __global__ __launch_bounds__(256) void k_mm_f32_ord(const uint8_t * __restrict__
 template <int NC, int EPI, int kU>
 __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                                    mi_src_cols x, const uint16_t * __restrict__ xh, int64_t ncols,
-                                                   float * __restrict__ dst, size_t ycol, mi_f16_epilogue e) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][K]
+                                                   float * __restrict__ dst, size_t ycol, mi_f16_epilogue e,
+                                                   mi_norm_prologue pro) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][K] f16 (+ [K] f32 for the norm prologue)
+    __shared__ double shd[9];
     const int q = threadIdx.x & 3;
     const int rpb = blockDim.x >> 2;
     const int64_t row = (int64_t) blockIdx.x * rpb + (threadIdx.x >> 2);
@@ -183,8 +175,46 @@ __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ 
     int nc = (int) (ncols - i11);
     nc = nc > NC ? NC : nc;
 
+    // The weights do not depend on the activations: the first kU steps of the row are requested
+    // before the activations are staged (and normalised), so their HBM latency overlaps that work.
+    const uint16_t * wrow = (const uint16_t *) (W + (live ? row : 0) * nb01);
+    const int64_t nsteps = K >> 5;  // whole 32-element steps
+    uint4 cur[kU];
+    if (nsteps > 0) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) cur[u] = *(const uint4 *) (wrow + (u < nsteps ? u : nsteps - 1) * 32 + 8 * q);
+    }
+
     // stage the activations: 16-byte loads, unrolled so each lane has its loads in flight at once
-    if (xh) {
+    if (pro.mode) {
+        // the graph's norm|rms_norm -> mul(g) -> add(b) producing this mul_mat's src1, computed per
+        // column exactly as k_norm does (ops.hip), then rounded to f16 as the CPU's from_float
+        float * xf = (float *) (xs + NC * K);
+        for (int c = 0; c < nc; c++) {
+            const float * xc = (const float *) (x.base + (i11 + c) * x.nb1);
+#pragma unroll 4
+            for (int64_t k = threadIdx.x; k < K; k += blockDim.x) xf[k] = xc[k];
+            __syncthreads();
+            float scale;
+            if (pro.mode == 2) {
+                const float mean = row_mean_cpu_order<true>(xf, K, shd);
+                scale = 1.0f / sqrtf(add_rn(mean, pro.eps));
+            } else {
+                const float mean = row_mean_cpu_order<false>(xf, K, shd);
+                for (int64_t k = threadIdx.x; k < K; k += blockDim.x) xf[k] = sub_rn(xf[k], mean);
+                __syncthreads();
+                const float variance = row_mean_cpu_order<true>(xf, K, shd);
+                scale = 1.0f / sqrtf(add_rn(variance, pro.eps));
+            }
+            for (int64_t k = threadIdx.x; k < K; k += blockDim.x) {
+                float v = mul_rn(xf[k], scale);
+                if (pro.g) v = mul_rn(v, pro.g[k]);
+                if (pro.b) v = add_rn(v, pro.b[k]);
+                xs[c * K + k] = mi_f2h(v);
+            }
+            __syncthreads();
+        }
+    } else if (xh) {
         // already converted (f16 [ncols][K] in scratch)
         for (int c = 0; c < nc; c++) {
             const uint4 * src = (const uint4 *) (xh + (i11 + c) * K);
@@ -213,14 +243,12 @@ __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ 
     }
     __syncthreads();
 
-    const uint16_t * wrow = (const uint16_t *) (W + (live ? row : 0) * nb01);
     float acc[NC][8];
 #pragma unroll
     for (int c = 0; c < NC; c++)
 #pragma unroll
         for (int l = 0; l < 8; l++) acc[c][l] = 0.0f;
 
-    const int64_t nsteps = K >> 5;  // whole 32-element steps
     auto step_compute = [&](const uint4 & wv4, int64_t st) {
         float w[8];
         h8_to_f(wv4, w);
@@ -236,9 +264,7 @@ __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ 
         }
     };
     if (nsteps > 0) {
-        uint4 cur[kU], nxt[kU];
-#pragma unroll
-        for (int u = 0; u < kU; u++) cur[u] = *(const uint4 *) (wrow + (u < nsteps ? u : nsteps - 1) * 32 + 8 * q);
+        uint4 nxt[kU];
         for (int64_t s0 = 0; s0 < nsteps; s0 += kU) {
             const int64_t s1 = s0 + kU;
             if (s1 < nsteps) {
@@ -271,27 +297,176 @@ __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ 
 
 template <int NC, int U>
 void launch_f16_x_u(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
-                    float * dst, size_t ycol, const mi_f16_epilogue & e, hipStream_t s, int threads) {
+                    float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int threads) {
     const int rpb = threads / 4;
     const dim3 grid((unsigned) ((N + rpb - 1) / rpb), (unsigned) ((ncols + NC - 1) / NC));
-    const size_t lds = (size_t) NC * K * sizeof(uint16_t);
+    const size_t lds = (size_t) NC * K * sizeof(uint16_t) + (pro.mode ? (size_t) K * sizeof(float) : 0);
     const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
     switch (epi) {
-        case 0: hipLaunchKernelGGL((k_mmv_f16_x<NC, 0, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e); break;
-        case 1: hipLaunchKernelGGL((k_mmv_f16_x<NC, 1, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e); break;
-        case 2: hipLaunchKernelGGL((k_mmv_f16_x<NC, 2, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e); break;
-        default: hipLaunchKernelGGL((k_mmv_f16_x<NC, 3, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e); break;
+        case 0: hipLaunchKernelGGL((k_mmv_f16_x<NC, 0, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro); break;
+        case 1: hipLaunchKernelGGL((k_mmv_f16_x<NC, 1, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro); break;
+        case 2: hipLaunchKernelGGL((k_mmv_f16_x<NC, 2, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro); break;
+        default: hipLaunchKernelGGL((k_mmv_f16_x<NC, 3, U>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro); break;
     }
 }
 
 template <int NC>
 void launch_f16_x(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
-                  float * dst, size_t ycol, const mi_f16_epilogue & e, hipStream_t s) {
+                  float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s) {
     // 64-lane workgroups (16 rows) while that still leaves >= 2 workgroups per CU, else 256;
     // deep prefetch when there are few rows (a few thousand quads cannot hide HBM latency)
     const int threads = N >= 16 * 1024 ? 256 : 64;
-    if (N * ((ncols + NC - 1) / NC) <= 8192) launch_f16_x_u<NC, 32>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s, threads);
-    else launch_f16_x_u<NC, 8>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s, threads);
+    if (N * ((ncols + NC - 1) / NC) <= 8192) launch_f16_x_u<NC, 32>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, threads);
+    else launch_f16_x_u<NC, 8>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, threads);
+}
+
+// ---- attention block of the GPT-2 graph in one kernel (main-backend.cpp:552-608) -----------------
+// For one (head h, query token t): KQ[k] = dot(K[:, k, h], Q[:, t, h]) over the head dim,
+// w = KQ * pre_scale, masked to -inf for k > n_past + t, soft_max (fp16 exp table, exact double
+// sum), then KQV[d] = dot(V_trans[:, d, h], p) over k, written straight into the merged [D*H, N]
+// layout. Every dot is ggml_vec_dot_f32's CPU order (quad per dot, as k_mm_f32_ord), every
+// rounding as the separate nodes do it, so the result is bit-identical to the unfused graph.
+
+// ggml_vec_dot_f32 order for one dot on a quad; valid in lane q == 0
+template <typename LX, typename LY>
+__device__ __forceinline__ float dot_f32_cpu_order(LX ldx, LY ldy, int64_t K, int q) {
+    float acc[8];
+#pragma unroll
+    for (int l = 0; l < 8; l++) acc[l] = 0.0f;
+    const int64_t np = K & ~(int64_t) 31;
+#pragma unroll 2
+    for (int64_t i = 8 * q; i < np; i += 32) {
+        float xv[8], yv[8];
+#pragma unroll
+        for (int l = 0; l < 8; l++) {
+            xv[l] = ldx(i + l);
+            yv[l] = ldy(i + l);
+        }
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc[l] = __fmaf_rn(xv[l], yv[l], acc[l]);
+    }
+    float s = quad_reduce_avx(acc);
+    if (q == 0) {
+        const int64_t L = K - np;
+        const int64_t fused_from = (L >= 8 ? (L / 8) * 8 : 0) + (((L >= 8 ? L % 8 : L) >= 4) ? 4 : 0);
+        for (int64_t j = 0; j < L; j++) {
+            const float a = ldx(np + j), b = ldy(np + j);
+            s = j < fused_from ? add_rn(s, mul_rn(a, b)) : __fmaf_rn(a, b, s);
+        }
+    }
+    return s;
+}
+
+// 512 lanes = 128 quads. Latency is the cost at decode sizes, so the K rows of the first KQ round
+// and the first 4 steps (128 positions) of every V column are requested before anything else.
+constexpr int kAttnThreads = 512;
+constexpr int kAttnVPre = 4;
+
+__global__ __launch_bounds__(kAttnThreads) void k_attn_ordered(mi_attn_desc a, const uint16_t * __restrict__ exp_table) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // q[D] | p[n_kv]
+    __shared__ float shf[kAttnThreads / 64];
+    __shared__ double shd[kAttnThreads / 64];
+    const int h = blockIdx.x, t = blockIdx.y;
+    const int hk = h / a.r2;  // K/V head (broadcast when Q has more heads)
+    const int q = threadIdx.x & 3, quad = threadIdx.x >> 2, nquads = blockDim.x >> 2;
+    const int nw = (int) (blockDim.x >> 6);
+    float * qv = sm;
+    float * p = sm + a.D;
+
+    // early V requests: quad d < D owns KQV column d; steps s < kAttnVPre of its ordered dot
+    const int64_t npv = (int64_t) a.n_kv & ~(int64_t) 31;
+    const int dq = quad < a.D ? quad : a.D - 1;
+    const char * vcol = a.v + (size_t) dq * a.v_nb[1] + (size_t) hk * a.v_nb[2];
+    const size_t vnb0 = a.v_nb[0];
+    float vpre[kAttnVPre][8];
+#pragma unroll
+    for (int st = 0; st < kAttnVPre; st++)
+#pragma unroll
+        for (int l = 0; l < 8; l++) {
+            const int64_t k = (int64_t) st * 32 + 8 * q + l;
+            vpre[st][l] = k < npv ? *(const float *) (vcol + k * vnb0) : 0.0f;
+        }
+
+    for (int d = threadIdx.x; d < a.D; d += blockDim.x) qv[d] = *(const float *) (a.q + d * a.q_nb[0] + t * a.q_nb[1] + h * a.q_nb[2]);
+    __syncthreads();
+    // KQ row, then pre-scale / causal mask / soft_max scale
+    for (int k0 = 0; k0 < a.n_kv; k0 += nquads) {
+        const int k = k0 + quad;
+        const int kk = k < a.n_kv ? k : a.n_kv - 1;
+        const char * krow = a.k + (size_t) kk * a.k_nb[1] + (size_t) hk * a.k_nb[2];
+        const size_t knb0 = a.k_nb[0];
+        const float v = dot_f32_cpu_order([&](int64_t i) { return *(const float *) (krow + i * knb0); },
+                                          [&](int64_t i) { return qv[i]; }, a.D, q);
+        if (q == 0 && k < a.n_kv) {
+            float w = mul_rn(v, a.pre_scale);
+            if (k >= a.n_past && k > a.n_past + t) w = -INFINITY;
+            p[k] = mul_rn(w, a.sm_scale);
+        }
+    }
+    __syncthreads();
+    float mx = -INFINITY;
+    for (int k = threadIdx.x; k < a.n_kv; k += blockDim.x) mx = fmaxf(mx, p[k]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    if ((threadIdx.x & 63) == 0) shf[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    mx = -INFINITY;
+    for (int w = 0; w < nw; w++) mx = fmaxf(mx, shf[w]);
+    double s = 0.0;
+    for (int k = threadIdx.x; k < a.n_kv; k += blockDim.x) {
+        const float w = p[k];
+        const float v = w == -INFINITY ? 0.0f : mi_h2f(exp_table[mi_f2h(sub_rn(w, mx))]);
+        p[k] = v;
+        s += (double) v;  // fp16 values: every partial double sum is exact
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) shd[threadIdx.x >> 6] = s;
+    __syncthreads();
+    double sum = 0.0;
+    for (int w = 0; w < nw; w++) sum += shd[w];
+    const float inv = (float) (1.0 / sum);
+    for (int k = threadIdx.x; k < a.n_kv; k += blockDim.x) p[k] = mul_rn(p[k], inv);
+    __syncthreads();
+
+    // KQV[d] = ggml_vec_dot_f32(n_kv, V_trans[:, d, h], p): quad d, first steps from vpre
+    for (int d0 = 0; d0 < a.D; d0 += nquads) {
+        const int d = d0 + quad;
+        const bool first = d0 == 0;
+        const int dd = d < a.D ? d : a.D - 1;
+        const char * vc = a.v + (size_t) dd * a.v_nb[1] + (size_t) hk * a.v_nb[2];
+        float acc[8];
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc[l] = 0.0f;
+        const int64_t nsteps = npv >> 5;
+        int64_t st = 0;
+        if (first) {
+#pragma unroll
+            for (int u = 0; u < kAttnVPre; u++) {
+                if (u < nsteps) {
+#pragma unroll
+                    for (int l = 0; l < 8; l++) acc[l] = __fmaf_rn(vpre[u][l], p[u * 32 + 8 * q + l], acc[l]);
+                }
+            }
+            st = nsteps < kAttnVPre ? nsteps : kAttnVPre;
+        }
+#pragma unroll 4
+        for (; st < nsteps; st++) {
+            const int64_t i = st * 32 + 8 * q;
+#pragma unroll
+            for (int l = 0; l < 8; l++) acc[l] = __fmaf_rn(*(const float *) (vc + (i + l) * vnb0), p[i + l], acc[l]);
+        }
+        float r = quad_reduce_avx(acc);
+        if (q == 0 && d < a.D) {
+            const int64_t L = a.n_kv - npv;
+            const int64_t fused_from = (L >= 8 ? (L / 8) * 8 : 0) + (((L >= 8 ? L % 8 : L) >= 4) ? 4 : 0);
+            for (int64_t j = 0; j < L; j++) {
+                const float x = *(const float *) (vc + (npv + j) * vnb0), y = p[npv + j];
+                r = j < fused_from ? add_rn(r, mul_rn(x, y)) : __fmaf_rn(x, y, r);
+            }
+            *(float *) (a.out + d * a.o_nb[0] + t * a.o_nb[1] + h * a.o_nb[2]) = r;
+        }
+    }
 }
 
 ord_geom make_ord_geom(const mi_mm_desc & m, int NC) {
@@ -336,17 +511,25 @@ void mi_mul_mat_f32(const mi_mm_desc & m, const mi_src_cols & x, hipStream_t s) 
     hipLaunchKernelGGL(k_mm_f32_ord, grid, dim3(256), 0, s, (const uint8_t *) m.W, x, m.dst, g);
 }
 
-bool mi_mul_mat_f16_fused_supported(int64_t K, int64_t ncols) { return ncols >= 1 && K >= 8 && K % 8 == 0 && K <= 32768; }
+bool mi_mul_mat_f16_fused_supported(int64_t K, int64_t ncols) { return ncols >= 1 && K >= 8 && K % 8 == 0 && K <= 10240; }
 
 void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh,
-                          int64_t ncols, float * dst, size_t ycol, const mi_f16_epilogue & e, hipStream_t s) {
-    // columns per workgroup: up to 4, with the f16 activations within 64 KB of LDS
-    const int64_t cap = 32768 / K;
+                          int64_t ncols, float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro,
+                          hipStream_t s) {
+    // columns per workgroup: up to 4, with the f16 activations (+ one f32 column) within 64 KB of LDS
+    const int64_t cap = (32768 - (pro.mode ? 2 * K : 0)) / K;
     const int nc = (int) std::min<int64_t>(std::min<int64_t>(ncols, 4), std::max<int64_t>(cap, 1));
     switch (nc) {
-        case 1: launch_f16_x<1>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s); break;
-        case 2: launch_f16_x<2>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s); break;
-        case 3: launch_f16_x<3>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s); break;
-        default: launch_f16_x<4>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, s); break;
+        case 1: launch_f16_x<1>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s); break;
+        case 2: launch_f16_x<2>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s); break;
+        case 3: launch_f16_x<3>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s); break;
+        default: launch_f16_x<4>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s); break;
     }
+}
+
+bool mi_attn_supported(int D, int n_kv) { return D >= 1 && D <= 256 && n_kv >= 1 && (size_t) (D + n_kv) * 4 <= 60 * 1024; }
+
+void mi_attn_ordered(const mi_attn_desc & a, const uint16_t * exp_table, hipStream_t s) {
+    const size_t lds = (size_t) (a.D + a.n_kv) * sizeof(float);
+    hipLaunchKernelGGL(k_attn_ordered, dim3((unsigned) a.H, (unsigned) a.N), dim3(kAttnThreads), lds, s, a, exp_table);
 }

@@ -103,7 +103,10 @@ _SIGS = {
     "ggml_cont": ([c_void_p, T], T),
     "ggml_transpose": ([c_void_p, T], T),
     "ggml_permute": ([c_void_p, T, c_int, c_int, c_int, c_int], T),
+    "ggml_view_1d": ([c_void_p, T, c_int64, c_size_t], T),
     "ggml_view_2d": ([c_void_p, T, c_int64, c_int64, c_size_t, c_size_t], T),
+    "ggml_cont_2d": ([c_void_p, T, c_int64, c_int64], T),
+    "ggml_cont_3d": ([c_void_p, T, c_int64, c_int64, c_int64], T),
     "ggml_view_3d": ([c_void_p, T, c_int64, c_int64, c_int64, c_size_t, c_size_t, c_size_t], T),
     "ggml_reshape_3d": ([c_void_p, T, c_int64, c_int64, c_int64], T),
     "ggml_new_graph": ([c_void_p], POINTER(ggml_cgraph)),

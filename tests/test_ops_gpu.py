@@ -202,6 +202,70 @@ def test_permute_cont_cpy_exact(libs):
     assert np.array_equal(a.view(np.uint16), b.view(np.uint16))
 
 
+@pytest.mark.parametrize("n_past,N", [(0, 1), (5, 1), (39, 8), (100, 28), (990, 10), (0, 512)])
+def test_gpt2_attention_block_exact(libs, n_past, N):
+    """The whole attention block of gpt2_graph (main-backend.cpp:532-608): Q/K/V views of the
+    c_attn output, K/V cache writes, cont/permute, KQ, scale, diag_mask_inf, soft_max, V_trans,
+    KQV, merge. On MI355X it runs as the fused k_attn_ordered kernel; bits must match the CPU."""
+    E, H, n_ctx = 768, 12, 1024
+    D = E // H
+    cur_v = rnd(13, 3 * E * N, 1.0)
+    mem_k = rnd(14, E * n_ctx, 1.0)
+    mem_v = rnd(15, E * n_ctx, 1.0)
+
+    def build(L, c):
+        cur = L.ggml_new_tensor_2d(c, F32, 3 * E, N)
+        mk = L.ggml_new_tensor_1d(c, F32, E * n_ctx)
+        mv = L.ggml_new_tensor_1d(c, F32, E * n_ctx)
+        nb1 = cur.contents.nb[1]
+        Qcur = L.ggml_view_2d(c, cur, E, N, nb1, 0)
+        Kcur = L.ggml_view_2d(c, cur, E, N, nb1, 4 * E)
+        Vcur = L.ggml_view_2d(c, cur, E, N, nb1, 8 * E)
+        k = L.ggml_view_1d(c, mk, N * E, 4 * E * n_past)
+        v = L.ggml_view_1d(c, mv, N * E, 4 * E * n_past)
+        ck = L.ggml_cpy(c, Kcur, k)
+        cv = L.ggml_cpy(c, Vcur, v)
+        Q = L.ggml_permute(c, L.ggml_cont_3d(c, Qcur, D, H, N), 0, 2, 1, 3)
+        K = L.ggml_permute(c, L.ggml_reshape_3d(c, L.ggml_view_1d(c, mk, (n_past + N) * E, 0), D, H, n_past + N), 0, 2, 1, 3)
+        KQ = L.ggml_mul_mat(c, K, Q)
+        sm = L.ggml_soft_max(c, L.ggml_diag_mask_inf(c, L.ggml_scale(c, KQ, 1.0 / np.sqrt(D)), n_past))
+        Vt = L.ggml_cont_3d(c, L.ggml_permute(c, L.ggml_reshape_3d(c, L.ggml_view_1d(c, mv, (n_past + N) * E, 0), D, H, n_past + N),
+                                              1, 2, 0, 3), n_past + N, D, H)
+        KQV = L.ggml_mul_mat(c, Vt, sm)
+        out = L.ggml_cont_2d(c, L.ggml_permute(c, KQV, 0, 2, 1, 3), E, N)
+        return [(cur, cur_v), (mk, mem_k), (mv, mem_v)], (out, [ck, cv])
+
+    rt, be, ref, cpu = libs
+
+    def run(L, b):
+        def bld(c):
+            feeds, (out, extra) = build(L, c)
+            return feeds, out, extra
+        return graph_once_multi(L, b, bld)
+
+    a, b = run(rt, be), run(ref, cpu)
+    assert_exact(a, b, "attention block")
+
+
+def graph_once_multi(lib, backend, build, n_tensors=96):
+    """graph_once with extra nodes expanded before the output (the K/V cache copies)."""
+    overhead = lib.ggml_tensor_overhead() * n_tensors + lib.ggml_graph_overhead()
+    with G.Context(lib, overhead, no_alloc=True) as c:
+        feeds, out, extra = build(c.ctx)
+        g = lib.ggml_new_graph(c.ctx)
+        for e in extra:
+            lib.ggml_build_forward_expand(g, e)
+        lib.ggml_build_forward_expand(g, out)
+        buf = lib.ggml_backend_alloc_ctx_tensors(c.ctx, backend)
+        try:
+            for t, arr in feeds:
+                G.tensor_set(lib, t, arr)
+            assert lib.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
+            return G.tensor_get(lib, out)
+        finally:
+            lib.ggml_backend_buffer_free(buf)
+
+
 @pytest.mark.parametrize("mode", [0, 2])
 def test_rope_close(libs, mode):
     """RoPE (LLaMA mode 0, NeoX mode 2): cos/sin come from libm on the CPU and from the device's
