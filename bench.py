@@ -176,6 +176,33 @@ def gpt2_cpu_baseline(threads, n_predict=64):
             "sample": f"examples/gpt-2/main-backend.cpp (reference program) -n {n_predict} -t {threads}: predict time / n_past"}
 
 
+def shard_range(total: int, world: int, rank: int):
+    """Balanced contiguous shard [start, start+count) of `total` units for `rank` (prompt columns
+    of a batched mul_mat: each GPU runs its columns against its own weight replica)."""
+    base, rem = divmod(total, world)
+    start = rank * base + min(rank, rem)
+    return start, base + (1 if rank < rem else 0)
+
+
+def timed_region(run, sync, dist=None, device=None):
+    """Barrier + sync on both sides of `run()`; returns the MAX wall time over ranks."""
+    sync()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run()
+    sync()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
 def event_time_per_step(torch, wl, stream_ptr, iters=20):
     """HIP-event duration of one step on the backend's own stream (ms)."""
     s = torch.cuda.ExternalStream(stream_ptr)
@@ -241,22 +268,16 @@ def main():
 
     for _ in range(args.warmup):
         wl.step()
-    lib.ggml_backend_synchronize(backend)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        wl.step()
-    lib.ggml_backend_synchronize(backend)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([dt], device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+
+    def sync():
+        lib.ggml_backend_synchronize(backend)
+        torch.cuda.synchronize()
+
+    def run_steps():
+        for _ in range(args.steps):
+            wl.step()
+
+    dt = timed_region(run_steps, sync, dist, torch.device("cuda", local_rank) if dist else None)
 
     ub = unit_bytes(t, K, N, B)
     value = R * ub * args.steps * world / dt / 1e9
@@ -323,6 +344,24 @@ def main():
                                                        "us_per_mul_mat": round(ms * 1e3 / 8, 2)}
             w3.free()
         result["sweep"] = sweep
+
+    if world > 1 and not args.no_sweep:
+        # BASELINE config 5: ONE B=512 prefill (Q4_K 4096x4096) prompt-sharded across the GPUs --
+        # each rank runs its columns against its own weight replica; no data-path collective
+        start, cnt = shard_range(512, world, rank)
+        w4 = MulMatWorkload(lib, backend, 12, 4096, 4096, cnt, 8)
+        for _ in range(3):
+            w4.step()
+
+        def run_pf():
+            for _ in range(5):
+                w4.step()
+
+        dtp = timed_region(run_pf, sync, dist, torch.device("cuda", local_rank))
+        result["prefill_sharded"] = {"workload": "8 x Q4_K 4096x4096 x B=512 per step, columns sharded over ranks",
+                                     "columns_per_rank": cnt, "TFLOP/s": round(2.0 * 4096 * 4096 * 512 * 8 * 5 / dtp / 1e12, 2),
+                                     "us_per_mul_mat": round(dtp / 5 / 8 * 1e6, 2)}
+        w4.free()
 
     if rank == 0 and world == 1 and not args.no_gpt2:
         # BASELINE config 4 (the metric's "+ GPT-2 tokens/s" half)

@@ -466,8 +466,9 @@ static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
                              mi_mmq_supported(m.type, m.K, m.nb01, m.nb1) && ((uintptr_t) m.W % 16) == 0;
         if (batched) {
             const mi_act_q8 aq = kind == 2 ? mi_act_q8{} : mi_act_q8_carve(act, m.K, ncols, kind == 1);
+            uint16_t * tmp = (uint16_t *) scratch_take(ctx, mi_mmq_scratch_bytes(m.type, m.K, ncols));
             mi_mul_mat_mmq(m.type, m.W, m.nb01, m.K, m.N, aq, kind == 2 ? (const uint16_t *) act : nullptr, ncols, m.dst,
-                           m.nb1, ctx->stream);
+                           m.nb1, tmp, ctx->stream);
         } else if (kind == 2) {
             mi_mul_mat_f16(m, (const uint16_t *) act, ctx->stream);
         } else {
@@ -634,7 +635,9 @@ static size_t graph_scratch_bytes(const ggml_cgraph * cgraph) {
         const int kind = act_kind(n->src[0]->type);
         if (kind < 0) continue;
         const ggml_tensor * b = n->src[1];
-        total += (act_bytes(kind, b->ne[0], b->ne[1] * b->ne[2] * b->ne[3]) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+        const int64_t ncols = b->ne[1] * b->ne[2] * b->ne[3];
+        total += (act_bytes(kind, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+        if (ncols > 8) total += (mi_mmq_scratch_bytes(n->src[0]->type, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
     }
     return total;
 }

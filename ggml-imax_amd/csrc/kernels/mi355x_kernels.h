@@ -83,8 +83,10 @@ void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s);
 // `ncols` activation columns already converted (act for quantized types, xh for F16),
 // dst columns of ycol bytes. Requires K % 256 == 0.
 bool mi_mmq_supported(int type, int64_t K, size_t nb01, size_t ycol);
+// scratch for the f16 expansion of quantized activations (0 for F16 weights)
+size_t mi_mmq_scratch_bytes(int type, int64_t K, int64_t ncols);
 void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_q8 & act, const uint16_t * xh,
-                    int64_t ncols, float * dst, size_t ycol, hipStream_t s);
+                    int64_t ncols, float * dst, size_t ycol, uint16_t * scratch, hipStream_t s);
 
 // ---- companion ops (ops.hip) ----
 // a tensor view as the element-wise kernels see it: f32 (type 0), f16 (1) or i32 (26) elements

@@ -1,18 +1,27 @@
 // mmq.hip -- batched GGML_OP_MUL_MAT (prompt / prefill regime, many activation columns) on the
 // gfx950 matrix cores.
 //
-// Per workgroup (256 threads = 4 wave64s) a 64 (weight rows n) x 64 (activation columns b)
-// output tile; per 256-deep K step:
-//   * weights: the 64 rows' blocks are dequantized into LDS as f16 with the reference's
-//     dequantize_row_* arithmetic (src/ggml-quants.c:980-998 q4_0, :1074-1088 q8_0,
-//     :2181-2218 q4_K, :2464-2507 q5_K; F16 weights are copied as is);
-//   * activations: columns already quantized bit-exactly like the CPU path (quantize.hip), staged
-//     as f16(d * q) -- for F16 weights the f16-rounded activations of ggml_fp32_to_fp16_row;
-//   * each wave runs v_mfma_f32_32x32x16_f16 over its 32x32 sub-tile (f32 accumulation).
-// Relative to the CPU path the only extra rounding is the f16 representation of the two
-// operands (<= 2^-11 each); the activation quantization itself is identical.
-// Rooflines: AI = 2*N*K*B / (weight bytes + 4*K*B + 4*N*B), ~650 flop/B at B=512 -> MFMA-bound
-// (f16 dense ~2.5 PF/s).
+// Activations: the columns are first quantized exactly as the CPU path quantizes them
+// (quantize.hip: q8_0 / q8_K, bit-identical) and then expanded once to f16(d * q) in a
+// [ncols][K] buffer (k_act_to_f16) -- every column tile of the GEMM reads them from there
+// instead of re-converting per tile. F16 weights use the f16-rounded activations of
+// ggml_fp32_to_fp16_row, as the CPU does.
+//
+// GEMM (k_mmq2): workgroup = 4 wave64s, output tile 64 weight rows x 128 activation columns,
+// each wave 32 rows x 64 columns = two v_mfma_f32_32x32x16_f16 per 16-deep K step sharing one
+// A fragment. Per 64-deep K stage the workgroup dequantizes its 64 x 64 weight slab into LDS
+// (16 consecutive weights per lane, the reference dequantize_row_* arithmetic:
+// src/ggml-quants.c:980-998 q4_0, :1074-1088 q8_0, :2181-2218 q4_K, :2464-2507 q5_K) and copies
+// the 128 x 64 activation slab; LDS is double-buffered, so the next stage's global loads are in
+// flight while the MFMAs of the current one run, and the dequantization of the next stage
+// follows the MFMAs (one barrier per stage).
+//
+// Relative to the CPU the only extra rounding is the f16 representation of the two operands
+// (<= 2^-11 each) and the f32 MFMA accumulation order.
+// Roofline: 2*N*K*B flops against weight bytes + 2*K*B (f16 activations) + 4*N*B -- at B=512,
+// N=K=4096 ~17.2 GFLOP over ~17 MB: MFMA-bound (f16 dense ~2.5 PF/s).
+
+#include <algorithm>
 
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
@@ -20,9 +29,9 @@
 namespace {
 
 constexpr int BM = 64;          // weight rows per tile
-constexpr int BN = 64;          // activation columns per tile
-constexpr int BK = 256;         // K per LDS stage
-constexpr int LDA = BK + 8;     // padded f16 row stride (528 B: conflict-free ds_read_b128)
+constexpr int BN = 128;         // activation columns per tile
+constexpr int BK = 64;          // K per LDS stage
+constexpr int LDS_STRIDE = BK + 8;  // padded f16 row stride (144 B)
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float float16v __attribute__((ext_vector_type(16)));
@@ -31,161 +40,201 @@ __device__ __forceinline__ uint32_t pack2h(float a, float b) {
     return (uint32_t) mi_f2h(a) | ((uint32_t) mi_f2h(b) << 16);
 }
 
-// write 8 f16 (given as f32) to LDS
-__device__ __forceinline__ void st8(_Float16 * p, const float (&v)[8]) {
-    uint4 u;
-    u.x = pack2h(v[0], v[1]);
-    u.y = pack2h(v[2], v[3]);
-    u.z = pack2h(v[4], v[5]);
-    u.w = pack2h(v[6], v[7]);
-    *(uint4 *) p = u;
-}
-
-// Dequantize 64 consecutive weights (quarter q of the 256-element K step starting at k0) of one
-// row into LDS. `row` points at the row start.
-template <int TYPE>
-__device__ __forceinline__ void dequant64(const uint8_t * row, int64_t k0, int q, _Float16 * out) {
-    if constexpr (TYPE == 12 || TYPE == 13) {
-        constexpr bool Q5 = TYPE == 13;
-        const uint8_t * blk = row + (k0 / 256) * (Q5 ? 176 : 144);
-        const uint4 hdr = *(const uint4 *) blk;
-        const float d = mi_h2f((uint16_t) (hdr.x & 0xFFFF));
-        const float dmin = mi_h2f((uint16_t) (hdr.x >> 16));
-        int sc0, m0, sc1, m1;
-        mi_scale_min_k4(2 * q, hdr.y, hdr.z, hdr.w, sc0, m0);
-        mi_scale_min_k4(2 * q + 1, hdr.y, hdr.z, hdr.w, sc1, m1);
-        const float d1 = d * sc0, mm1 = dmin * m0, d2 = d * sc1, mm2 = dmin * m1;
-        const uint8_t * qs = blk + (Q5 ? 48 : 16) + 32 * q;
-        uint32_t qw[8], hw[8];
-        const uint4 a = *(const uint4 *) qs, b = *(const uint4 *) (qs + 16);
-        qw[0] = a.x; qw[1] = a.y; qw[2] = a.z; qw[3] = a.w; qw[4] = b.x; qw[5] = b.y; qw[6] = b.z; qw[7] = b.w;
-        if constexpr (Q5) {
-            const uint4 ha = *(const uint4 *) (blk + 16), hb = *(const uint4 *) (blk + 32);
-            hw[0] = ha.x; hw[1] = ha.y; hw[2] = ha.z; hw[3] = ha.w; hw[4] = hb.x; hw[5] = hb.y; hw[6] = hb.z; hw[7] = hb.w;
+// ---- activations: q8 (+ scales) -> f16(d * q), [ncols][K] ----------------------------------
+template <int QKA>
+__global__ __launch_bounds__(256) void k_act_to_f16(mi_act_q8 act, int64_t K, uint16_t * __restrict__ out, int64_t total8) {
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < total8; i += (int64_t) gridDim.x * blockDim.x) {
+        const int64_t e0 = i * 8;                 // 8 consecutive elements of one column
+        const int64_t c = e0 / K, k = e0 - c * K;
+        const float d = act.d[c * (K / QKA) + k / QKA];
+        const int2 q = *(const int2 *) (act.qs + e0);
+        const int qq[2] = {q.x, q.y};
+        uint32_t h[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int w = qq[j >> 1];
+            const int sh = 16 * (j & 1);
+            h[j] = pack2h(d * (float) (int8_t) (w >> sh), d * (float) (int8_t) (w >> (sh + 8)));
         }
-#pragma unroll
-        for (int g = 0; g < 4; g++) {  // 8 bytes -> elements l = 8g..8g+7 (low) and 32+l (high)
-            float lo[8], hi[8];
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const int l = 8 * g + e;
-                const uint32_t byte = (qw[l >> 2] >> (8 * (l & 3))) & 0xFF;
-                int vl = byte & 0xF, vh = byte >> 4;
-                if constexpr (Q5) {
-                    const uint32_t hb8 = (hw[l >> 2] >> (8 * (l & 3))) & 0xFF;
-                    vl += (hb8 >> (2 * q)) & 1 ? 16 : 0;
-                    vh += (hb8 >> (2 * q + 1)) & 1 ? 16 : 0;
-                }
-                lo[e] = d1 * (float) vl - mm1;
-                hi[e] = d2 * (float) vh - mm2;
-            }
-            st8(out + 8 * g, lo);
-            st8(out + 32 + 8 * g, hi);
-        }
-    } else if constexpr (TYPE == 2 || TYPE == 8) {
-        constexpr bool Q8 = TYPE == 8;
-        constexpr int BS = Q8 ? 34 : 18;
-#pragma unroll
-        for (int bi = 0; bi < 2; bi++) {  // two 32-blocks per quarter
-            const uint8_t * blk = row + ((k0 + 64 * q) / 32 + bi) * BS;
-            const float d = mi_h2f((uint16_t) (blk[0] | (blk[1] << 8)));
-            float v[32];
-            if constexpr (Q8) {
-#pragma unroll
-                for (int e = 0; e < 32; e++) v[e] = (float) (int8_t) blk[2 + e] * d;
-            } else {
-#pragma unroll
-                for (int e = 0; e < 16; e++) {
-                    const int byte = blk[2 + e];
-                    v[e] = (float) ((byte & 0xF) - 8) * d;
-                    v[e + 16] = (float) ((byte >> 4) - 8) * d;
-                }
-            }
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const float (&vv)[8] = *(const float (*)[8]) (v + 8 * g);
-                st8(out + 32 * bi + 8 * g, vv);
-            }
-        }
-    } else {  // F16
-        const uint4 * src = (const uint4 *) (row + (k0 + 64 * q) * 2);
-#pragma unroll
-        for (int g = 0; g < 8; g++) *(uint4 *) (out + 8 * g) = src[g];
+        *(uint4 *) (out + e0) = make_uint4(h[0], h[1], h[2], h[3]);
     }
 }
 
+// ---- weights: raw loads for 16 consecutive elements of one row, then dequantization ----------
+// The raw registers are loaded before a stage's MFMAs and dequantized after them.
 template <int TYPE>
-__global__ __launch_bounds__(256) void k_mmq_f16(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
-                                                 mi_act_q8 act, const uint16_t * __restrict__ xh, int64_t ncols,
-                                                 float * __restrict__ dst, size_t ycol) {
-    __shared__ __attribute__((aligned(16))) _Float16 lw[BM * LDA];
-    __shared__ __attribute__((aligned(16))) _Float16 lx[BN * LDA];
+struct WRaw;
+
+// Q4_K / Q5_K: header (d, dmin, 12 scale bytes) + 16 quant bytes (+ 16 qh bytes)
+template <int TYPE>
+struct WRaw {
+    static constexpr bool Q5 = TYPE == 13;
+    static constexpr int BS = Q5 ? 176 : 144;
+    uint4 hdr, qs, qh;
+    __device__ __forceinline__ void load(const uint8_t * row, int64_t k) {
+        // k: first of the 16 elements; within superblock s = k/256, 64-group j, part p = 0..3
+        const uint8_t * blk = row + (k >> 8) * BS;
+        const int p = (int) (k & 63) >> 4;  // 16-element part of the 64-group
+        const int j = (int) (k & 255) >> 6;
+        hdr = *(const uint4 *) blk;
+        qs = *(const uint4 *) (blk + (Q5 ? 48 : 16) + 32 * j + 16 * (p & 1));
+        if constexpr (Q5) qh = *(const uint4 *) (blk + 16 + 16 * (p & 1));
+    }
+    __device__ __forceinline__ void dequant(int64_t k, float (&v)[16]) const {
+        const int p = (int) (k & 63) >> 4;
+        const int j = (int) (k & 255) >> 6;
+        const bool high = p >= 2;  // elements 32..63 of the group: high nibbles, subblock 2j+1
+        const float d = mi_h2f((uint16_t) (hdr.x & 0xFFFF));
+        const float dmin = mi_h2f((uint16_t) (hdr.x >> 16));
+        int sc, m;
+        mi_scale_min_k4(2 * j + (high ? 1 : 0), hdr.y, hdr.z, hdr.w, sc, m);
+        const float d1 = d * sc, m1 = dmin * m;
+        const uint32_t q[4] = {qs.x, qs.y, qs.z, qs.w};
+        const uint32_t h[4] = {qh.x, qh.y, qh.z, qh.w};
+        const int hbit = 2 * j + (high ? 1 : 0);
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            const uint32_t byte = (q[e >> 2] >> (8 * (e & 3))) & 0xFF;
+            int val = high ? (int) (byte >> 4) : (int) (byte & 0xF);
+            if constexpr (Q5) val += ((h[e >> 2] >> (8 * (e & 3) + hbit)) & 1) ? 16 : 0;
+            v[e] = d1 * (float) val - m1;
+        }
+    }
+};
+
+// Q4_0 (18 B) / Q8_0 (34 B): 2-byte aligned blocks; dword loads re-aligned with v_alignbyte
+template <bool Q8>
+struct WRawQ0 {
+    static constexpr int BS = Q8 ? 34 : 18;
+    static constexpr int NW = Q8 ? 5 : 5;  // dwords covering the 16 quant bytes + misalignment
+    uint32_t w[NW];
+    uint32_t shift;
+    uint32_t dbits;
+    __device__ __forceinline__ void load(const uint8_t * row, int64_t k) {
+        const uint8_t * blk = row + (k >> 5) * BS;
+        const int half = (int) (k & 31) >> 4;  // Q8_0: bytes 16*half..; Q4_0: nibble half
+        const uint8_t * qp = blk + 2 + (Q8 ? 16 * half : 0);
+        const uintptr_t a = (uintptr_t) qp;
+        const uint32_t * wp = (const uint32_t *) (a & ~(uintptr_t) 3);
+        shift = (uint32_t) (a & 3);
+#pragma unroll
+        for (int i = 0; i < NW; i++) w[i] = wp[i];  // buffers carry 256 B of tail slack
+        dbits = *(const uint16_t *) blk;
+    }
+    __device__ __forceinline__ void dequant(int64_t k, float (&v)[16]) const {
+        const int half = (int) (k & 31) >> 4;
+        const float d = mi_h2f((uint16_t) dbits);
+        uint32_t t[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) t[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shift);
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            const uint32_t byte = (t[e >> 2] >> (8 * (e & 3))) & 0xFF;
+            if constexpr (Q8) {
+                v[e] = (float) (int8_t) byte * d;
+            } else {
+                const int q = half ? (int) (byte >> 4) : (int) (byte & 0xF);
+                v[e] = (float) (q - 8) * d;
+            }
+        }
+    }
+};
+
+struct WRawF16 {
+    uint4 a, b;
+    __device__ __forceinline__ void load(const uint8_t * row, int64_t k) {
+        a = *(const uint4 *) (row + k * 2);
+        b = *(const uint4 *) (row + k * 2 + 16);
+    }
+};
+
+template <int TYPE> struct raw_of { using T = WRaw<TYPE>; };
+template <> struct raw_of<2> { using T = WRawQ0<false>; };
+template <> struct raw_of<8> { using T = WRawQ0<true>; };
+template <> struct raw_of<1> { using T = WRawF16; };
+
+// ---- the GEMM ---------------------------------------------------------------------------------
+template <int TYPE>
+__global__ __launch_bounds__(256) void k_mmq2(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                              const uint16_t * __restrict__ xh, int64_t ncols, float * __restrict__ dst,
+                                              size_t ycol) {
+    __shared__ __attribute__((aligned(16))) _Float16 la[2][BM * LDS_STRIDE];
+    __shared__ __attribute__((aligned(16))) _Float16 lb[2][BN * LDS_STRIDE];
+    using Raw = typename raw_of<TYPE>::T;
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int64_t n0 = (int64_t) blockIdx.x * BM;
     const int64_t b0 = (int64_t) blockIdx.y * BN;
-    const int wm = wave & 1, wb = wave >> 1;
-    float16v acc = {};
+    const int wm = wave & 1, wb = wave >> 1;  // wave sub-tile: rows wm*32.., columns wb*64..
 
-    // staging roles: thread t -> row/column t/4, quarter t%4 (64 elements)
-    const int sr = tid >> 2, sq = tid & 3;
-    const int64_t wrow = n0 + sr, xcol = b0 + sr;
-    constexpr bool QK = TYPE == 12 || TYPE == 13;
+    // staging roles: weights -- thread t: row t/4, 16 elements at (t%4)*16;
+    //                activations -- thread t: column t/2, 32 elements at (t%2)*32
+    const int ar = tid >> 2, ak = (tid & 3) * 16;
+    const int bc = tid >> 1, bk = (tid & 1) * 32;
+    const int64_t arow = n0 + ar;
+    const bool alive = arow < N;
+    const uint8_t * wrow = W + (alive ? arow : 0) * nb01;
+    const int64_t bcol = b0 + bc;
+    const bool blive = bcol < ncols;
+    const uint16_t * xcol = xh + (blive ? bcol : 0) * K;
 
-    for (int64_t k0 = 0; k0 < K; k0 += BK) {
-        // weights -> f16 LDS
-        if (wrow < N) {
-            dequant64<TYPE>(W + wrow * nb01, k0, sq, lw + sr * LDA + 64 * sq);
+    Raw raw;
+    uint4 xb[4];
+    auto load_stage = [&](int64_t k0) {
+        raw.load(wrow, k0 + ak);
+#pragma unroll
+        for (int i = 0; i < 4; i++) xb[i] = *(const uint4 *) (xcol + k0 + bk + 8 * i);
+    };
+    auto store_stage = [&](int buf, int64_t k0) {
+        _Float16 * pa = la[buf] + ar * LDS_STRIDE + ak;
+        if constexpr (TYPE == 1) {
+            *(uint4 *) pa = alive ? raw.a : make_uint4(0, 0, 0, 0);
+            *(uint4 *) (pa + 8) = alive ? raw.b : make_uint4(0, 0, 0, 0);
         } else {
-#pragma unroll
-            for (int g = 0; g < 8; g++) *(uint4 *) (lw + sr * LDA + 64 * sq + 8 * g) = make_uint4(0, 0, 0, 0);
+            float v[16];
+            raw.dequant(k0 + ak, v);
+            uint4 u0, u1;
+            u0.x = pack2h(v[0], v[1]);   u0.y = pack2h(v[2], v[3]);   u0.z = pack2h(v[4], v[5]);   u0.w = pack2h(v[6], v[7]);
+            u1.x = pack2h(v[8], v[9]);   u1.y = pack2h(v[10], v[11]); u1.z = pack2h(v[12], v[13]); u1.w = pack2h(v[14], v[15]);
+            if (!alive) u0 = u1 = make_uint4(0, 0, 0, 0);
+            *(uint4 *) pa = u0;
+            *(uint4 *) (pa + 8) = u1;
         }
-        // activations -> f16 LDS
-        _Float16 * xo = lx + sr * LDA + 64 * sq;
-        if (xcol < ncols) {
-            if constexpr (TYPE == 1) {
-                const uint4 * src = (const uint4 *) (xh + xcol * K + k0 + 64 * sq);
+        _Float16 * pb = lb[buf] + bc * LDS_STRIDE + bk;
 #pragma unroll
-                for (int g = 0; g < 8; g++) *(uint4 *) (xo + 8 * g) = src[g];
-            } else {
-                const int8_t * qs = act.qs + xcol * K + k0 + 64 * sq;
-                const int4 * q4 = (const int4 *) qs;
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const int4 w = q4[g];
-                    const int ww[4] = {w.x, w.y, w.z, w.w};
-                    // the 16 quants of this group share one scale (32-block or 256-superblock)
-                    const float d = QK ? act.d[xcol * (K / 256) + k0 / 256]
-                                       : act.d[xcol * (K / 32) + (k0 + 64 * sq + 16 * g) / 32];
-                    float v[16];
-#pragma unroll
-                    for (int e = 0; e < 16; e++) v[e] = d * (float) (int8_t) (ww[e >> 2] >> (8 * (e & 3)));
-                    st8(xo + 16 * g, *(const float (*)[8]) v);
-                    st8(xo + 16 * g + 8, *(const float (*)[8]) (v + 8));
-                }
-            }
-        } else {
-#pragma unroll
-            for (int g = 0; g < 8; g++) *(uint4 *) (xo + 8 * g) = make_uint4(0, 0, 0, 0);
-        }
-        __syncthreads();
+        for (int i = 0; i < 4; i++) *(uint4 *) (pb + 8 * i) = blive ? xb[i] : make_uint4(0, 0, 0, 0);
+    };
 
-        // 32x32 sub-tile per wave: A = weights (rows n), B = activations (columns b)
-        const int r = lane & 31, h = lane >> 5;
-        const _Float16 * pa = lw + (wm * 32 + r) * LDA + 8 * h;
-        const _Float16 * pb = lx + (wb * 32 + r) * LDA + 8 * h;
+    float16v acc0 = {}, acc1 = {};
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t nst = K / BK;
+    load_stage(0);
+    store_stage(0, 0);
+    __syncthreads();
+    for (int64_t st = 0; st < nst; st++) {
+        const int cur = (int) (st & 1);
+        if (st + 1 < nst) load_stage((st + 1) * BK);
+        const _Float16 * pa = la[cur] + (wm * 32 + r) * LDS_STRIDE + 8 * h;
+        const _Float16 * pb0 = lb[cur] + (wb * 64 + r) * LDS_STRIDE + 8 * h;
+        const _Float16 * pb1 = pb0 + 32 * LDS_STRIDE;
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 16) {
             const half8 a = *(const half8 *) (pa + kk);
-            const half8 b = *(const half8 *) (pb + kk);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
+            const half8 x0 = *(const half8 *) (pb0 + kk);
+            const half8 x1 = *(const half8 *) (pb1 + kk);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, x0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, x1, acc1, 0, 0, 0);
         }
+        if (st + 1 < nst) store_stage(cur ^ 1, (st + 1) * BK);
         __syncthreads();
     }
 
     // D[n][b]: column b = lane & 31, rows n = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
-    const int64_t b = b0 + wb * 32 + (lane & 31);
-    if (b < ncols) {
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+        const float16v & acc = half ? acc1 : acc0;
+        const int64_t b = b0 + wb * 64 + 32 * half + (lane & 31);
+        if (b >= ncols) continue;
         float * out = (float *) ((char *) dst + b * ycol);
 #pragma unroll
         for (int g = 0; g < 4; g++) {
@@ -204,21 +253,33 @@ __global__ __launch_bounds__(256) void k_mmq_f16(const uint8_t * __restrict__ W,
 
 bool mi_mmq_supported(int type, int64_t K, size_t nb01, size_t ycol) {
     if (type != 12 && type != 13 && type != 2 && type != 8 && type != 1) return false;
-    if (K % BK != 0) return false;
+    if (K % 256 != 0) return false;
     if (type == 1 && nb01 % 16 != 0) return false;
     return ycol % 16 == 0;
 }
 
+size_t mi_mmq_scratch_bytes(int type, int64_t K, int64_t ncols) {
+    return type == 1 ? 0 : (size_t) K * ncols * sizeof(uint16_t);
+}
+
 void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_q8 & act, const uint16_t * xh,
-                    int64_t ncols, float * dst, size_t ycol, hipStream_t s) {
+                    int64_t ncols, float * dst, size_t ycol, uint16_t * scratch, hipStream_t s) {
+    if (type != 1) {
+        // quantized activations -> f16(d * q) once for all column tiles
+        const int64_t total8 = K * ncols / 8;
+        const unsigned grid = (unsigned) std::min<int64_t>((total8 + 255) / 256, 8192);
+        if (type == 12 || type == 13) hipLaunchKernelGGL(k_act_to_f16<256>, dim3(grid), dim3(256), 0, s, act, K, scratch, total8);
+        else hipLaunchKernelGGL(k_act_to_f16<32>, dim3(grid), dim3(256), 0, s, act, K, scratch, total8);
+        xh = scratch;
+    }
     const dim3 grid((unsigned) ((N + BM - 1) / BM), (unsigned) ((ncols + BN - 1) / BN));
     const uint8_t * w = (const uint8_t *) W;
     switch (type) {
-        case 12: hipLaunchKernelGGL(k_mmq_f16<12>, grid, dim3(256), 0, s, w, nb01, K, N, act, xh, ncols, dst, ycol); break;
-        case 13: hipLaunchKernelGGL(k_mmq_f16<13>, grid, dim3(256), 0, s, w, nb01, K, N, act, xh, ncols, dst, ycol); break;
-        case 2: hipLaunchKernelGGL(k_mmq_f16<2>, grid, dim3(256), 0, s, w, nb01, K, N, act, xh, ncols, dst, ycol); break;
-        case 8: hipLaunchKernelGGL(k_mmq_f16<8>, grid, dim3(256), 0, s, w, nb01, K, N, act, xh, ncols, dst, ycol); break;
-        case 1: hipLaunchKernelGGL(k_mmq_f16<1>, grid, dim3(256), 0, s, w, nb01, K, N, act, xh, ncols, dst, ycol); break;
+        case 12: hipLaunchKernelGGL(k_mmq2<12>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
+        case 13: hipLaunchKernelGGL(k_mmq2<13>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
+        case 2: hipLaunchKernelGGL(k_mmq2<2>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
+        case 8: hipLaunchKernelGGL(k_mmq2<8>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
+        case 1: hipLaunchKernelGGL(k_mmq2<1>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
         default: break;
     }
 }
