@@ -12,6 +12,9 @@
 // oracle/, which gives the CPU logits).
 
 #include "gpt2-mi355x.h"
+#ifdef GPT2_WITH_SCHED
+#include "ggml_sched_abi.h"
+#endif
 
 #include <cmath>
 #include <cstdio>
@@ -58,11 +61,53 @@ struct gpt2_model {
     int last_nodes = 0;
     int64_t us_build = 0, us_alloc = 0, us_inputs = 0, us_compute = 0;
     std::vector<int32_t> tok, pos;  // input staging, alive until the next eval
+    // scheduler mode (examples/gpt-2/main-sched.cpp): layers split over backends
+    std::vector<ggml_backend_t> backends;       // [gpu, ..., cpu]
+    std::vector<ggml_backend_buffer_t> buffers_w;
+    ggml_backend_buffer_t buffer_input = nullptr;
+    ggml_context * ctx_in = nullptr;
+    ggml_tensor * embd_in = nullptr, * pos_in = nullptr;  // persistent input tensors
+    void * sched = nullptr;                     // ggml_backend_sched_t
+    int n_gpu_layers = 0;
 };
 
 namespace {
 
 template <typename T> bool rd(std::ifstream & f, T & v) { return (bool) f.read((char *) &v, sizeof(T)); }
+
+// main-sched.cpp:306-366: wte/wpe on the GPU only when every layer is, ln_f/lm_head on the GPU
+// when any layer is, layer il on the GPU when il >= n_layer - n_gpu_layers; one buffer per backend
+bool place_weights_sched(gpt2_model & m) {
+    ggml_backend_t gpu = m.backends.front(), cpu = m.backends.back();
+    const int first_gpu_layer = m.hp.n_layer - m.n_gpu_layers;
+    std::map<ggml_tensor *, ggml_backend_t> where;
+    for (auto & kv : m.tensors) {
+        const std::string & name = kv.first;
+        ggml_backend_t b = cpu;
+        if (name == "model/wte" || name == "model/wpe") b = m.n_gpu_layers > m.hp.n_layer ? gpu : cpu;
+        else if (name == "model/ln_f/g" || name == "model/ln_f/b" || name == "model/lm_head") b = m.n_gpu_layers > 0 ? gpu : cpu;
+        else if (name.compare(0, 7, "model/h") == 0) b = std::stoi(name.substr(7, 2)) >= first_gpu_layer ? gpu : cpu;
+        where[kv.second] = b;
+    }
+    for (ggml_backend_t b : m.backends) {
+        size_t size = 0;
+        for (auto & kv : where) if (kv.second == b) size += ggml_nbytes(kv.first) + 512;
+        if (size == 0) {
+            m.buffers_w.push_back(nullptr);
+            continue;
+        }
+        ggml_backend_buffer_t buf = ggml_backend_alloc_buffer(b, size);
+        if (!buf) {
+            fprintf(stderr, "gpt2_model_load: %s weight buffer allocation failed\n", ggml_backend_name(b));
+            return false;
+        }
+        ggml_backend_buffer_set_usage(buf, GGML_BACKEND_BUFFER_USAGE_WEIGHTS);
+        m.buffers_w.push_back(buf);
+        ggml_tallocr alloc = ggml_tallocr_new(buf);
+        for (auto & kv : where) if (kv.second == b) ggml_tallocr_alloc(&alloc, kv.first);
+    }
+    return true;
+}
 
 bool load_file(gpt2_model & m, const char * fname, int n_ctx_override) {
     std::ifstream fin(fname, std::ios::binary);
@@ -154,15 +199,20 @@ bool load_file(gpt2_model & m, const char * fname, int n_ctx_override) {
             m.tensors[p + "/mlp/c_proj/b"] = L.c_mlp_proj_b;
         }
     }
-    m.buffer_w = ggml_backend_alloc_ctx_tensors(m.ctx_w, m.backend);
-    if (!m.buffer_w) {
-        fprintf(stderr, "gpt2_model_load: weight buffer allocation failed\n");
+    if (m.backends.empty()) {
+        m.buffer_w = ggml_backend_alloc_ctx_tensors(m.ctx_w, m.backend);
+        if (!m.buffer_w) {
+            fprintf(stderr, "gpt2_model_load: weight buffer allocation failed\n");
+            return false;
+        }
+    } else if (!place_weights_sched(m)) {
         return false;
     }
 
     if (n_ctx_override > 0) hp.n_ctx = n_ctx_override;
 
-    // KV memory, f32, n_layer*n_ctx*n_embd each (:306-343)
+    // KV memory, f32, n_layer*n_ctx*n_embd each (:306-343; main-sched.cpp:367-403 puts it on the
+    // GPU when at least half the layers are there)
     {
         ggml_init_params ip = {ggml_tensor_overhead() * 2, nullptr, true};
         m.ctx_kv = ggml_init(ip);
@@ -170,7 +220,9 @@ bool load_file(gpt2_model & m, const char * fname, int n_ctx_override) {
         const int64_t n_elements = (int64_t) hp.n_embd * hp.n_layer * hp.n_ctx;
         m.memory_k = ggml_new_tensor_1d(m.ctx_kv, GGML_TYPE_F32, n_elements);
         m.memory_v = ggml_new_tensor_1d(m.ctx_kv, GGML_TYPE_F32, n_elements);
-        m.buffer_kv = ggml_backend_alloc_ctx_tensors(m.ctx_kv, m.backend);
+        ggml_backend_t be_kv = m.backend;
+        if (!m.backends.empty()) be_kv = m.n_gpu_layers >= hp.n_layer / 2 ? m.backends.front() : m.backends.back();
+        m.buffer_kv = ggml_backend_alloc_ctx_tensors(m.ctx_kv, be_kv);
         if (!m.buffer_kv) {
             fprintf(stderr, "gpt2_model_load: KV buffer allocation failed\n");
             return false;
@@ -211,7 +263,7 @@ bool load_file(gpt2_model & m, const char * fname, int n_ctx_override) {
             return false;
         }
         const size_t nb = ggml_nbytes(t);
-        if (ggml_backend_buffer_is_host(m.buffer_w)) {
+        if (t->buffer && ggml_backend_buffer_is_host(t->buffer)) {
             fin.read((char *) t->data, nb);
         } else {
             buf.resize(nb);
@@ -240,12 +292,19 @@ ggml_cgraph * build_graph(gpt2_model & m, int n_past, int N) {
     ggml_context * ctx = ggml_init(ip);
     ggml_cgraph * gf = ggml_new_graph_custom(ctx, kMaxNodes, false);
 
-    ggml_tensor * embd = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, N);
-    ggml_set_name(embd, "embd");
-    ggml_set_input(embd);
-    ggml_tensor * position = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, N);
-    ggml_set_name(position, "position");
-    ggml_set_input(position);
+    ggml_tensor * embd, * position;
+    if (m.embd_in) {
+        // scheduler mode: views of persistent input tensors (main-sched.cpp:562-570)
+        embd = ggml_view_1d(ctx, m.embd_in, N, 0);
+        position = ggml_view_1d(ctx, m.pos_in, N, 0);
+    } else {
+        embd = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, N);
+        ggml_set_name(embd, "embd");
+        ggml_set_input(embd);
+        position = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, N);
+        ggml_set_name(position, "position");
+        ggml_set_input(position);
+    }
 
     ggml_tensor * inpL = ggml_add(ctx, ggml_get_rows(ctx, m.wte, embd), ggml_get_rows(ctx, m.wpe, position));
 
@@ -353,8 +412,71 @@ gpt2_model * gpt2_model_load(const char * fname, ggml_backend_t backend, int n_c
     return m;
 }
 
+gpt2_model * gpt2_model_load_sched(const char * fname, ggml_backend_t * backends, int n_backends, int n_gpu_layers, int n_ctx,
+                                   int n_batch) {
+#ifdef GPT2_WITH_SCHED
+    if (!backends || n_backends < 1) {
+        fprintf(stderr, "gpt2_model_load_sched: no backends\n");
+        return nullptr;
+    }
+    auto * m = new gpt2_model();
+    m->backends.assign(backends, backends + n_backends);
+    m->backend = backends[n_backends - 1];
+    m->n_gpu_layers = n_backends > 1 ? n_gpu_layers : 0;
+    if (!load_file(*m, fname, n_ctx)) {
+        gpt2_model_free(m);
+        return nullptr;
+    }
+    // persistent inputs (main-sched.cpp:512-534): on the GPU only when every layer is
+    {
+        ggml_init_params ip = {ggml_tensor_overhead() * 2, nullptr, true};
+        m->ctx_in = ggml_init(ip);
+        m->embd_in = ggml_new_tensor_1d(m->ctx_in, GGML_TYPE_I32, m->hp.n_ctx);
+        m->pos_in = ggml_new_tensor_1d(m->ctx_in, GGML_TYPE_I32, m->hp.n_ctx);
+        ggml_set_name(m->embd_in, "in/embd");
+        ggml_set_name(m->pos_in, "in/position");
+        ggml_backend_t be_in = m->n_gpu_layers >= m->hp.n_layer ? m->backends.front() : m->backends.back();
+        m->buffer_input = ggml_backend_alloc_ctx_tensors(m->ctx_in, be_in);
+        if (!m->buffer_input) {
+            gpt2_model_free(m);
+            return nullptr;
+        }
+    }
+    auto * sched = ggml_backend_sched_new(m->backends.data(), nullptr, n_backends, kMaxNodes, false);
+    m->sched = sched;
+    const int n_tokens = std::min(m->hp.n_ctx, n_batch > 0 ? n_batch : 8);
+    ggml_cgraph * gf = build_graph(*m, m->hp.n_ctx - n_tokens, n_tokens);
+    if (!ggml_backend_sched_reserve(sched, gf)) {
+        fprintf(stderr, "gpt2_model_load_sched: compute buffer reservation failed\n");
+        gpt2_model_free(m);
+        return nullptr;
+    }
+    return m;
+#else
+    (void) fname; (void) backends; (void) n_backends; (void) n_gpu_layers; (void) n_ctx; (void) n_batch;
+    fprintf(stderr, "gpt2_model_load_sched: this build has no ggml_backend_sched (link the driver against a libggml "
+                    "that provides it, e.g. oracle/_ref/libgpt2_ref.so)\n");
+    return nullptr;
+#endif
+}
+
+int gpt2_sched_n_splits(const gpt2_model * m) {
+#ifdef GPT2_WITH_SCHED
+    return m->sched ? ggml_backend_sched_get_n_splits((ggml_backend_sched_t) m->sched) : 0;
+#else
+    (void) m;
+    return 0;
+#endif
+}
+
 void gpt2_model_free(gpt2_model * m) {
     if (!m) return;
+#ifdef GPT2_WITH_SCHED
+    if (m->sched) ggml_backend_sched_free((ggml_backend_sched_t) m->sched);
+#endif
+    if (m->buffer_input) ggml_backend_buffer_free(m->buffer_input);
+    if (m->ctx_in) ggml_free(m->ctx_in);
+    for (ggml_backend_buffer_t b : m->buffers_w) if (b) ggml_backend_buffer_free(b);
     if (m->allocr) ggml_gallocr_free(m->allocr);
     if (m->buffer_w) ggml_backend_buffer_free(m->buffer_w);
     if (m->buffer_kv) ggml_backend_buffer_free(m->buffer_kv);
@@ -380,6 +502,33 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
             return 1;
         }
     }
+#ifdef GPT2_WITH_SCHED
+    if (m->sched) {
+        // main-sched.cpp:854-884: inputs into the persistent tensors, sched reset + compute
+        const int64_t t0 = now_us();
+        ggml_backend_tensor_set(m->embd_in, tokens, 0, (size_t) N * sizeof(int32_t));
+        m->pos.resize(N);
+        for (int i = 0; i < N; i++) m->pos[i] = n_past + i;
+        ggml_backend_tensor_set(m->pos_in, m->pos.data(), 0, (size_t) N * sizeof(int32_t));
+        ggml_cgraph * gf = build_graph(*m, n_past, N);
+        const int64_t t1 = now_us();
+        auto * sched = (ggml_backend_sched_t) m->sched;
+        ggml_backend_sched_reset(sched);
+        if (ggml_backend_sched_graph_compute(sched, gf) != GGML_STATUS_SUCCESS) {
+            fprintf(stderr, "gpt2_eval: scheduler compute failed\n");
+            return 1;
+        }
+        ggml_tensor * out = gf->nodes[gf->n_nodes - 1];
+        const size_t nv = (size_t) m->hp.n_vocab;
+        if (all_logits) ggml_backend_tensor_get(out, logits, 0, sizeof(float) * nv * N);
+        else ggml_backend_tensor_get(out, logits, sizeof(float) * nv * (N - 1), sizeof(float) * nv);
+        m->last_nodes = gf->n_nodes;
+        m->us_build = t1 - t0;
+        m->us_alloc = m->us_inputs = 0;
+        m->us_compute = now_us() - t1;
+        return 0;
+    }
+#endif
     const int64_t t0 = now_us();
     ggml_cgraph * gf = build_graph(*m, n_past, N);
     const int64_t t1 = now_us();

@@ -80,9 +80,45 @@ __device__ float row_mean_cpu_order(const float * buf, int64_t n, double * shd) 
     return r;
 }
 
+// Wave-level variant for rows held in registers: lane l owns elements k = l + 64 j (j < J), so
+// element order k is (j, lane). Every lane ends with the same float (no LDS, no barrier). The
+// sequential fallback walks k in order with v_readlane.
+template <bool SQ, int J>
+__device__ float wave_mean_cpu_order(const float (&v)[J], int64_t n) {
+    const int lane = threadIdx.x & 63;
+    double s = 0.0, a = 0.0;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        if ((int64_t) j * 64 + lane < n) {
+            const double t = (double) sum_term<SQ>(v[j]);
+            s += t;
+            a += fabs(t);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        s += __shfl_xor(s, off, 64);
+        a += __shfl_xor(a, off, 64);
+    }
+    const double B = 4.0 * (double) n * a * 0x1p-53 + 0x1p-1074;
+    const float lo = (float) ((s - B) / (double) n);
+    const float hi = (float) ((s + B) / (double) n);
+    if (lo == hi) return lo == 0.0f ? 0.0f : lo;  // the CPU's chain starts at +0.0
+    double q = 0.0;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const float t = sum_term<SQ>(v[j]);
+        for (int l = 0; l < 64; l++) {
+            if ((int64_t) j * 64 + l < n) q += (double) __shfl(t, l, 64);
+        }
+    }
+    return (float) (q / (double) n);
+}
+
 } // namespace mi_cpu
 
 using mi_cpu::add_rn;
 using mi_cpu::mul_rn;
 using mi_cpu::row_mean_cpu_order;
 using mi_cpu::sub_rn;
+using mi_cpu::wave_mean_cpu_order;

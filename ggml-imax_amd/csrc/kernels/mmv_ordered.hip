@@ -186,7 +186,48 @@ __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ 
     }
 
     // stage the activations: 16-byte loads, unrolled so each lane has its loads in flight at once
-    if (pro.mode) {
+    constexpr int kJ = 12;  // register path: K <= 64 * kJ
+    if (pro.mode && K <= 64 * kJ) {
+        // the graph's norm|rms_norm -> mul(g) -> add(b), per column, held in registers: every wave
+        // computes it (no barriers, no LDS round trips), wave 0 writes the f16 result
+        const int lane = threadIdx.x & 63;
+        const bool writer = (threadIdx.x >> 6) == 0;
+        for (int c = 0; c < nc; c++) {
+            const float * xc = (const float *) (x.base + (i11 + c) * x.nb1);
+            float v[kJ], gv[kJ], bv[kJ];
+#pragma unroll
+            for (int j = 0; j < kJ; j++) {
+                const int64_t k = (int64_t) j * 64 + lane;
+                const bool in = k < K;
+                v[j] = in ? xc[k] : 0.0f;
+                gv[j] = in && pro.g ? pro.g[k] : 1.0f;
+                bv[j] = in && pro.b ? pro.b[k] : 0.0f;
+            }
+            float scale;
+            if (pro.mode == 2) {
+                const float mean = wave_mean_cpu_order<true, kJ>(v, K);
+                scale = 1.0f / sqrtf(add_rn(mean, pro.eps));
+            } else {
+                const float mean = wave_mean_cpu_order<false, kJ>(v, K);
+#pragma unroll
+                for (int j = 0; j < kJ; j++) v[j] = sub_rn(v[j], mean);
+                const float variance = wave_mean_cpu_order<true, kJ>(v, K);
+                scale = 1.0f / sqrtf(add_rn(variance, pro.eps));
+            }
+            if (writer) {
+#pragma unroll
+                for (int j = 0; j < kJ; j++) {
+                    const int64_t k = (int64_t) j * 64 + lane;
+                    if (k < K) {
+                        float y = mul_rn(v[j], scale);
+                        if (pro.g) y = mul_rn(y, gv[j]);
+                        if (pro.b) y = add_rn(y, bv[j]);
+                        xs[c * K + k] = mi_f2h(y);
+                    }
+                }
+            }
+        }
+    } else if (pro.mode) {
         // the graph's norm|rms_norm -> mul(g) -> add(b) producing this mul_mat's src1, computed per
         // column exactly as k_norm does (ops.hip), then rounded to f16 as the CPU's from_float
         float * xf = (float *) (xs + NC * K);

@@ -170,6 +170,8 @@ _SIGS = {
     # GPT-2 driver (include/gpt2-mi355x.h)
     "gpt2_model_load": ([c_char_p, c_void_p, c_int, c_int], c_void_p),
     "gpt2_model_free": ([c_void_p], None),
+    "gpt2_model_load_sched": ([c_char_p, c_void_p, c_int, c_int, c_int, c_int], c_void_p),
+    "gpt2_sched_n_splits": ([c_void_p], c_int),
     "gpt2_model_hparams": ([c_void_p, c_void_p], None),
     "gpt2_model_size": ([c_void_p], c_size_t),
     "gpt2_compute_buffer_size": ([c_void_p], c_size_t),

@@ -28,6 +28,13 @@ struct gpt2_hparams_c {
 // and a graph allocator reserved for the worst-case graph of n_batch tokens (:832-846).
 // n_ctx <= 0 keeps the file's context. Returns NULL (with a message on stderr) on failure.
 GGML_API struct gpt2_model * gpt2_model_load(const char * fname, ggml_backend_t backend, int n_ctx, int n_batch);
+// examples/gpt-2/main-sched.cpp: layers split over `backends` (the last one is the CPU fallback,
+// as ggml_backend_sched requires) by n_gpu_layers, executed through ggml_backend_sched. Needs a
+// ggml runtime that provides the scheduler (the reference libggml: oracle/_ref/libgpt2_ref.so);
+// other builds return NULL with a message.
+GGML_API struct gpt2_model * gpt2_model_load_sched(const char * fname, ggml_backend_t * backends, int n_backends, int n_gpu_layers,
+                                                   int n_ctx, int n_batch);
+GGML_API int gpt2_sched_n_splits(const struct gpt2_model * model);
 GGML_API void gpt2_model_free(struct gpt2_model * model);
 GGML_API void gpt2_model_hparams(const struct gpt2_model * model, struct gpt2_hparams_c * out);
 GGML_API size_t gpt2_model_size(const struct gpt2_model * model);   // bytes of weight data read

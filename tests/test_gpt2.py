@@ -185,3 +185,63 @@ def test_gpt2_long_context_decode(model_path):
         rm.free()
         lib.ggml_backend_free(be)
         ref.ggml_backend_free(rbe)
+
+
+# ---- ggml_backend_sched: the backend as a drop-in under the reference scheduler -------------------
+
+SCHED_CHILD = os.path.join(REPO, "tests", "_sched_child.py")
+
+
+def _teacher_forced_direct(m, toks):
+    outs, n_past = [], 0
+    for i in range(0, len(toks), 8):
+        outs.append(m.eval(n_past, toks[i:i + 8], all_logits=True))
+        n_past += len(toks[i:i + 8])
+    nxt = int(np.argmax(outs[-1][-1]))
+    for _ in range(8):
+        lg = m.eval(n_past, [nxt])
+        outs.append(lg)
+        n_past += 1
+        nxt = int(np.argmax(lg[-1]))
+    return np.concatenate(outs)
+
+
+def _run_sched_child(model_path, tmp_path, layers):
+    import sys
+    p = subprocess.run([sys.executable, SCHED_CHILD, model_path, str(tmp_path), ",".join(str(v) for v in layers)],
+                       capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return p.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+def test_sched_mode_on_reference_cpu_matches_direct(model_path, tmp_path):
+    """main-sched.cpp's path (ggml_backend_sched, CPU only) == main-backend.cpp's path, bit for bit."""
+    _run_sched_child(model_path, tmp_path, [0])
+    ref, be, m = _ref_model(model_path)
+    try:
+        direct = _teacher_forced_direct(m, m.tokenize(PROMPT))
+    finally:
+        m.free()
+        ref.ggml_backend_free(be)
+    sched = np.load(tmp_path / "ngl0.npy")
+    assert np.array_equal(sched.view(np.uint32), direct.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+def test_gpt2_partial_offload_under_reference_scheduler(model_path, tmp_path):
+    """examples/gpt-2/main-sched.cpp's layer split: the reference's own ggml_backend_sched places
+    n_gpu_layers of 12 on MI355X0 and the rest on the reference CPU backend, copying activations
+    across the split. Every split point gives logits bit-identical to the CPU-only run."""
+    out = _run_sched_child(model_path, tmp_path, [0, 3, 6, 12, 13])
+    print(out)
+    base = np.load(tmp_path / "ngl0.npy")
+    for ngl in (3, 6, 12, 13):
+        got = np.load(tmp_path / f"ngl{ngl}.npy")
+        diff = float(np.max(np.abs(got - base)))
+        print(f"n_gpu_layers={ngl}: max |d| = {diff:.3e}")
+        assert np.array_equal(got.view(np.uint32), base.view(np.uint32)), (ngl, diff)
+    import re
+    splits = {int(a): int(b) for a, b in re.findall(r"n_gpu_layers=(\d+): splits=(\d+)", out)}
+    assert splits[6] > 1 and splits[3] > 1  # the graph really crosses devices
