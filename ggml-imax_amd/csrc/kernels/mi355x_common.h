@@ -17,6 +17,15 @@ static_assert(sizeof(mi_block_q8_0) == 34, "q8_0");
 static_assert(sizeof(mi_block_q4_K) == 144, "q4_K");
 static_assert(sizeof(mi_block_q5_K) == 176, "q5_K");
 
+// Workgroup barrier for LDS hand-offs that leaves global loads in flight: __syncthreads() carries
+// a release/acquire fence, for which the compiler waits for every outstanding memory operation
+// (vmcnt(0)) -- which drains a register prefetch ring at every barrier. This waits for this
+// wave's LDS operations only, then s_barrier; the memory clobber keeps the compiler from moving
+// memory accesses across it.
+__device__ __forceinline__ void mi_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ float mi_h2f(uint16_t h) {
     _Float16 v;
     __builtin_memcpy(&v, &h, 2);

@@ -32,6 +32,7 @@ constexpr int BM = 64;          // weight rows per tile
 constexpr int BN = 128;         // activation columns per tile
 constexpr int BK = 64;          // K per LDS stage
 constexpr int LDS_STRIDE = BK + 8;  // padded f16 row stride (144 B)
+constexpr int kPF = 4;          // stages of global loads in flight (register ring)
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float float16v __attribute__((ext_vector_type(16)));
@@ -178,21 +179,24 @@ __global__ __launch_bounds__(256) void k_mmq2(const uint8_t * __restrict__ W, si
     const bool blive = bcol < ncols;
     const uint16_t * xcol = xh + (blive ? bcol : 0) * K;
 
-    Raw raw;
-    uint4 xb[4];
-    auto load_stage = [&](int64_t k0) {
-        raw.load(wrow, k0 + ak);
+    // register ring: the raw weights and activations of the next kPF stages are in flight while
+    // the current stage's MFMAs run (a memory round trip is ~1 us = several stages of MFMA work)
+    Raw raw[kPF];
+    uint4 xb[kPF][4];
+    auto load_stage = [&](int slot_unused, Raw & rw, uint4 (&xv)[4], int64_t k0) {
+        (void) slot_unused;
+        rw.load(wrow, k0 + ak);
 #pragma unroll
-        for (int i = 0; i < 4; i++) xb[i] = *(const uint4 *) (xcol + k0 + bk + 8 * i);
+        for (int i = 0; i < 4; i++) xv[i] = *(const uint4 *) (xcol + k0 + bk + 8 * i);
     };
-    auto store_stage = [&](int buf, int64_t k0) {
+    auto store_stage = [&](int buf, const Raw & rw, const uint4 (&xv)[4], int64_t k0) {
         _Float16 * pa = la[buf] + ar * LDS_STRIDE + ak;
         if constexpr (TYPE == 1) {
-            *(uint4 *) pa = alive ? raw.a : make_uint4(0, 0, 0, 0);
-            *(uint4 *) (pa + 8) = alive ? raw.b : make_uint4(0, 0, 0, 0);
+            *(uint4 *) pa = alive ? rw.a : make_uint4(0, 0, 0, 0);
+            *(uint4 *) (pa + 8) = alive ? rw.b : make_uint4(0, 0, 0, 0);
         } else {
             float v[16];
-            raw.dequant(k0 + ak, v);
+            rw.dequant(k0 + ak, v);
             uint4 u0, u1;
             u0.x = pack2h(v[0], v[1]);   u0.y = pack2h(v[2], v[3]);   u0.z = pack2h(v[4], v[5]);   u0.w = pack2h(v[6], v[7]);
             u1.x = pack2h(v[8], v[9]);   u1.y = pack2h(v[10], v[11]); u1.z = pack2h(v[12], v[13]); u1.w = pack2h(v[14], v[15]);
@@ -202,31 +206,41 @@ __global__ __launch_bounds__(256) void k_mmq2(const uint8_t * __restrict__ W, si
         }
         _Float16 * pb = lb[buf] + bc * LDS_STRIDE + bk;
 #pragma unroll
-        for (int i = 0; i < 4; i++) *(uint4 *) (pb + 8 * i) = blive ? xb[i] : make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < 4; i++) *(uint4 *) (pb + 8 * i) = blive ? xv[i] : make_uint4(0, 0, 0, 0);
     };
 
     float16v acc0 = {}, acc1 = {};
     const int r = lane & 31, h = lane >> 5;
     const int64_t nst = K / BK;
-    load_stage(0);
-    store_stage(0, 0);
-    __syncthreads();
-    for (int64_t st = 0; st < nst; st++) {
-        const int cur = (int) (st & 1);
-        if (st + 1 < nst) load_stage((st + 1) * BK);
-        const _Float16 * pa = la[cur] + (wm * 32 + r) * LDS_STRIDE + 8 * h;
-        const _Float16 * pb0 = lb[cur] + (wb * 64 + r) * LDS_STRIDE + 8 * h;
-        const _Float16 * pb1 = pb0 + 32 * LDS_STRIDE;
+    // K % 256 == 0 (mi_mmq_supported) -> nst is a multiple of kPF. Loads are unconditional
+    // (clamped to the last stage): a predicated load makes the compiler drain vmcnt to 0.
 #pragma unroll
-        for (int kk = 0; kk < BK; kk += 16) {
-            const half8 a = *(const half8 *) (pa + kk);
-            const half8 x0 = *(const half8 *) (pb0 + kk);
-            const half8 x1 = *(const half8 *) (pb1 + kk);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, x0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, x1, acc1, 0, 0, 0);
+    for (int u = 0; u < kPF; u++) load_stage(u, raw[u], xb[u], (int64_t) (u < nst ? u : nst - 1) * BK);
+    store_stage(0, raw[0], xb[0], 0);
+    mi_lds_barrier();
+    for (int64_t s0 = 0; s0 < nst; s0 += kPF) {
+#pragma unroll
+        for (int u = 0; u < kPF; u++) {
+            const int64_t st = s0 + u;
+            const int cur = (int) (st & 1);
+            // slot u held stage st, already in LDS: refill it with stage st + kPF
+            const int64_t nxt = st + kPF < nst ? st + kPF : nst - 1;
+            load_stage(u, raw[u], xb[u], nxt * BK);
+            const _Float16 * pa = la[cur] + (wm * 32 + r) * LDS_STRIDE + 8 * h;
+            const _Float16 * pb0 = lb[cur] + (wb * 64 + r) * LDS_STRIDE + 8 * h;
+            const _Float16 * pb1 = pb0 + 32 * LDS_STRIDE;
+#pragma unroll
+            for (int kk = 0; kk < BK; kk += 16) {
+                const half8 a = *(const half8 *) (pa + kk);
+                const half8 x0 = *(const half8 *) (pb0 + kk);
+                const half8 x1 = *(const half8 *) (pb1 + kk);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, x0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, x1, acc1, 0, 0, 0);
+            }
+            const int un = (u + 1) % kPF;
+            store_stage(cur ^ 1, raw[un], xb[un], (st + 1 < nst ? st + 1 : st) * BK);  // last: harmless rewrite
+            mi_lds_barrier();  // keeps the ring's global loads in flight
         }
-        if (st + 1 < nst) store_stage(cur ^ 1, (st + 1) * BK);
-        __syncthreads();
     }
 
     // D[n][b]: column b = lane & 31, rows n = (reg&3) + 8*(reg>>2) + 4*(lane>>5)

@@ -1,0 +1,24 @@
+"""Batched-prefill mul_mat timing (BASELINE config 5 shape) on MI355X: HIP-event time per
+mul_mat for B in sys.argv (default 512 64), all weight types of the path."""
+import os, sys
+import numpy as np
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "ggml-imax_amd"))
+import bench  # noqa: E402
+from ggml_mi355x import ggml as G  # noqa: E402
+import torch  # noqa: E402
+
+lib = G.runtime()
+be = G.mi355x_backend(lib, 0)
+sp = lib.ggml_backend_mi355x_get_stream(be)
+Bs = [int(b) for b in sys.argv[1:]] or [512, 64]
+for tname in ("q4_K", "q5_K", "q4_0", "q8_0", "f16"):
+    for B in Bs:
+        t = bench.TYPE_NAMES[tname]
+        wl = bench.MulMatWorkload(lib, be, t, 4096, 4096, B, 8)
+        for _ in range(3):
+            wl.step()
+        ms = np.median([bench.event_time_per_step(torch, wl, sp, iters=5) for _ in range(3)])
+        print(f"{tname:5s} B={B:4d}: {ms * 1e3 / 8:8.2f} us/mul_mat  {2 * 4096 * 4096 * B * 8 / (ms / 1e3) / 1e12:7.1f} TFLOP/s")
+        wl.free()
+lib.ggml_backend_free(be)
