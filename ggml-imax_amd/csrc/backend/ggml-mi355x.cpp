@@ -367,8 +367,9 @@ static int act_kind(ggml_type wtype) {
     }
 }
 
+// kinds: 0 q8_0, 1 q8_K, 2 f16, 3/4 q8_0/q8_K quants expanded to f16(d * q) (mmq.hip operand)
 static size_t act_bytes(int kind, int64_t K, int64_t ncols) {
-    if (kind == 2) return (size_t) K * ncols * 2;
+    if (kind >= 2) return (size_t) K * ncols * 2;
     return mi_act_q8_bytes(K, ncols, kind == 1);
 }
 
@@ -398,6 +399,8 @@ static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, in
     const mi_src_cols x = src_cols(src1);
     if (kind == 2) {
         mi_convert_f16(x, K, (uint16_t *) dev, ctx->stream);
+    } else if (kind >= 3) {
+        mi_quantize_expand_f16(x, K, ncols, kind == 4, (uint16_t *) dev, ctx->stream);
     } else {
         const mi_act_q8 act = mi_act_q8_carve(dev, K, ncols, kind == 1);
         if (kind == 1) mi_quantize_q8_K(x, K, act, ctx->stream);
@@ -459,20 +462,19 @@ static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
         MI_ASSERT(src0->type == GGML_TYPE_F32);
         mi_mul_mat_f32(m, src_cols(src1), ctx->stream);
     } else {
-        void * act = get_activations(ctx, src1, kind, m.K);
         const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
         static const bool no_mmq = getenv("GGML_MI355X_NO_MMQ") != nullptr;
         const bool batched = !no_mmq && src1->ne[1] > 8 && m.ne02 == 1 && m.ne03 == 1 && m.ne12 == 1 && m.ne13 == 1 &&
                              mi_mmq_supported(m.type, m.K, m.nb01, m.nb1) && ((uintptr_t) m.W % 16) == 0;
         if (batched) {
-            const mi_act_q8 aq = kind == 2 ? mi_act_q8{} : mi_act_q8_carve(act, m.K, ncols, kind == 1);
-            uint16_t * tmp = (uint16_t *) scratch_take(ctx, mi_mmq_scratch_bytes(m.type, m.K, ncols));
-            mi_mul_mat_mmq(m.type, m.W, m.nb01, m.K, m.N, aq, kind == 2 ? (const uint16_t *) act : nullptr, ncols, m.dst,
-                           m.nb1, tmp, ctx->stream);
+            // the GEMM's activation operand: f16 for F16 weights, else f16(d * q) of the q8 quants
+            // written by the quantizer itself (kinds 3/4)
+            const uint16_t * xh = (const uint16_t *) get_activations(ctx, src1, kind == 2 ? 2 : kind + 3, m.K);
+            mi_mul_mat_mmq(m.type, m.W, m.nb01, m.K, m.N, mi_act_q8{}, xh, ncols, m.dst, m.nb1, nullptr, ctx->stream);
         } else if (kind == 2) {
-            mi_mul_mat_f16(m, (const uint16_t *) act, ctx->stream);
+            mi_mul_mat_f16(m, (const uint16_t *) get_activations(ctx, src1, kind, m.K), ctx->stream);
         } else {
-            mi_mul_mat_q(m, mi_act_q8_carve(act, m.K, ncols, kind == 1), ctx->stream);
+            mi_mul_mat_q(m, mi_act_q8_carve(get_activations(ctx, src1, kind, m.K), m.K, ncols, kind == 1), ctx->stream);
         }
     }
     ctx->last_launches++;
@@ -636,8 +638,9 @@ static size_t graph_scratch_bytes(const ggml_cgraph * cgraph) {
         if (kind < 0) continue;
         const ggml_tensor * b = n->src[1];
         const int64_t ncols = b->ne[1] * b->ne[2] * b->ne[3];
+        // q8 blocks and/or their f16 expansion (batched) -- both counted, the choice is made at run time
         total += (act_bytes(kind, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
-        if (ncols > 8) total += (mi_mmq_scratch_bytes(n->src[0]->type, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+        if (ncols > 8 && kind != 2) total += (act_bytes(kind + 3, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
     }
     return total;
 }

@@ -44,6 +44,9 @@ mi_act_q8 mi_act_q8_carve(void * base, int64_t K, int64_t ncols, bool is_q8K);
 void mi_quantize_q8_0(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s);
 void mi_quantize_q8_K(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s);
 void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s);
+// quantize to q8_K / q8_0 exactly as above and store f16(d * q) as [ncols][K] (no q8 blocks):
+// the activation operand of mi_mul_mat_mmq for quantized weights
+void mi_quantize_expand_f16(const mi_src_cols & x, int64_t K, int64_t ncols, bool is_q8K, uint16_t * xh, hipStream_t s);
 
 // quantized weights x quantized activations (integer dot products), any number of columns
 void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s);
@@ -80,10 +83,12 @@ extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);
 void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s);
 // Batched (prefill) mul_mat on MFMA: 2-D weights [K, N] of type Q4_0/Q8_0/Q4_K/Q5_K/F16,
-// `ncols` activation columns already converted (act for quantized types, xh for F16),
+// `ncols` activation columns already converted: xh = f16 [ncols][K] (F16 weights: the f16
+// activations; quantized weights: f16(d * q) from mi_quantize_expand_f16), or, for quantized
+// weights with xh == nullptr, the q8 blocks in act expanded into `scratch` first.
 // dst columns of ycol bytes. Requires K % 256 == 0.
 bool mi_mmq_supported(int type, int64_t K, size_t nb01, size_t ycol);
-// scratch for the f16 expansion of quantized activations (0 for F16 weights)
+// scratch for the f16 expansion of quantized activations when xh == nullptr (0 for F16 weights)
 size_t mi_mmq_scratch_bytes(int type, int64_t K, int64_t ncols);
 void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_q8 & act, const uint16_t * xh,
                     int64_t ncols, float * dst, size_t ycol, uint16_t * scratch, hipStream_t s);

@@ -155,14 +155,18 @@ template <> struct raw_of<8> { using T = WRawQ0<true>; };
 template <> struct raw_of<1> { using T = WRawF16; };
 
 // ---- the GEMM ---------------------------------------------------------------------------------
-template <int TYPE>
-__global__ __launch_bounds__(256) void k_mmq2(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+template <int TYPE, int SK>
+__global__ __launch_bounds__(256 * SK) void k_mmq2(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                               const uint16_t * __restrict__ xh, int64_t ncols, float * __restrict__ dst,
                                               size_t ycol) {
-    __shared__ __attribute__((aligned(16))) _Float16 la[2][BM * LDS_STRIDE];
-    __shared__ __attribute__((aligned(16))) _Float16 lb[2][BN * LDS_STRIDE];
+    // SK K-split groups of 4 waves each, every group with its own double-buffered LDS slabs
+    __shared__ __attribute__((aligned(16))) _Float16 lds_a[SK][2][BM * LDS_STRIDE];
+    __shared__ __attribute__((aligned(16))) _Float16 lds_b[SK][2][BN * LDS_STRIDE];
     using Raw = typename raw_of<TYPE>::T;
-    const int tid = threadIdx.x;
+    const int grp = (int) threadIdx.x >> 8;
+    const int tid = (int) threadIdx.x & 255;
+    _Float16 (&la)[2][BM * LDS_STRIDE] = lds_a[grp];
+    _Float16 (&lb)[2][BN * LDS_STRIDE] = lds_b[grp];
     const int wave = tid >> 6, lane = tid & 63;
     const int64_t n0 = (int64_t) blockIdx.x * BM;
     const int64_t b0 = (int64_t) blockIdx.y * BN;
@@ -211,12 +215,13 @@ __global__ __launch_bounds__(256) void k_mmq2(const uint8_t * __restrict__ W, si
 
     float16v acc0 = {}, acc1 = {};
     const int r = lane & 31, h = lane >> 5;
-    const int64_t nst = K / BK;
+    const int64_t nst = K / BK / SK;  // stages of this group
+    const int64_t kg = (int64_t) grp * nst * BK;  // first K of this group
     // K % 256 == 0 (mi_mmq_supported) -> nst is a multiple of kPF. Loads are unconditional
     // (clamped to the last stage): a predicated load makes the compiler drain vmcnt to 0.
 #pragma unroll
-    for (int u = 0; u < kPF; u++) load_stage(u, raw[u], xb[u], (int64_t) (u < nst ? u : nst - 1) * BK);
-    store_stage(0, raw[0], xb[0], 0);
+    for (int u = 0; u < kPF; u++) load_stage(u, raw[u], xb[u], kg + (int64_t) (u < nst ? u : nst - 1) * BK);
+    store_stage(0, raw[0], xb[0], kg);
     mi_lds_barrier();
     for (int64_t s0 = 0; s0 < nst; s0 += kPF) {
 #pragma unroll
@@ -225,7 +230,7 @@ __global__ __launch_bounds__(256) void k_mmq2(const uint8_t * __restrict__ W, si
             const int cur = (int) (st & 1);
             // slot u held stage st, already in LDS: refill it with stage st + kPF
             const int64_t nxt = st + kPF < nst ? st + kPF : nst - 1;
-            load_stage(u, raw[u], xb[u], nxt * BK);
+            load_stage(u, raw[u], xb[u], kg + nxt * BK);
             const _Float16 * pa = la[cur] + (wm * 32 + r) * LDS_STRIDE + 8 * h;
             const _Float16 * pb0 = lb[cur] + (wb * 64 + r) * LDS_STRIDE + 8 * h;
             const _Float16 * pb1 = pb0 + 32 * LDS_STRIDE;
@@ -238,8 +243,29 @@ __global__ __launch_bounds__(256) void k_mmq2(const uint8_t * __restrict__ W, si
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, x1, acc1, 0, 0, 0);
             }
             const int un = (u + 1) % kPF;
-            store_stage(cur ^ 1, raw[un], xb[un], (st + 1 < nst ? st + 1 : st) * BK);  // last: harmless rewrite
+            store_stage(cur ^ 1, raw[un], xb[un], kg + (st + 1 < nst ? st + 1 : st) * BK);  // last: harmless rewrite
             mi_lds_barrier();  // keeps the ring's global loads in flight
+        }
+    }
+
+    if constexpr (SK == 2) {
+        // group 1 hands its partial sums to group 0 through its own activation slabs (36 KB, idle
+        // once every wave is past its last MFMA); the sum is group0 + group1 in that fixed order
+        float * red = (float *) &lds_b[1][0][0];
+        mi_lds_barrier();
+        if (grp == 1) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                red[(i * 2 + 0) * 256 + tid] = acc0[i];
+                red[(i * 2 + 1) * 256 + tid] = acc1[i];
+            }
+        }
+        __syncthreads();
+        if (grp == 1) return;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            acc0[i] += red[(i * 2 + 0) * 256 + tid];
+            acc1[i] += red[(i * 2 + 1) * 256 + tid];
         }
     }
 
@@ -278,7 +304,7 @@ size_t mi_mmq_scratch_bytes(int type, int64_t K, int64_t ncols) {
 
 void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_q8 & act, const uint16_t * xh,
                     int64_t ncols, float * dst, size_t ycol, uint16_t * scratch, hipStream_t s) {
-    if (type != 1) {
+    if (type != 1 && xh == nullptr) {
         // quantized activations -> f16(d * q) once for all column tiles
         const int64_t total8 = K * ncols / 8;
         const unsigned grid = (unsigned) std::min<int64_t>((total8 + 255) / 256, 8192);
@@ -288,12 +314,19 @@ void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N,
     }
     const dim3 grid((unsigned) ((N + BM - 1) / BM), (unsigned) ((ncols + BN - 1) / BN));
     const uint8_t * w = (const uint8_t *) W;
+    // split K over two 4-wave groups when each group keeps a whole number of ring turns: with
+    // one 64x128 tile per CU (grid <= 256) a single 4-wave group leaves one wave per SIMD
+    const bool sk2 = K % (2 * BK * kPF) == 0;
+#define MI_MMQ_LAUNCH(T)                                                                                             \
+    if (sk2) hipLaunchKernelGGL((k_mmq2<T, 2>), grid, dim3(512), 0, s, w, nb01, K, N, xh, ncols, dst, ycol);           \
+    else hipLaunchKernelGGL((k_mmq2<T, 1>), grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol);
     switch (type) {
-        case 12: hipLaunchKernelGGL(k_mmq2<12>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
-        case 13: hipLaunchKernelGGL(k_mmq2<13>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
-        case 2: hipLaunchKernelGGL(k_mmq2<2>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
-        case 8: hipLaunchKernelGGL(k_mmq2<8>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
-        case 1: hipLaunchKernelGGL(k_mmq2<1>, grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); break;
+        case 12: MI_MMQ_LAUNCH(12) break;
+        case 13: MI_MMQ_LAUNCH(13) break;
+        case 2: MI_MMQ_LAUNCH(2) break;
+        case 8: MI_MMQ_LAUNCH(8) break;
+        case 1: MI_MMQ_LAUNCH(1) break;
         default: break;
     }
+#undef MI_MMQ_LAUNCH
 }

@@ -42,8 +42,11 @@ mi_act_q8 mi_act_q8_carve(void * base, int64_t K, int64_t ncols, bool is_q8K) {
     return a;
 }
 
-// One 32-element block per half-wave, one element per lane.
-__global__ __launch_bounds__(256) void k_quantize_q8_0(mi_src_cols x, int64_t K, mi_act_q8 act, int64_t nblocks_total) {
+// One 32-element block per half-wave, one element per lane. XH: write f16(d * q) to xh[c*K + k]
+// (the batched-prompt GEMM's operand, mmq.hip) instead of the q8 blocks.
+template <bool XH>
+__global__ __launch_bounds__(256) void k_quantize_q8_0(mi_src_cols x, int64_t K, mi_act_q8 act, uint16_t * xh,
+                                                       int64_t nblocks_total) {
     const int64_t gid = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t blk = gid >> 5;
     const int l = threadIdx.x & 31;
@@ -58,12 +61,18 @@ __global__ __launch_bounds__(256) void k_quantize_q8_0(mi_src_cols x, int64_t K,
     const float d = amax / 127.f;
     const float id = amax != 0.0f ? 127.f / amax : 0.0f;
     const float q = __builtin_rintf(__fmul_rn(v, id));
+    if constexpr (XH) {
+        xh[c * K + b * 32 + l] = mi_f2h(mi_h2f(mi_f2h(d)) * (float) (int8_t) (int) q);
+        return;
+    }
     act.qs[c * K + b * 32 + l] = (int8_t) (int) q;
     if (l == 0) act.d[c * nb_per_col + b] = mi_h2f(mi_f2h(d));
 }
 
-// One 256-element superblock per wave, four consecutive elements per lane.
-__global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K, mi_act_q8 act, int64_t nblocks_total) {
+// One 256-element superblock per wave, four consecutive elements per lane (XH as for q8_0).
+template <bool XH>
+__global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K, mi_act_q8 act, uint16_t * xh,
+                                                       int64_t nblocks_total) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int64_t blk = (int64_t) blockIdx.x * 4 + wave;
@@ -88,6 +97,24 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K,
         const float ov = __shfl_xor(vmax, off, 64);
         const int oi = __shfl_xor(idx, off, 64);
         if (oa > amax || (oa == amax && oi < idx)) { amax = oa; vmax = ov; idx = oi; }
+    }
+    if constexpr (XH) {
+        uint2 o = make_uint2(0, 0);
+        if (amax != 0.0f) {
+            const float iscale = -127.f / vmax;
+            const float d = 1.0f / iscale;
+            uint32_t h[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int bits = __float_as_int(__builtin_fmaf(iscale, v[i], 12582912.f));
+                int q = (bits & 0x007fffff) - 0x00400000;
+                q = q < 127 ? q : 127;
+                h[i] = mi_f2h(d * (float) (int8_t) q);
+            }
+            o = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        }
+        *(uint2 *) (xh + c * K + b * 256 + lane * 4) = o;
+        return;
     }
     int8_t * qs = act.qs + c * K + b * 256;
     int16_t * s32 = act.s32 + c * (K / 32) + b * 8;
@@ -127,12 +154,24 @@ __global__ __launch_bounds__(256) void k_convert_f16(mi_src_cols x, int64_t K, u
 void mi_quantize_q8_0(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s) {
     const int64_t nblk = (K / 32) * act.ncols;
     const int64_t threads = nblk * 32;
-    hipLaunchKernelGGL(k_quantize_q8_0, dim3((unsigned) ((threads + 255) / 256)), dim3(256), 0, s, x, K, act, nblk);
+    hipLaunchKernelGGL(k_quantize_q8_0<false>, dim3((unsigned) ((threads + 255) / 256)), dim3(256), 0, s, x, K, act, nullptr,
+                       nblk);
 }
 
 void mi_quantize_q8_K(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s) {
     const int64_t nblk = (K / 256) * act.ncols;
-    hipLaunchKernelGGL(k_quantize_q8_K, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, act, nblk);
+    hipLaunchKernelGGL(k_quantize_q8_K<false>, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, act, nullptr, nblk);
+}
+
+void mi_quantize_expand_f16(const mi_src_cols & x, int64_t K, int64_t ncols, bool is_q8K, uint16_t * xh, hipStream_t s) {
+    if (is_q8K) {
+        const int64_t nblk = (K / 256) * ncols;
+        hipLaunchKernelGGL(k_quantize_q8_K<true>, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, mi_act_q8{}, xh, nblk);
+    } else {
+        const int64_t nblk = (K / 32) * ncols;
+        hipLaunchKernelGGL(k_quantize_q8_0<true>, dim3((unsigned) ((nblk * 32 + 255) / 256)), dim3(256), 0, s, x, K, mi_act_q8{},
+                           xh, nblk);
+    }
 }
 
 void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s) {

@@ -12,7 +12,7 @@ lib = G.runtime()
 be = G.mi355x_backend(lib, 0)
 sp = lib.ggml_backend_mi355x_get_stream(be)
 Bs = [int(b) for b in sys.argv[1:]] or [512, 64]
-for tname in ("q4_K", "q5_K", "q4_0", "q8_0", "f16"):
+for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
     for B in Bs:
         t = bench.TYPE_NAMES[tname]
         wl = bench.MulMatWorkload(lib, be, t, 4096, 4096, B, 8)
