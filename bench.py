@@ -273,9 +273,16 @@ def main():
         lib.ggml_backend_synchronize(backend)
         torch.cuda.synchronize()
 
+    # HIP events on the backend's own stream bracket exactly the timed steps
+    ext_stream = torch.cuda.ExternalStream(stream_ptr)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+
     def run_steps():
+        ev0.record(ext_stream)
         for _ in range(args.steps):
             wl.step()
+        ev1.record(ext_stream)
 
     dt = timed_region(run_steps, sync, dist, torch.device("cuda", local_rank) if dist else None)
 
@@ -283,11 +290,12 @@ def main():
     value = R * ub * args.steps * world / dt / 1e9
     launches = lib.ggml_backend_mi355x_last_launch_count(backend)
 
-    # dominant kernel: HIP events on the backend's own stream around whole steps. The backend
-    # serves the R independent mul_mats of a step with `launches` kernel launches (1 when the
-    # fused streaming GEMV groups them), so per launch: bytes = R*ub/launches, duration =
+    # dominant kernel: HIP events on the backend's own stream around the timed steps. The
+    # backend serves the R independent mul_mats of a step with `launches` kernel launches (1 when
+    # the fused streaming GEMV groups them), so per launch: bytes = R*ub/launches, duration =
     # step time / launches.
-    step_ms = event_time_per_step(torch, wl, stream_ptr)
+    ev1.synchronize()
+    step_ms = ev0.elapsed_time(ev1) / args.steps
     launches = max(launches, 1)
     bytes_per_launch = R * ub / launches
     achieved = bytes_per_launch / (step_ms / 1e3 / launches) / 1e9
@@ -314,7 +322,7 @@ def main():
                      "kernel_launches_per_step": launches, "event_ms_per_step": round(step_ms, 4),
                      "algorithmic_bytes_per_launch": int(bytes_per_launch),
                      "note": "achieved = algorithmic bytes per launch (R mul_mats x (N*K/256*144 + 4K + 4N) / launches) "
-                             "/ HIP-event duration per launch on the backend stream; activation quantization is inside "
+                             "/ HIP-event duration per launch on the backend stream over the timed steps; activation quantization is inside "
                              "the kernel; traffic = PMC HBM bytes per launch (tools/pmc_traffic.py, gfx950-corrected)"},
     }
 

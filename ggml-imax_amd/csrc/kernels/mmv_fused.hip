@@ -114,15 +114,17 @@ struct FmtKQ {
         uint4 ha, hb;  // Q5 only
     };
     __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item) {
-        const int s = item >> 2, j = item & 3;
-        const uint8_t * blk = row + (size_t) s * BS;
-        r.hdr = *(const uint4 *) blk;
-        const uint8_t * qp = blk + (Q5 ? 48 : 16) + 32 * j;
-        r.qa = *(const uint4 *) qp;
-        r.qb = *(const uint4 *) (qp + 16);
+        // row is wave-uniform and the lane offsets are 32-bit: scalar base + vector offset
+        // addressing, no per-lane 64-bit address arithmetic per row
+        const uint32_t s = (uint32_t) item >> 2, j = (uint32_t) item & 3;
+        const uint32_t blk = s * BS;
+        const uint32_t qp = blk + (Q5 ? 48 : 16) + 32 * j;
+        r.hdr = *(const uint4 *) (row + blk);
+        r.qa = *(const uint4 *) (row + qp);
+        r.qb = *(const uint4 *) (row + qp + 16);
         if constexpr (Q5) {
-            r.ha = *(const uint4 *) (blk + 16);
-            r.hb = *(const uint4 *) (blk + 32);
+            r.ha = *(const uint4 *) (row + blk + 16);
+            r.hb = *(const uint4 *) (row + blk + 32);
         }
     }
     template <int NC>
@@ -146,9 +148,22 @@ struct FmtKQ {
         }
         const float dw = mi_h2f((uint16_t) (r.hdr.x & 0xFFFF));
         const float dmw = mi_h2f((uint16_t) (r.hdr.x >> 16));
+        // 6-bit scales / mins of sub-blocks 2j and 2j+1 (get_scale_min_k4,
+        // src/ggml-quants.c:1357-1365) without divergent branches: j is lane-dependent
+        const uint32_t sh = 16u * (uint32_t) (j & 1);
+        const uint32_t x0 = r.hdr.y >> sh, x1 = r.hdr.z >> sh, x2 = r.hdr.w >> sh;
         int sc0, m0, sc1, m1;
-        mi_scale_min_k4(2 * j, r.hdr.y, r.hdr.z, r.hdr.w, sc0, m0);
-        mi_scale_min_k4(2 * j + 1, r.hdr.y, r.hdr.z, r.hdr.w, sc1, m1);
+        if (j < 2) {  // sub-blocks 0..3: plain 6-bit fields (a select, both sides are cheap)
+            sc0 = (int) (x0 & 63);
+            sc1 = (int) ((x0 >> 8) & 63);
+            m0 = (int) (x1 & 63);
+            m1 = (int) ((x1 >> 8) & 63);
+        } else {      // sub-blocks 4..7: low 4 bits from bytes 8..11, high 2 bits from bytes 0..7
+            sc0 = (int) ((x2 & 0xF) | (((x0 >> 6) & 3) << 4));
+            sc1 = (int) (((x2 >> 8) & 0xF) | (((x0 >> 14) & 3) << 4));
+            m0 = (int) (((x2 >> 4) & 0xF) | (((x1 >> 6) & 3) << 4));
+            m1 = (int) (((x2 >> 12) & 0xF) | (((x1 >> 14) & 3) << 4));
+        }
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             if (NC > 1 && c >= ncols) break;
@@ -163,9 +178,12 @@ struct FmtKQ {
                 hi = mi_dot4((int) qhi[i], ahi[i], hi);
             }
             const int ss = *(const int *) (a.s32 + c * (K / 32) + s * 8 + 2 * j);
-            const int sumi = sc0 * lo + sc1 * hi;
-            const int summ = m0 * (int) (int16_t) (ss & 0xFFFF) + m1 * (ss >> 16);
-            acc[c] += a.d[c * (K / 256) + s] * (dw * (float) sumi - dmw * (float) summ);
+            // sc*lo + sc*hi and m*bsum + m*bsum in f32 are exact (|.| < 2^24: 63*32*31*127 and
+            // 63*32*128 per term), i.e. (float) of the reference's int32 sums, without the
+            // quarter-rate 32-bit integer multiplies
+            const float sumi = fmaf((float) sc1, (float) hi, (float) sc0 * (float) lo);
+            const float summ = fmaf((float) m1, (float) (ss >> 16), (float) m0 * (float) (int) (int16_t) (ss & 0xFFFF));
+            acc[c] += a.d[c * (K / 256) + s] * (dw * sumi - dmw * summ);
         }
     }
 };
@@ -179,25 +197,28 @@ struct FmtQ0 {
     static constexpr int BS = Q8 ? 34 : 18;
     static constexpr int NQ = Q8 ? 8 : 4;  // quant dwords per block
     struct Regs {
-        uint32_t w[NQ + 1];
-        uint32_t d;
-        uint32_t shift;
+        uint32_t w[NQ + 1];  // the dwords covering d and the quants
+        uint32_t off;        // byte offset of the block in w[0]: 0 or 2
     };
     __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item) {
-        const uint8_t * blk = row + (size_t) item * BS;
-        const uintptr_t qa = (uintptr_t) (blk + 2);
-        const uint32_t * w = (const uint32_t *) (qa & ~(uintptr_t) 3);
-        r.shift = (uint32_t) (qa & 3);  // 0 or 2
+        // rows start 16-byte aligned (fused_mv_eligible), so the block's misalignment is a
+        // function of the item alone; dword loads only (a 16-bit load of d gets a zero-extend
+        // the compiler places right behind the load, which waits for it), on 32-bit lane offsets
+        // from the wave-uniform row pointer
+        const uint32_t blk = (uint32_t) item * BS;
+        r.off = blk & 2;
+        const uint32_t base = blk - r.off;
 #pragma unroll
-        for (int i = 0; i <= NQ; i++) r.w[i] = w[i];  // buffers carry 256 B of tail slack
-        r.d = *(const uint16_t *) blk;
+        for (int i = 0; i <= NQ; i++) r.w[i] = *(const uint32_t *) (row + base + 4 * i);  // 256 B tail slack
     }
     template <int NC>
     __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
+        // d = bytes off..off+1 of w[0]; the quants start at byte off + 2
         uint32_t t[NQ];
 #pragma unroll
-        for (int i = 0; i < NQ; i++) t[i] = __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], r.shift);
-        const float dw = mi_h2f((uint16_t) r.d);
+        for (int i = 0; i < NQ; i++) t[i] = r.off ? r.w[i + 1] : __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], 2);
+        const uint32_t dbits = (r.off ? r.w[0] >> 16 : r.w[0]) & 0xFFFF;
+        const float dw = mi_h2f((uint16_t) dbits);
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             if (NC > 1 && c >= ncols) break;
@@ -225,7 +246,7 @@ struct FmtQ0 {
 
 // IPL = items per lane held in the prefetch ring (further items of long rows are loaded
 // in-line); PD = rows in flight ahead of the row being computed.
-template <class F, int NC, int PD, int IPL>
+template <class F, int NC, int PD, int IPL, bool TAIL>
 __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int NB = PD + 1;  // ring slots
@@ -241,26 +262,33 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     const int ncols = g.ncols;
     const lds_act act = lds_carve<F::QKA>(lds, NC, K);
 
-    const int64_t row_begin = (int64_t) rb * g.rows_per_block;
-    const int64_t row_end = row_begin + g.rows_per_block < g.N ? row_begin + g.rows_per_block : g.N;
-    const int64_t nrows = row_end - row_begin > wave ? (row_end - row_begin - wave + 3) / 4 : 0;
-    auto wrow_of = [&](int64_t k) { return W + (row_begin + 4 * k + wave) * g.nb01; };
+    // 32-bit row bookkeeping (N < 2^31): scalar compares, no 64-bit VGPR temporaries in the loop
+    const int Nr = (int) g.N;
+    const int row_begin = rb * (int) g.rows_per_block;
+    const int row_end = row_begin + (int) g.rows_per_block < Nr ? row_begin + (int) g.rows_per_block : Nr;
+    const int nrows = row_end - row_begin > wave ? (row_end - row_begin - wave + 3) / 4 : 0;
+    auto wrow_of = [&](int k) {
+        const int r = row_begin + 4 * k + wave;
+        return W + (size_t) (r < Nr ? r : Nr - 1) * g.nb01;
+    };
 
+    // Every load of the ring is unconditional, with clamped row / item indices: a load under a
+    // branch makes the compiler merge the ring registers after it, and the merge copy waits for
+    // the load just issued (vmcnt(0)), which serialises the prefetch.
     typename F::Regs ring[NB][IPL];
-    auto prefetch = [&](typename F::Regs (&slot)[IPL], int64_t k) {
+    auto prefetch = [&](typename F::Regs (&slot)[IPL], int k) {
         const uint8_t * wr = wrow_of(k);
 #pragma unroll
         for (int i = 0; i < IPL; i++) {
             const int item = lane + 64 * i;
-            if (item < nitems) F::load(slot[i], wr, item);
+            F::load(slot[i], wr, item < nitems ? item : nitems - 1);
         }
     };
+    const int klast = nrows > 0 ? nrows - 1 : 0;
 
     // 1) the first PD rows' weights in flight
 #pragma unroll
-    for (int u = 0; u < PD; u++) {
-        if (u < nrows) prefetch(ring[u], u);
-    }
+    for (int u = 0; u < PD; u++) prefetch(ring[u], u < klast ? u : klast);
 
     // 2) quantize the member's activation columns into LDS (wave w: 256-slices w, w+4, ...)
     {
@@ -288,12 +316,13 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     __syncthreads();
 
     // 3) stream: ring slot u holds row k0+u; refill it with row k0+u+PD right before using it
-    for (int64_t k0 = 0; k0 < nrows; k0 += NB) {
+    //    (the last row again past the end: an L2 hit)
+    for (int k0 = 0; k0 < nrows; k0 += NB) {
 #pragma unroll
         for (int u = 0; u < NB; u++) {
-            const int64_t k = k0 + u;
+            const int k = k0 + u;
             if (k >= nrows) break;  // wave-uniform
-            if (k + PD < nrows) prefetch(ring[(u + PD) % NB], k + PD);
+            prefetch(ring[(u + PD) % NB], k + PD < klast ? k + PD : klast);
             float acc[NC];
 #pragma unroll
             for (int c = 0; c < NC; c++) acc[c] = 0.0f;
@@ -302,13 +331,17 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                 const int item = lane + 64 * i;
                 if (item < nitems) F::template dot<NC>(ring[u][i], item, act, K, ncols, acc);
             }
-            const uint8_t * wr = wrow_of(k);
-            for (int item = lane + 64 * IPL; item < nitems; item += 64) {
-                typename F::Regs rr;
-                F::load(rr, wr, item);
-                F::template dot<NC>(rr, item, act, K, ncols, acc);
+            if constexpr (TAIL) {
+                // items beyond the ring's IPL per lane, loaded in-line (long rows only: a loop
+                // with loads here makes the compiler drain vmcnt at the top of every row group)
+                const uint8_t * wr = wrow_of(k);
+                for (int item = lane + 64 * IPL; item < nitems; item += 64) {
+                    typename F::Regs rr;
+                    F::load(rr, wr, item);
+                    F::template dot<NC>(rr, item, act, K, ncols, acc);
+                }
             }
-            const int64_t row = row_begin + 4 * k + wave;
+            const int row = row_begin + 4 * k + wave;
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 const float v = mi_wave_sum_u(acc[c]);
@@ -336,10 +369,10 @@ int resident_blocks(const void * fn, size_t lds) {
     return n;
 }
 
-template <class F, int NC, int PD, int IPL>
+template <class F, int NC, int PD, int IPL, bool TAIL>
 void launch_one(mi_mmv_group g, hipStream_t s) {
     const size_t lds = lds_bytes<F::QKA>(NC, g.K);
-    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL>;
+    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL, TAIL>;
     const int target = g_mi_tuning.mmv_blocks > 0 ? g_mi_tuning.mmv_blocks : resident_blocks(fn, lds);
     int bpm = target / g.n;
     if (bpm < 1) bpm = 1;
@@ -347,7 +380,14 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
     rows = (rows + 3) / 4 * 4;
     g.rows_per_block = rows;
     g.blocks_per_member = (int) ((g.N + rows - 1) / rows);
-    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds, s, g);
+    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL, TAIL>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds, s,
+                       g);
+}
+
+template <class F, int NC, int PD, int IPL>
+void launch_tail(const mi_mmv_group & g, hipStream_t s) {
+    if (g.K / F::ITEM > 64 * IPL) launch_one<F, NC, PD, IPL, true>(g, s);
+    else launch_one<F, NC, PD, IPL, false>(g, s);
 }
 
 template <class F, int NC>
@@ -355,14 +395,14 @@ void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
     const int items = (int) (g.K / F::ITEM);
     if (items > 64) {
         // two items per lane in the ring (Q4_0 / Q8_0 at K=4096)
-        if (variant / 10 == 1) launch_one<F, NC, 1, 2>(g, s);
-        else launch_one<F, NC, 2, 2>(g, s);
+        if (variant / 10 == 1) launch_tail<F, NC, 1, 2>(g, s);
+        else launch_tail<F, NC, 2, 2>(g, s);
         return;
     }
     switch (variant / 10) {
-        case 1: launch_one<F, NC, 1, 1>(g, s); break;
-        case 3: launch_one<F, NC, 3, 1>(g, s); break;
-        default: launch_one<F, NC, 2, 1>(g, s); break;
+        case 1: launch_one<F, NC, 1, 1, false>(g, s); break;
+        case 3: launch_one<F, NC, 3, 1, false>(g, s); break;
+        default: launch_one<F, NC, 2, 1, false>(g, s); break;
     }
 }
 
