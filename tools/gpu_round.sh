@@ -1,0 +1,22 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, the bench line, a rocprofv3 kernel-trace summary of the same
+# bench, and the PMC traffic passes. Every GPU step has its own time limit and the steps are
+# chained so that the first failure ends the call.
+#   usage: gpurun --timeout 1100 -- bash tools/gpu_round.sh TAG [skip-tests]
+set -eo pipefail
+TAG=${1:-r01}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+if [ "$2" != "skip-tests" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+  tail -3 "$OUT/pytest_gpu.log"
+fi
+timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+cat "$OUT/bench.json"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+  python3 bench.py --steps 50 --warmup 10 --no-cpu --no-gpt2 > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
+head -8 "$OUT/kernel_stats.csv" | cut -c1-200
+timeout -k 10 300 python tools/pmc_traffic.py --tag "$TAG" > "$OUT/pmc.log" 2>&1
+tail -5 "$OUT/pmc.log"
