@@ -1441,6 +1441,14 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.mmv_variant = value;
         return true;
     }
+    if (strcmp(name, "f16_variant") == 0) {
+        g_mi_tuning.f16_variant = value;
+        return true;
+    }
+    if (strcmp(name, "f16_threads") == 0 && (value == 0 || value == 64 || value == 128 || value == 256)) {
+        g_mi_tuning.f16_threads = value;
+        return true;
+    }
     return false;
 }
 

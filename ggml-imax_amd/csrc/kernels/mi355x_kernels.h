@@ -78,6 +78,8 @@ bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols);
 struct mi_tuning {
     int mmv_blocks;   // target resident workgroups for the fused GEMV (all members)
     int mmv_variant;  // 10*prefetch_depth + {0: activations in VGPRs, 1: from LDS, 2: LDS + waves/EU cap}
+    int f16_variant;  // decode F16 GEMV: 0 = 16 lanes per row (k_mmv_f16_w16), 1 = quad per row (k_mmv_f16_x)
+    int f16_threads;  // k_mmv_f16_w16 workgroup size override (0 = automatic)
 };
 extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);

@@ -151,47 +151,21 @@ __global__ __launch_bounds__(256) void k_mm_f32_ord(const uint8_t * __restrict__
     }
 }
 
-// Decode-regime F16 GEMV with the activation conversion and the graph's epilogue fused in:
-//   - each workgroup converts its NC f32 activation columns to f16 in LDS (RNE, as the CPU's
-//     ggml_fp32_to_fp16_row, src/ggml.c:610-612), so no separate conversion launch;
-//   - weights stream through a two-deep register prefetch of kU 16-byte steps per lane, so a
-//     quad keeps up to 2*kU loads in flight instead of one per dependent FMA step (kU = 32 when
-//     the matrix has too few rows to fill the chip with waves, 8 otherwise);
-//   - epilogue (EPI): 1 = + bias[row], 2 = + bias[row] + resid, 3 = gelu(. + bias[row]) via the
-//     fp16 table -- the graph's following ADD / ADD / GELU nodes, each rounded as the CPU does.
-
-template <int NC, int EPI, int kU>
-__global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
-                                                   mi_src_cols x, const uint16_t * __restrict__ xh, int64_t ncols,
-                                                   float * __restrict__ dst, size_t ycol, mi_f16_epilogue e,
-                                                   mi_norm_prologue pro) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][K] f16 (+ [K] f32 for the norm prologue)
-    __shared__ double shd[9];
-    const int q = threadIdx.x & 3;
-    const int rpb = blockDim.x >> 2;
-    const int64_t row = (int64_t) blockIdx.x * rpb + (threadIdx.x >> 2);
-    const bool live = row < N;
-    const int64_t i11 = (int64_t) blockIdx.y * NC;
-    int nc = (int) (ncols - i11);
-    nc = nc > NC ? NC : nc;
-
-    // The weights do not depend on the activations: the first kU steps of the row are requested
-    // before the activations are staged (and normalised), so their HBM latency overlaps that work.
-    const uint16_t * wrow = (const uint16_t *) (W + (live ? row : 0) * nb01);
-    const int64_t nsteps = K >> 5;  // whole 32-element steps
-    uint4 cur[kU];
-    if (nsteps > 0) {
-#pragma unroll
-        for (int u = 0; u < kU; u++) cur[u] = *(const uint4 *) (wrow + (u < nsteps ? u : nsteps - 1) * 32 + 8 * q);
-    }
-
+// Stage NC f32 activation columns as f16 in LDS (RNE, as the CPU's ggml_fp32_to_fp16_row,
+// src/ggml.c:610-612), optionally through the graph's preceding norm -> mul(g) -> add(b) chain
+// (pro), or copy already-converted f16 columns (xh). Ends without a barrier.
+template <int NC>
+__device__ __forceinline__ void stage_f16_activations(uint16_t * xs, double * shd, int64_t K, int64_t i11, int nc,
+                                                      const mi_src_cols & x, const uint16_t * __restrict__ xh,
+                                                      const mi_norm_prologue & pro) {
     // stage the activations: 16-byte loads, unrolled so each lane has its loads in flight at once
     constexpr int kJ = 12;  // register path: K <= 64 * kJ
     if (pro.mode && K <= 64 * kJ) {
-        // the graph's norm|rms_norm -> mul(g) -> add(b), per column, held in registers: every wave
-        // computes it (no barriers, no LDS round trips), wave 0 writes the f16 result
+        // the graph's norm|rms_norm -> mul(g) -> add(b), per column, held in registers by wave 0
+        // (no LDS round trips); the other waves wait at the caller's barrier with their weight
+        // loads in flight
         const int lane = threadIdx.x & 63;
-        const bool writer = (threadIdx.x >> 6) == 0;
+        if ((threadIdx.x >> 6) != 0) return;
         for (int c = 0; c < nc; c++) {
             const float * xc = (const float *) (x.base + (i11 + c) * x.nb1);
             float v[kJ], gv[kJ], bv[kJ];
@@ -214,16 +188,14 @@ __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ 
                 const float variance = wave_mean_cpu_order<true, kJ>(v, K);
                 scale = 1.0f / sqrtf(add_rn(variance, pro.eps));
             }
-            if (writer) {
 #pragma unroll
-                for (int j = 0; j < kJ; j++) {
-                    const int64_t k = (int64_t) j * 64 + lane;
-                    if (k < K) {
-                        float y = mul_rn(v[j], scale);
-                        if (pro.g) y = mul_rn(y, gv[j]);
-                        if (pro.b) y = add_rn(y, bv[j]);
-                        xs[c * K + k] = mi_f2h(y);
-                    }
+            for (int j = 0; j < kJ; j++) {
+                const int64_t k = (int64_t) j * 64 + lane;
+                if (k < K) {
+                    float y = mul_rn(v[j], scale);
+                    if (pro.g) y = mul_rn(y, gv[j]);
+                    if (pro.b) y = add_rn(y, bv[j]);
+                    xs[c * K + k] = mi_f2h(y);
                 }
             }
         }
@@ -282,6 +254,43 @@ __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ 
             for (int64_t k = threadIdx.x; k < K; k += blockDim.x) xs[c * K + k] = mi_f2h(xc[k]);
         }
     }
+}
+
+// Decode-regime F16 GEMV with the activation conversion and the graph's epilogue fused in:
+//   - each workgroup converts its NC f32 activation columns to f16 in LDS (RNE, as the CPU's
+//     ggml_fp32_to_fp16_row, src/ggml.c:610-612), so no separate conversion launch;
+//   - weights stream through a two-deep register prefetch of kU 16-byte steps per lane, so a
+//     quad keeps up to 2*kU loads in flight instead of one per dependent FMA step (kU = 32 when
+//     the matrix has too few rows to fill the chip with waves, 8 otherwise);
+//   - epilogue (EPI): 1 = + bias[row], 2 = + bias[row] + resid, 3 = gelu(. + bias[row]) via the
+//     fp16 table -- the graph's following ADD / ADD / GELU nodes, each rounded as the CPU does.
+
+template <int NC, int EPI, int kU>
+__global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                   mi_src_cols x, const uint16_t * __restrict__ xh, int64_t ncols,
+                                                   float * __restrict__ dst, size_t ycol, mi_f16_epilogue e,
+                                                   mi_norm_prologue pro) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][K] f16 (+ [K] f32 for the norm prologue)
+    __shared__ double shd[9];
+    const int q = threadIdx.x & 3;
+    const int rpb = blockDim.x >> 2;
+    const int64_t row = (int64_t) blockIdx.x * rpb + (threadIdx.x >> 2);
+    const bool live = row < N;
+    const int64_t i11 = (int64_t) blockIdx.y * NC;
+    int nc = (int) (ncols - i11);
+    nc = nc > NC ? NC : nc;
+
+    // The weights do not depend on the activations: the first kU steps of the row are requested
+    // before the activations are staged (and normalised), so their HBM latency overlaps that work.
+    const uint16_t * wrow = (const uint16_t *) (W + (live ? row : 0) * nb01);
+    const int64_t nsteps = K >> 5;  // whole 32-element steps
+    uint4 cur[kU];
+    if (nsteps > 0) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) cur[u] = *(const uint4 *) (wrow + (u < nsteps ? u : nsteps - 1) * 32 + 8 * q);
+    }
+
+    stage_f16_activations<NC>(xs, shd, K, i11, nc, x, xh, pro);
     __syncthreads();
 
     float acc[NC][8];
@@ -336,6 +345,113 @@ __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ 
     }
 }
 
+// Same contract as k_mmv_f16_x, with the 32 partial sums of a dot spread over 16 lanes instead of
+// a quad: lane m of a row's 16-lane group owns the two sums of elements i = 2m, 2m+1 (mod 32),
+// i.e. AVX register r = m / 4, lanes 2(m % 4) and 2(m % 4) + 1, and loads one dword (two f16) per
+// 32-element step. A row's 6 KB (K = 3072) is then 96 dwords per lane, all requested at once
+// (kS steps per batch, two batches in flight), so a 768-row matrix keeps the whole matrix in
+// flight from 192 waves instead of 48 quads-per-wave waves draining it in dependent rounds. The
+// partial sums are combined in GGML_F32x8_REDUCE's order (src/ggml.c:1172-1190) across lanes:
+// xor 8 = (s0 += s2, s1 += s3), xor 4 = (s0 += s1), xor 2 = (lane k + lane k+4), then
+// (t0 + t1) + (t2 + t3).
+template <int NC, int EPI, int kS>
+__global__ __launch_bounds__(256) void k_mmv_f16_w16(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                     mi_src_cols x, const uint16_t * __restrict__ xh, int64_t ncols,
+                                                     float * __restrict__ dst, size_t ycol, mi_f16_epilogue e,
+                                                     mi_norm_prologue pro) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][K] f16 (+ [K] f32 for the norm prologue)
+    __shared__ double shd[9];
+    const int m = threadIdx.x & 15;
+    const int rpb = blockDim.x >> 4;
+    const int64_t row = (int64_t) blockIdx.x * rpb + (threadIdx.x >> 4);
+    const bool live = row < N;
+    const int64_t i11 = (int64_t) blockIdx.y * NC;
+    int nc = (int) (ncols - i11);
+    nc = nc > NC ? NC : nc;
+
+    const uint32_t * wrow = (const uint32_t *) (W + (live ? row : 0) * nb01);
+    const int nsteps = (int) (K >> 5);
+    uint32_t cur[kS];
+    if (nsteps > 0) {
+#pragma unroll
+        for (int u = 0; u < kS; u++) cur[u] = wrow[(u < nsteps ? u : nsteps - 1) * 16 + m];
+    }
+
+    stage_f16_activations<NC>(xs, shd, K, i11, nc, x, xh, pro);
+    __syncthreads();
+
+    float acc[NC][2];
+#pragma unroll
+    for (int c = 0; c < NC; c++) acc[c][0] = acc[c][1] = 0.0f;
+
+    const uint32_t * xs32 = (const uint32_t *) xs;
+    auto step_compute = [&](uint32_t wv, int st) {
+        const float w0 = mi_h2f((uint16_t) (wv & 0xffffu)), w1 = mi_h2f((uint16_t) (wv >> 16));
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (c < nc) {
+                const uint32_t xv = xs32[((size_t) c * K >> 1) + st * 16 + m];
+                acc[c][0] = __fmaf_rn(w0, mi_h2f((uint16_t) (xv & 0xffffu)), acc[c][0]);
+                acc[c][1] = __fmaf_rn(w1, mi_h2f((uint16_t) (xv >> 16)), acc[c][1]);
+            }
+        }
+    };
+    if (nsteps > 0) {
+        uint32_t nxt[kS];
+        for (int s0 = 0; s0 < nsteps; s0 += kS) {
+            const int s1 = s0 + kS;
+            if (s1 < nsteps) {
+#pragma unroll
+                for (int u = 0; u < kS; u++) nxt[u] = wrow[(s1 + u < nsteps ? s1 + u : nsteps - 1) * 16 + m];
+            }
+#pragma unroll
+            for (int u = 0; u < kS; u++) {
+                if (s0 + u < nsteps) step_compute(cur[u], s0 + u);
+            }
+#pragma unroll
+            for (int u = 0; u < kS; u++) cur[u] = nxt[u];
+        }
+    }
+    const int64_t np = (int64_t) nsteps * 32;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        float a0 = acc[c][0], a1 = acc[c][1];
+        a0 = add_rn(a0, __shfl_xor(a0, 8, 64));
+        a1 = add_rn(a1, __shfl_xor(a1, 8, 64));
+        a0 = add_rn(a0, __shfl_xor(a0, 4, 64));
+        a1 = add_rn(a1, __shfl_xor(a1, 4, 64));
+        a0 = add_rn(a0, __shfl_xor(a0, 2, 64));  // lane 0: t0, t1; lane 1: t2, t3
+        a1 = add_rn(a1, __shfl_xor(a1, 2, 64));
+        float u = add_rn(a0, a1);
+        u = add_rn(u, __shfl_xor(u, 1, 64));
+        if (m == 0 && live && c < nc) {
+            const uint16_t * wr16 = (const uint16_t *) wrow;
+            double sd = (double) u;
+            for (int64_t i = np; i < K; i++) sd += (double) mul_rn(mi_h2f(wr16[i]), mi_h2f(xs[c * K + i]));
+            float v = (float) sd;
+            if (EPI >= 1) v = add_rn(v, e.bias[row]);
+            if (EPI == 2) v = add_rn(v, *(const float *) (e.resid + (i11 + c) * e.resid_nb1 + row * sizeof(float)));
+            if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
+            *(float *) ((char *) dst + (i11 + c) * ycol + row * sizeof(float)) = v;
+        }
+    }
+}
+
+template <int NC, int kS>
+void launch_f16_w16(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
+                    float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int threads) {
+    const int rpb = threads / 16;
+    const dim3 grid((unsigned) ((N + rpb - 1) / rpb), (unsigned) ((ncols + NC - 1) / NC));
+    const size_t lds = (size_t) NC * K * sizeof(uint16_t) + (pro.mode ? (size_t) K * sizeof(float) : 0);
+    const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
+    switch (epi) {
+        case 0: hipLaunchKernelGGL((k_mmv_f16_w16<NC, 0, kS>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro); break;
+        case 1: hipLaunchKernelGGL((k_mmv_f16_w16<NC, 1, kS>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro); break;
+        case 2: hipLaunchKernelGGL((k_mmv_f16_w16<NC, 2, kS>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro); break;
+        default: hipLaunchKernelGGL((k_mmv_f16_w16<NC, 3, kS>), grid, dim3(threads), lds, s, (const uint8_t *) W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro); break;
+    }
+}
+
 template <int NC, int U>
 void launch_f16_x_u(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
                     float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int threads) {
@@ -357,6 +473,17 @@ void launch_f16_x(const void * W, size_t nb01, int64_t K, int64_t N, const mi_sr
     // 64-lane workgroups (16 rows) while that still leaves >= 2 workgroups per CU, else 256;
     // deep prefetch when there are few rows (a few thousand quads cannot hide HBM latency)
     const int threads = N >= 16 * 1024 ? 256 : 64;
+    const int variant = g_mi_tuning.f16_variant;
+    // 16 lanes per row while the matrix is small enough that a quad per row leaves too few waves
+    // to keep it in flight (measured on MI355X, GPT-2 shapes: K=3072 N=768 12.2 -> 8.2 us,
+    // K=768 N=2304 with the norm prologue 6.8 -> 6.3 us); the quad kernel above that (lm_head
+    // N=50257: 17 us vs 32 us -- four times fewer workgroups, each amortising its prologue).
+    if (variant == 0 && (K >> 5) > 0 && N * ((ncols + NC - 1) / NC) < 16384) {
+        const int t16 = g_mi_tuning.f16_threads ? g_mi_tuning.f16_threads : 256;
+        if (K <= 48 * 32 * 2) launch_f16_w16<NC, 48>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, t16);
+        else launch_f16_w16<NC, 16>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, t16);
+        return;
+    }
     if (N * ((ncols + NC - 1) / NC) <= 8192) launch_f16_x_u<NC, 32>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, threads);
     else launch_f16_x_u<NC, 8>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, threads);
 }
