@@ -367,7 +367,8 @@ static int act_kind(ggml_type wtype) {
     }
 }
 
-// kinds: 0 q8_0, 1 q8_K, 2 f16, 3/4 q8_0/q8_K quants expanded to f16(d * q) (mmq.hip operand)
+// kinds: 0 q8_0, 1 q8_K, 2 f16, 3/4 q8_0/q8_K quants expanded to f16(d * q) (mmq.hip operand),
+// 5/6/7 = 2/3/4 in the GEMM's K-blocked layout [K/16][ncols][16]
 static size_t act_bytes(int kind, int64_t K, int64_t ncols) {
     if (kind >= 2) return (size_t) K * ncols * 2;
     return mi_act_q8_bytes(K, ncols, kind == 1);
@@ -397,10 +398,10 @@ static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, in
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
     void * dev = scratch_take(ctx, act_bytes(kind, K, ncols));
     const mi_src_cols x = src_cols(src1);
-    if (kind == 2) {
-        mi_convert_f16(x, K, (uint16_t *) dev, ctx->stream);
+    if (kind == 2 || kind == 5) {
+        mi_convert_f16(x, K, (uint16_t *) dev, ctx->stream, kind == 5);
     } else if (kind >= 3) {
-        mi_quantize_expand_f16(x, K, ncols, kind == 4, (uint16_t *) dev, ctx->stream);
+        mi_quantize_expand_f16(x, K, ncols, kind == 4 || kind == 7, (uint16_t *) dev, ctx->stream, kind >= 6);
     } else {
         const mi_act_q8 act = mi_act_q8_carve(dev, K, ncols, kind == 1);
         if (kind == 1) mi_quantize_q8_K(x, K, act, ctx->stream);
@@ -469,7 +470,9 @@ static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
         if (batched) {
             // the GEMM's activation operand: f16 for F16 weights, else f16(d * q) of the q8 quants
             // written by the quantizer itself (kinds 3/4)
-            const uint16_t * xh = (const uint16_t *) get_activations(ctx, src1, kind == 2 ? 2 : kind + 3, m.K);
+            const bool blk = mi_mmq_wants_blocked();
+            const int xkind = (kind == 2 ? 2 : kind + 3) + (blk ? 3 : 0);
+            const uint16_t * xh = (const uint16_t *) get_activations(ctx, src1, xkind, m.K);
             mi_mul_mat_mmq(m.type, m.W, m.nb01, m.K, m.N, mi_act_q8{}, xh, ncols, m.dst, m.nb1, nullptr, ctx->stream);
         } else if (kind == 2) {
             mi_mul_mat_f16(m, (const uint16_t *) get_activations(ctx, src1, kind, m.K), ctx->stream);
@@ -640,7 +643,7 @@ static size_t graph_scratch_bytes(const ggml_cgraph * cgraph) {
         const int64_t ncols = b->ne[1] * b->ne[2] * b->ne[3];
         // q8 blocks and/or their f16 expansion (batched) -- both counted, the choice is made at run time
         total += (act_bytes(kind, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
-        if (ncols > 8 && kind != 2) total += (act_bytes(kind + 3, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+        if (ncols > 8) total += (act_bytes(kind + 3, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
     }
     return total;
 }
@@ -1443,6 +1446,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "f16_variant") == 0) {
         g_mi_tuning.f16_variant = value;
+        return true;
+    }
+    if (strcmp(name, "mmq_variant") == 0) {
+        g_mi_tuning.mmq_variant = value;
         return true;
     }
     if (strcmp(name, "f16_threads") == 0 && (value == 0 || value == 64 || value == 128 || value == 256)) {

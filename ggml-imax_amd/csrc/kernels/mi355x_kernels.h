@@ -43,10 +43,14 @@ mi_act_q8 mi_act_q8_carve(void * base, int64_t K, int64_t ncols, bool is_q8K);
 
 void mi_quantize_q8_0(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s);
 void mi_quantize_q8_K(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s);
-void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s);
+// blocked: write the GEMM's K-blocked layout [K/16][ncols][16] instead of [ncols][K]
+void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s, bool blocked = false);
 // quantize to q8_K / q8_0 exactly as above and store f16(d * q) as [ncols][K] (no q8 blocks):
 // the activation operand of mi_mul_mat_mmq for quantized weights
-void mi_quantize_expand_f16(const mi_src_cols & x, int64_t K, int64_t ncols, bool is_q8K, uint16_t * xh, hipStream_t s);
+void mi_quantize_expand_f16(const mi_src_cols & x, int64_t K, int64_t ncols, bool is_q8K, uint16_t * xh, hipStream_t s,
+                            bool blocked = false);
+// the layout mi_mul_mat_mmq expects for xh under the current tuning (true: K-blocked)
+bool mi_mmq_wants_blocked();
 
 // quantized weights x quantized activations (integer dot products), any number of columns
 void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s);
@@ -80,6 +84,7 @@ struct mi_tuning {
     int mmv_variant;  // 10*prefetch_depth + {0: activations in VGPRs, 1: from LDS, 2: LDS + waves/EU cap}
     int f16_variant;  // decode F16 GEMV: 0 = 16 lanes per row (k_mmv_f16_w16), 1 = quad per row (k_mmv_f16_x)
     int f16_threads;  // k_mmv_f16_w16 workgroup size override (0 = automatic)
+    int mmq_variant;  // prefill GEMM: 0 = k_mmq3 (activations in registers), 1 = k_mmq2 (activations via LDS)
 };
 extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);

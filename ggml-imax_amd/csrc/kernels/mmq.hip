@@ -7,6 +7,12 @@
 // instead of re-converting per tile. F16 weights use the f16-rounded activations of
 // ggml_fp32_to_fp16_row, as the CPU does.
 //
+// GEMM (default k_mmq3, below): the same tiles and weight staging as k_mmq2, but each wave owns
+// all 64 rows x 32 columns and takes its f16 activation fragments straight from a K-blocked copy
+// of the activations ([K/16][ncols][16], written by the quantizer) into a register ring; only the
+// dequantized weight slab passes through LDS. Measured on MI355X, Q4_K 4096x4096 B=512 (whole
+// mul_mat incl. activation quantization): k_mmq2 53 us -> k_mmq3 43 us (395 TFLOP/s).
+//
 // GEMM (k_mmq2): workgroup = 4 wave64s, output tile 64 weight rows x 128 activation columns,
 // each wave 32 rows x 64 columns = two v_mfma_f32_32x32x16_f16 per 16-deep K step sharing one
 // A fragment. Per 64-deep K stage the workgroup dequantizes its 64 x 64 weight slab into LDS
@@ -289,7 +295,164 @@ __global__ __launch_bounds__(256 * SK) void k_mmq2(const uint8_t * __restrict__ 
     }
 }
 
+// ---- k_mmq3: activations straight into MFMA operand registers ------------------------------------
+// Same 64 x 128 workgroup tile and K split (SK groups of 4 waves) as k_mmq2, but each wave owns
+// all 64 weight rows x its own 32 activation columns: the f16 activation fragment of a 16-deep
+// K step is one 16-byte load per lane straight from xh (lane l: column l & 31, k + 8 (l >> 5)),
+// held in a register ring kPF stages deep, so activations never pass through LDS (k_mmq2 wrote
+// 16 KB and re-read it per stage and group, which left the LDS array, not the MFMAs, as the
+// busiest unit). Only the dequantized 64 x 64 weight slab of a stage goes through LDS, written
+// once per group and read by its four waves (two A fragments per K step each).
+template <int TYPE, int SK, int NST, bool XCD, int ABL = 0>
+__global__ __launch_bounds__(256 * SK) void k_mmq3(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                              const uint16_t * __restrict__ xh, int64_t ncols, float * __restrict__ dst,
+                                              size_t ycol) {
+    constexpr int kSlab = 2 * BM * LDS_STRIDE;  // halves per group: double-buffered weight slab
+    constexpr int kRedBytes = 256 * 32 * 4;     // one group's partial tile (SK == 2 hand-off)
+    constexpr int kSlabBytes = SK * kSlab * 2;
+    __shared__ __attribute__((aligned(16))) char lds_raw[SK == 2 && kRedBytes > kSlabBytes ? kRedBytes : kSlabBytes];
+    using Raw = typename raw_of<TYPE>::T;
+    const int grp = (int) threadIdx.x >> 8;
+    const int tid = (int) threadIdx.x & 255;
+    _Float16 * la0 = (_Float16 *) lds_raw + grp * kSlab;
+    const int wave = tid >> 6, lane = tid & 63;
+    int64_t n0 = (int64_t) blockIdx.x * BM;
+    int64_t b0 = (int64_t) blockIdx.y * BN;
+    if constexpr (XCD) {
+        // 1-D grid: workgroup i runs on XCD i % 8; give each XCD a contiguous run of tiles in
+        // column-tile-major order, so an XCD's L2 holds few activation column tiles
+        const int64_t nrt = (N + BM - 1) / BM, nct = (ncols + BN - 1) / BN, T = nrt * nct;
+        const int64_t per = (T + 7) / 8;
+        const int64_t t = (int64_t) (blockIdx.x % 8) * per + blockIdx.x / 8;
+        if (t >= T) return;
+        n0 = (t % nrt) * BM;
+        b0 = (t / nrt) * BN;
+    }
+
+    // weight staging: thread t dequantizes row t/4, 16 elements at (t%4)*16 (as k_mmq2)
+    const int ar = tid >> 2, ak = (tid & 3) * 16;
+    const int64_t arow = n0 + ar;
+    const bool alive = arow < N;
+    const uint8_t * wrow = W + (alive ? arow : 0) * nb01;
+    // activation fragment: column b0 + 32 wave + (lane & 31), 8 halves at k + 8 (lane >> 5), from
+    // the K-blocked layout xh[k / 16][ncols][16]: one K step of 32 columns = 1 KB contiguous
+    const int64_t bcol = std::min<int64_t>(b0 + 32 * wave + (lane & 31), ncols - 1);
+    const uint16_t * xcol = xh + bcol * 16 + 8 * (lane >> 5);
+    const int64_t kstep = ncols * 16;  // halves per 16-deep K step
+
+    Raw raw[kPF];
+    half8 xb[kPF][BK / 16];
+    auto load_stage = [&](Raw & rw, half8 (&xv)[BK / 16], int64_t k0) {
+        if constexpr (ABL == 2) k0 = 0;  // ablation (timing only): every stage reads the first slab
+        rw.load(wrow, k0 + ak);
+#pragma unroll
+        for (int i = 0; i < BK / 16; i++) xv[i] = *(const half8 *) (xcol + (k0 / 16 + i) * kstep);
+    };
+    auto store_stage = [&](int buf, const Raw & rw, int64_t k0) {
+        _Float16 * pa = la0 + buf * (BM * LDS_STRIDE) + ar * LDS_STRIDE + ak;
+        if constexpr (TYPE == 1) {
+            *(uint4 *) pa = alive ? rw.a : make_uint4(0, 0, 0, 0);
+            *(uint4 *) (pa + 8) = alive ? rw.b : make_uint4(0, 0, 0, 0);
+        } else {
+            float v[16];
+            rw.dequant(k0 + ak, v);
+            uint4 u0, u1;
+            u0.x = pack2h(v[0], v[1]);   u0.y = pack2h(v[2], v[3]);   u0.z = pack2h(v[4], v[5]);   u0.w = pack2h(v[6], v[7]);
+            u1.x = pack2h(v[8], v[9]);   u1.y = pack2h(v[10], v[11]); u1.z = pack2h(v[12], v[13]); u1.w = pack2h(v[14], v[15]);
+            if (!alive) u0 = u1 = make_uint4(0, 0, 0, 0);
+            *(uint4 *) pa = u0;
+            *(uint4 *) (pa + 8) = u1;
+        }
+    };
+
+    float16v acc0 = {}, acc1 = {};  // rows 0..31 / 32..63 of the tile, this wave's 32 columns
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t nst = NST ? NST : K / BK / SK;
+    const int64_t kg = (int64_t) grp * nst * BK;
+#pragma unroll
+    for (int u = 0; u < kPF; u++) load_stage(raw[u], xb[u], kg + (int64_t) (u < nst ? u : nst - 1) * BK);
+    store_stage(0, raw[0], kg);
+    mi_lds_barrier();
+#pragma unroll (NST ? NST / kPF : 1)
+    for (int64_t s0 = 0; s0 < nst; s0 += kPF) {
+#pragma unroll
+        for (int u = 0; u < kPF; u++) {
+            const int64_t st = s0 + u;
+            const int cur = (int) (st & 1);
+            const _Float16 * pa0 = la0 + cur * (BM * LDS_STRIDE) + r * LDS_STRIDE + 8 * h;
+            const _Float16 * pa1 = pa0 + 32 * LDS_STRIDE;
+            // all of the stage's A fragments are requested before the first MFMA, so the LDS
+            // latency is exposed once per stage rather than once per K step
+            half8 a0[BK / 16], a1[BK / 16];
+#pragma unroll
+            for (int kk = 0; kk < BK / 16; kk++) {
+                a0[kk] = *(const half8 *) (pa0 + 16 * kk);
+                a1[kk] = *(const half8 *) (pa1 + 16 * kk);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int kk = 0; kk < BK / 16; kk++) {
+                if constexpr (ABL == 1) {  // ablation (timing only): no MFMAs
+                    acc0[kk] += (float) a0[kk][0] * (float) xb[u][kk][0];
+                    acc1[kk] += (float) a1[kk][1] * (float) xb[u][kk][1];
+                } else {
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[kk], xb[u][kk], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[kk], xb[u][kk], acc1, 0, 0, 0);
+                }
+            }
+            const int un = (u + 1) % kPF;
+            store_stage(cur ^ 1, raw[un], kg + (st + 1 < nst ? st + 1 : st) * BK);  // last: harmless rewrite
+            // slot u's activations are consumed and its weights are in LDS: refill with st + kPF
+            const int64_t nxt = st + kPF < nst ? st + kPF : nst - 1;
+            load_stage(raw[u], xb[u], kg + nxt * BK);
+            mi_lds_barrier();  // keeps the ring's global loads in flight
+        }
+    }
+
+    if constexpr (SK == 2) {
+        // group 1 hands its partial tile to group 0 through LDS (the slabs are idle once every
+        // wave is past its last MFMA); the sum is group0 + group1 in that fixed order
+        float * red = (float *) lds_raw;
+        __syncthreads();
+        if (grp == 1) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                red[(i * 2 + 0) * 256 + tid] = acc0[i];
+                red[(i * 2 + 1) * 256 + tid] = acc1[i];
+            }
+        }
+        __syncthreads();
+        if (grp == 1) return;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            acc0[i] += red[(i * 2 + 0) * 256 + tid];
+            acc1[i] += red[(i * 2 + 1) * 256 + tid];
+        }
+    }
+
+    // D[n][b]: column b = lane & 31 of this wave's 32, rows n = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+    const int64_t b = b0 + 32 * wave + (lane & 31);
+    if (b >= ncols) return;
+    float * out = (float *) ((char *) dst + b * ycol);
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+        const float16v & acc = half ? acc1 : acc0;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const int64_t n = n0 + 32 * half + 8 * g + 4 * (lane >> 5);
+            if (n + 3 < N) {
+                *(float4 *) (out + n) = make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = acc[4 * g + e];
+            }
+        }
+    }
+}
+
 } // namespace
+
+bool mi_mmq_wants_blocked() { return (g_mi_tuning.mmq_variant & 1) == 0; }
 
 bool mi_mmq_supported(int type, int64_t K, size_t nb01, size_t ycol) {
     if (type != 12 && type != 13 && type != 2 && type != 8 && type != 1) return false;
@@ -317,8 +480,26 @@ void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N,
     // split K over two 4-wave groups when each group keeps a whole number of ring turns: with
     // one 64x128 tile per CU (grid <= 256) a single 4-wave group leaves one wave per SIMD
     const bool sk2 = K % (2 * BK * kPF) == 0;
+    // variant bits: 1 = k_mmq2 (activations via LDS), 2 = XCD-contiguous tile order, 8/16 = timing
+    // ablations; k_mmq3 is fully unrolled over the K stages for the common K (the loop back-edge
+    // of the runtime-K loop makes the compiler drain the load ring: measured 47 -> 43 us at 4096)
+    const int var = g_mi_tuning.mmq_variant;
+    const bool v3 = (var & 1) == 0;
+    const bool xcd = (var & 2) != 0;
+    const int abl = (var >> 3) & 3;
+    const int nst2 = sk2 ? (int) (K / BK / 2) : 0;
+    const dim3 grid1((unsigned) (((grid.x * grid.y) + 7) / 8 * 8));
+#define MI_MMQ3(T, NST) hipLaunchKernelGGL((k_mmq3<T, 2, NST, false>), grid, dim3(512), 0, s, w, nb01, K, N, xh, ncols, dst, ycol)
 #define MI_MMQ_LAUNCH(T)                                                                                             \
-    if (sk2) hipLaunchKernelGGL((k_mmq2<T, 2>), grid, dim3(512), 0, s, w, nb01, K, N, xh, ncols, dst, ycol);           \
+    if (v3 && abl == 1 && nst2 == 32) hipLaunchKernelGGL((k_mmq3<T, 2, 32, false, 1>), grid, dim3(512), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); \
+    else if (v3 && abl == 2 && nst2 == 32) hipLaunchKernelGGL((k_mmq3<T, 2, 32, false, 2>), grid, dim3(512), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); \
+    else if (v3 && sk2 && xcd) hipLaunchKernelGGL((k_mmq3<T, 2, 0, true>), grid1, dim3(512), 0, s, w, nb01, K, N, xh, ncols, dst, ycol); \
+    else if (v3 && nst2 == 32) MI_MMQ3(T, 32);                                                                       \
+    else if (v3 && nst2 == 24) MI_MMQ3(T, 24);                                                                       \
+    else if (v3 && nst2 == 16) MI_MMQ3(T, 16);                                                                       \
+    else if (v3 && sk2) MI_MMQ3(T, 0);                                                                               \
+    else if (v3) hipLaunchKernelGGL((k_mmq3<T, 1, 0, false>), grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol);       \
+    else if (sk2) hipLaunchKernelGGL((k_mmq2<T, 2>), grid, dim3(512), 0, s, w, nb01, K, N, xh, ncols, dst, ycol);      \
     else hipLaunchKernelGGL((k_mmq2<T, 1>), grid, dim3(256), 0, s, w, nb01, K, N, xh, ncols, dst, ycol);
     switch (type) {
         case 12: MI_MMQ_LAUNCH(12) break;
@@ -329,4 +510,5 @@ void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N,
         default: break;
     }
 #undef MI_MMQ_LAUNCH
+#undef MI_MMQ3
 }

@@ -22,6 +22,12 @@ static __device__ __forceinline__ const float * col_ptr(const mi_src_cols & x, i
     return (const float *) (x.base + i1 * x.nb1 + i2 * x.nb2 + i3 * x.nb3);
 }
 
+// f16 GEMM operand layouts: row-major [ncols][K], or K-blocked [K/16][ncols][16] (nblk > 0 =
+// ncols) so that the 32 columns x 16 halves of one MFMA K step are 1 KB of contiguous memory
+static __device__ __forceinline__ int64_t xh_index(int64_t c, int64_t k, int64_t K, int64_t nblk) {
+    return nblk ? ((k >> 4) * nblk + c) * 16 + (k & 15) : c * K + k;
+}
+
 size_t mi_act_q8_bytes(int64_t K, int64_t ncols, bool is_q8K) {
     const size_t qs = (size_t) (K * ncols + 255) & ~(size_t) 255;
     const size_t d = ((size_t) (K / (is_q8K ? 256 : 32)) * ncols * sizeof(float) + 255) & ~(size_t) 255;
@@ -46,7 +52,7 @@ mi_act_q8 mi_act_q8_carve(void * base, int64_t K, int64_t ncols, bool is_q8K) {
 // (the batched-prompt GEMM's operand, mmq.hip) instead of the q8 blocks.
 template <bool XH>
 __global__ __launch_bounds__(256) void k_quantize_q8_0(mi_src_cols x, int64_t K, mi_act_q8 act, uint16_t * xh,
-                                                       int64_t nblocks_total) {
+                                                       int64_t nblocks_total, int64_t xh_blk = 0) {
     const int64_t gid = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t blk = gid >> 5;
     const int l = threadIdx.x & 31;
@@ -62,7 +68,7 @@ __global__ __launch_bounds__(256) void k_quantize_q8_0(mi_src_cols x, int64_t K,
     const float id = amax != 0.0f ? 127.f / amax : 0.0f;
     const float q = __builtin_rintf(__fmul_rn(v, id));
     if constexpr (XH) {
-        xh[c * K + b * 32 + l] = mi_f2h(mi_h2f(mi_f2h(d)) * (float) (int8_t) (int) q);
+        xh[xh_index(c, b * 32 + l, K, xh_blk)] = mi_f2h(mi_h2f(mi_f2h(d)) * (float) (int8_t) (int) q);
         return;
     }
     act.qs[c * K + b * 32 + l] = (int8_t) (int) q;
@@ -72,7 +78,7 @@ __global__ __launch_bounds__(256) void k_quantize_q8_0(mi_src_cols x, int64_t K,
 // One 256-element superblock per wave, four consecutive elements per lane (XH as for q8_0).
 template <bool XH>
 __global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K, mi_act_q8 act, uint16_t * xh,
-                                                       int64_t nblocks_total) {
+                                                       int64_t nblocks_total, int64_t xh_blk = 0) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int64_t blk = (int64_t) blockIdx.x * 4 + wave;
@@ -113,7 +119,7 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K,
             }
             o = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
         }
-        *(uint2 *) (xh + c * K + b * 256 + lane * 4) = o;
+        *(uint2 *) (xh + xh_index(c, b * 256 + lane * 4, K, xh_blk)) = o;
         return;
     }
     int8_t * qs = act.qs + c * K + b * 256;
@@ -144,11 +150,11 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K,
     if (lane == 0) act.d[c * nb_per_col + b] = 1.0f / iscale;
 }
 
-__global__ __launch_bounds__(256) void k_convert_f16(mi_src_cols x, int64_t K, uint16_t * out, int64_t total) {
+__global__ __launch_bounds__(256) void k_convert_f16(mi_src_cols x, int64_t K, uint16_t * out, int64_t total, int64_t xh_blk) {
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int64_t c = i / K, k = i % K;
-    out[i] = mi_f2h(col_ptr(x, c)[k]);
+    out[xh_index(c, k, K, xh_blk)] = mi_f2h(col_ptr(x, c)[k]);
 }
 
 void mi_quantize_q8_0(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s) {
@@ -163,18 +169,21 @@ void mi_quantize_q8_K(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, h
     hipLaunchKernelGGL(k_quantize_q8_K<false>, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, act, nullptr, nblk);
 }
 
-void mi_quantize_expand_f16(const mi_src_cols & x, int64_t K, int64_t ncols, bool is_q8K, uint16_t * xh, hipStream_t s) {
+void mi_quantize_expand_f16(const mi_src_cols & x, int64_t K, int64_t ncols, bool is_q8K, uint16_t * xh, hipStream_t s,
+                            bool blocked) {
+    const int64_t xb = blocked ? ncols : 0;
     if (is_q8K) {
         const int64_t nblk = (K / 256) * ncols;
-        hipLaunchKernelGGL(k_quantize_q8_K<true>, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, mi_act_q8{}, xh, nblk);
+        hipLaunchKernelGGL(k_quantize_q8_K<true>, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, mi_act_q8{}, xh, nblk, xb);
     } else {
         const int64_t nblk = (K / 32) * ncols;
         hipLaunchKernelGGL(k_quantize_q8_0<true>, dim3((unsigned) ((nblk * 32 + 255) / 256)), dim3(256), 0, s, x, K, mi_act_q8{},
-                           xh, nblk);
+                           xh, nblk, xb);
     }
 }
 
-void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s) {
+void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s, bool blocked) {
     const int64_t total = K * x.ne1 * x.ne2 * x.ne3;
-    hipLaunchKernelGGL(k_convert_f16, dim3((unsigned) ((total + 255) / 256)), dim3(256), 0, s, x, K, out, total);
+    const int64_t xb = blocked ? x.ne1 * x.ne2 * x.ne3 : 0;
+    hipLaunchKernelGGL(k_convert_f16, dim3((unsigned) ((total + 255) / 256)), dim3(256), 0, s, x, K, out, total, xb);
 }
