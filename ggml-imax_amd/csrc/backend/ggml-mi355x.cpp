@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -227,6 +228,177 @@ static bool mi_host_buft_supports(ggml_backend_buffer_type_t, ggml_backend_t bac
 static bool mi_host_buft_is_host(ggml_backend_buffer_type_t) { return true; }
 
 // ---------------------------------------------------------------------------------------------
+// tensor-split row buffer type (ggml-cuda.cu:578-975 analogue)
+// ---------------------------------------------------------------------------------------------
+// The rows of each weight matrix are divided over "slots" by the cumulative fractions given to
+// ggml_backend_mi355x_split_buffer_type(); slot s lives on device s. With the test setting
+// GGML_MI355X_SPLIT_SLOTS=n on a machine with fewer devices, slot s lives on device s % count,
+// still with its own allocation, stream and copies, so the whole multi-device path (activation
+// copy in, per-slot GEMM, gather of the row slices) runs on one GPU. GGML_OP_MUL_MAT with such a
+// weight is op_mul_mat_split below.
+
+static int split_slots() {
+    static int n = [] {
+        const char * e = getenv("GGML_MI355X_SPLIT_SLOTS");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? std::min(v, GGML_MI355X_MAX_DEVICES) : std::max(device_count(), 1);
+    }();
+    return n;
+}
+
+static int slot_device(int slot) { return slot % std::max(device_count(), 1); }
+
+struct mi_split_slice {
+    int slot;
+    int device;
+    int64_t row_low, row_high;
+    char * ptr;
+};
+struct mi_split_extra {
+    std::vector<mi_split_slice> slices;
+};
+struct mi_split_buft_ctx {
+    std::vector<float> split;  // cumulative start fraction of each slot
+};
+struct mi_split_buffer_ctx {
+    std::vector<mi_split_extra *> extras;
+};
+
+// slices start on multiples of the GEMM's 64-row tile (any row count is valid for every kernel)
+static constexpr int64_t kSplitRowRounding = 64;
+
+static void split_rows(const ggml_tensor * t, const mi_split_buft_ctx * c, int slot, int64_t & lo, int64_t & hi) {
+    const int64_t nrows = ggml_nrows(t);
+    const int n = (int) c->split.size();
+    lo = slot == 0 ? 0 : (int64_t) ((double) nrows * c->split[slot]);
+    lo -= lo % kSplitRowRounding;
+    if (slot == n - 1) {
+        hi = nrows;
+    } else {
+        hi = (int64_t) ((double) nrows * c->split[slot + 1]);
+        hi -= hi % kSplitRowRounding;
+    }
+    hi = std::max(hi, lo);
+}
+
+static const char * mi_split_buffer_name(ggml_backend_buffer_t) { return "MI355X_Split"; }
+
+static bool buffer_is_split(ggml_backend_buffer_t buffer) {
+    return buffer && buffer->iface.get_name == mi_split_buffer_name;
+}
+
+static bool is_split_tensor(const ggml_tensor * t) {
+    const ggml_tensor * base = t->view_src ? t->view_src : t;
+    return buffer_is_split(base->buffer);
+}
+
+static void mi_split_buffer_free(ggml_backend_buffer_t buffer) {
+    auto * ctx = (mi_split_buffer_ctx *) buffer->context;
+    for (mi_split_extra * e : ctx->extras) {
+        for (const auto & sl : e->slices) {
+            mi_device_guard g(sl.device);
+            MI_CHECK(hipFree(sl.ptr));
+        }
+        delete e;
+    }
+    delete ctx;
+}
+
+static void * mi_split_buffer_base(ggml_backend_buffer_t) {
+    return (void *) 0x1000;  // the slices' pointers live in tensor->extra; never dereferenced
+}
+
+static void mi_split_buffer_init_tensor(ggml_backend_buffer_t buffer, ggml_tensor * tensor) {
+    MI_ASSERT(tensor->view_src == nullptr && "views of split tensors are not supported");
+    auto * ctx = (mi_split_buffer_ctx *) buffer->context;
+    auto * bctx = (mi_split_buft_ctx *) buffer->buft->context;
+    auto * extra = new mi_split_extra();
+    ctx->extras.push_back(extra);
+    const size_t nb1 = ggml_row_size(tensor->type, tensor->ne[0]);
+    for (int s = 0; s < (int) bctx->split.size(); s++) {
+        int64_t lo, hi;
+        split_rows(tensor, bctx, s, lo, hi);
+        if (hi == lo) continue;
+        mi_split_slice sl{s, slot_device(s), lo, hi, nullptr};
+        mi_device_guard g(sl.device);
+        const size_t bytes = (size_t) (hi - lo) * nb1;
+        MI_CHECK(hipMalloc((void **) &sl.ptr, bytes + kBufferSlack));  // init_tensor cannot fail (ggml-cuda.cu:755)
+        MI_CHECK(hipMemset(sl.ptr + bytes, 0, kBufferSlack));
+        extra->slices.push_back(sl);
+    }
+    tensor->extra = extra;
+}
+
+static void mi_split_buffer_set_tensor(ggml_backend_buffer_t, ggml_tensor * tensor, const void * data, size_t offset, size_t size) {
+    // split tensors are set whole (ggml-cuda.cu:781-782)
+    MI_ASSERT(offset == 0 && size == ggml_nbytes(tensor));
+    const auto * extra = (const mi_split_extra *) tensor->extra;
+    for (const auto & sl : extra->slices) {
+        mi_device_guard g(sl.device);
+        MI_CHECK(hipMemcpy(sl.ptr, (const char *) data + sl.row_low * tensor->nb[1], (size_t) (sl.row_high - sl.row_low) * tensor->nb[1],
+                           hipMemcpyHostToDevice));
+    }
+}
+
+static void mi_split_buffer_get_tensor(ggml_backend_buffer_t, const ggml_tensor * tensor, void * data, size_t offset, size_t size) {
+    MI_ASSERT(offset == 0 && size == ggml_nbytes(tensor));
+    const auto * extra = (const mi_split_extra *) tensor->extra;
+    for (const auto & sl : extra->slices) {
+        mi_device_guard g(sl.device);
+        MI_CHECK(hipMemcpy((char *) data + sl.row_low * tensor->nb[1], sl.ptr, (size_t) (sl.row_high - sl.row_low) * tensor->nb[1],
+                           hipMemcpyDeviceToHost));
+    }
+}
+
+static void mi_split_buffer_clear(ggml_backend_buffer_t, uint8_t) {}  // as ggml-cuda.cu:856-859
+
+static const ggml_backend_buffer_i k_mi_split_buffer_i = {
+    /* get_name    */ mi_split_buffer_name,
+    /* free_buffer */ mi_split_buffer_free,
+    /* get_base    */ mi_split_buffer_base,
+    /* init_tensor */ mi_split_buffer_init_tensor,
+    /* set_tensor  */ mi_split_buffer_set_tensor,
+    /* get_tensor  */ mi_split_buffer_get_tensor,
+    /* cpy_tensor  */ nullptr,
+    /* clear       */ mi_split_buffer_clear,
+    /* reset       */ nullptr,
+};
+
+static const char * mi_split_buft_name(ggml_backend_buffer_type_t) { return "MI355X_Split"; }
+
+static ggml_backend_buffer_t mi_split_buft_alloc(ggml_backend_buffer_type_t buft, size_t size) {
+    // the slices are allocated per tensor in init_tensor, once the rounded split is known; size is
+    // the bound ggml-alloc enforces with get_alloc_size (ggml-cuda.cu:887-895)
+    return ggml_backend_buffer_init(buft, k_mi_split_buffer_i, new mi_split_buffer_ctx(), size);
+}
+
+static size_t mi_split_buft_align(ggml_backend_buffer_type_t) { return kBufferAlign; }
+
+static size_t mi_split_buft_alloc_size(ggml_backend_buffer_type_t buft, const ggml_tensor * tensor) {
+    auto * c = (mi_split_buft_ctx *) buft->context;
+    const size_t nb1 = ggml_row_size(tensor->type, tensor->ne[0]);
+    size_t total = 0;
+    for (int s = 0; s < (int) c->split.size(); s++) {
+        int64_t lo, hi;
+        split_rows(tensor, c, s, lo, hi);
+        if (hi > lo) total += (size_t) (hi - lo) * nb1 + kBufferSlack;
+    }
+    return std::max(total, ggml_nbytes(tensor));
+}
+
+static bool mi_split_buft_supports(ggml_backend_buffer_type_t, ggml_backend_t backend) { return ggml_backend_is_mi355x(backend); }
+
+static const ggml_backend_buffer_type_i k_mi_split_buft_i = {
+    /* get_name         */ mi_split_buft_name,
+    /* alloc_buffer     */ mi_split_buft_alloc,
+    /* get_alignment    */ mi_split_buft_align,
+    /* get_max_size     */ nullptr,
+    /* get_alloc_size   */ mi_split_buft_alloc_size,
+    /* supports_backend */ mi_split_buft_supports,
+    /* is_host          */ nullptr,
+};
+
+// ---------------------------------------------------------------------------------------------
 // backend context
 // ---------------------------------------------------------------------------------------------
 
@@ -250,6 +422,7 @@ struct mi_backend_ctx {
     bool graph_capture = true;
     int last_launches = 0;
     uint16_t * tables = nullptr;  // device: exp, gelu, silu fp16 tables (3 x 65536)
+    hipEvent_t split_ready = nullptr;  // src1 of a split mul_mat is ready on `stream`
 };
 
 static ggml_guid_t mi_guid() {
@@ -430,21 +603,22 @@ static void invalidate_activations(mi_backend_ctx * ctx, const ggml_tensor * wri
             c.end());
 }
 
-static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
-    const ggml_tensor * src0 = dst->src[0];
-    const ggml_tensor * src1 = dst->src[1];
+// The mul_mat of (src0, src1) with src0's rows taken from (W, N) and the output written at out
+// (column strides nb1..nb3): op_mul_mat runs the whole node through it, the split-buffer path
+// (op_mul_mat_split) each device's row slice.
+static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const void * W, int64_t N, const ggml_tensor * src1,
+                        float * out, size_t nb1, size_t nb2, size_t nb3) {
     MI_ASSERT(src1->type == GGML_TYPE_F32);
     MI_ASSERT(src0->nb[0] == ggml_type_size(src0->type));
     MI_ASSERT(src1->nb[0] == sizeof(float));
-    MI_ASSERT(dst->nb[0] == sizeof(float));
     MI_ASSERT(src0->ne[0] == src1->ne[0]);
     MI_ASSERT(src1->ne[2] % src0->ne[2] == 0 && src1->ne[3] % src0->ne[3] == 0);
 
     mi_mm_desc m;
-    m.W = src0->data;
+    m.W = W;
     m.type = src0->type;
     m.K = src0->ne[0];
-    m.N = src0->ne[1];
+    m.N = N;
     m.ne02 = src0->ne[2];
     m.ne03 = src0->ne[3];
     m.nb01 = src0->nb[1];
@@ -453,10 +627,10 @@ static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
     m.ne11 = src1->ne[1];
     m.ne12 = src1->ne[2];
     m.ne13 = src1->ne[3];
-    m.dst = (float *) dst->data;
-    m.nb1 = dst->nb[1];
-    m.nb2 = dst->nb[2];
-    m.nb3 = dst->nb[3];
+    m.dst = out;
+    m.nb1 = nb1;
+    m.nb2 = nb2;
+    m.nb3 = nb3;
 
     const int kind = act_kind(src0->type);
     if (kind < 0) {
@@ -481,6 +655,106 @@ static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
         }
     }
     ctx->last_launches++;
+}
+
+static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
+    MI_ASSERT(dst->nb[0] == sizeof(float));
+    const ggml_tensor * src0 = dst->src[0];
+    mul_mat_run(ctx, src0, src0->data, src0->ne[1], dst->src[1], (float *) dst->data, dst->nb[1], dst->nb[2], dst->nb[3]);
+}
+
+// Per-slot helper context of the split path: its own stream (on the slot's device), scratch and
+// activation cache, plus the event that hands the slot's gathered rows back to the caller.
+struct mi_split_aux {
+    mi_backend_ctx ctx;
+    hipEvent_t done = nullptr;
+};
+
+static mi_split_aux * split_aux(int slot, int main_device) {
+    static std::mutex mutex;
+    static mi_split_aux * aux[GGML_MI355X_MAX_DEVICES] = {};
+    std::lock_guard<std::mutex> lock(mutex);
+    if (!aux[slot]) {
+        auto * a = new mi_split_aux();
+        a->ctx.device = slot_device(slot);
+        a->ctx.name = "MI355X_Split" + std::to_string(slot);
+        mi_device_guard g(a->ctx.device);
+        MI_CHECK(hipStreamCreateWithFlags(&a->ctx.stream, hipStreamNonBlocking));
+        MI_CHECK(hipEventCreateWithFlags(&a->done, hipEventDisableTiming));
+        aux[slot] = a;
+    }
+    if (aux[slot]->ctx.device != main_device) {
+        // peer access both ways for the activation copy in and the row gather out (xGMI)
+        for (const auto & pr : {std::make_pair(aux[slot]->ctx.device, main_device), std::make_pair(main_device, aux[slot]->ctx.device)}) {
+            mi_device_guard g(pr.first);
+            const hipError_t e = hipDeviceEnablePeerAccess(pr.second, 0);
+            if (e != hipSuccess) (void) hipGetLastError();  // already enabled
+        }
+    }
+    return aux[slot];
+}
+
+// GGML_OP_MUL_MAT with a weight in the split buffer type (ggml-cuda.cu:1360-1647 analogue): the
+// slot on the backend's own device computes its rows in place into dst; every other slot gets
+// src1 copied to its device (peer copy over xGMI), computes its rows on its own stream into local
+// scratch, and copies them back into dst's row range (a pitched copy), ordered by events.
+static void op_mul_mat_split(mi_backend_ctx * ctx, ggml_tensor * dst) {
+    const ggml_tensor * src0 = dst->src[0];
+    const ggml_tensor * src1 = dst->src[1];
+    MI_ASSERT(src0->view_src == nullptr && "views of split tensors are not supported");
+    MI_ASSERT(src0->ne[2] == 1 && src0->ne[3] == 1 && src1->ne[2] == 1 && src1->ne[3] == 1);
+    MI_ASSERT(src1->type == GGML_TYPE_F32 && ggml_is_contiguous(src1) && dst->nb[0] == sizeof(float));
+    const auto * extra = (const mi_split_extra *) src0->extra;
+    const int64_t K = src0->ne[0], ncols = src1->ne[1];
+    bool ready_recorded = false;
+    std::vector<mi_split_aux *> waits;
+    for (const auto & sl : extra->slices) {
+        const int64_t rows = sl.row_high - sl.row_low;
+        float * out = (float *) ((char *) dst->data + sl.row_low * sizeof(float));
+        if (sl.slot == ctx->device) {
+            mul_mat_run(ctx, src0, sl.ptr, rows, src1, out, dst->nb[1], dst->nb[2], dst->nb[3]);
+            continue;
+        }
+        mi_split_aux * a = split_aux(sl.slot, ctx->device);
+        if (!ready_recorded) {
+            mi_device_guard g(ctx->device);
+            if (!ctx->split_ready) MI_CHECK(hipEventCreateWithFlags(&ctx->split_ready, hipEventDisableTiming));
+            MI_CHECK(hipEventRecord(ctx->split_ready, ctx->stream));
+            ready_recorded = true;
+        }
+        mi_device_guard g(a->ctx.device);
+        MI_CHECK(hipStreamWaitEvent(a->ctx.stream, ctx->split_ready, 0));
+        const int64_t ld = (rows + 3) & ~(int64_t) 3;  // 16-byte aligned local columns
+        const size_t xbytes = (size_t) K * ncols * sizeof(float);
+        const size_t ybytes = (size_t) ld * ncols * sizeof(float);
+        const int kind = act_kind(src0->type);
+        size_t need = xbytes + ybytes + 4 * kBufferAlign;
+        if (kind >= 0) need += act_bytes(kind, K, ncols) + act_bytes(kind == 2 ? 5 : kind + 6, K, ncols) + 2 * kBufferAlign;
+        scratch_reserve(&a->ctx, need);  // stream-ordered reuse: earlier users of this scratch ran on the same stream
+        a->ctx.scratch_used = 0;
+        a->ctx.act_cache.clear();
+        void * xl = scratch_take(&a->ctx, xbytes);
+        float * yl = (float *) scratch_take(&a->ctx, ybytes);
+        if (a->ctx.device == ctx->device) {
+            MI_CHECK(hipMemcpyAsync(xl, src1->data, xbytes, hipMemcpyDeviceToDevice, a->ctx.stream));
+        } else {
+            MI_CHECK(hipMemcpyPeerAsync(xl, a->ctx.device, src1->data, ctx->device, xbytes, a->ctx.stream));
+        }
+        ggml_tensor x1 = *src1;  // src1 as it lies on the slot's device
+        x1.data = xl;
+        x1.view_src = nullptr;
+        x1.view_offs = 0;
+        a->ctx.last_launches = 0;
+        mul_mat_run(&a->ctx, src0, sl.ptr, rows, &x1, yl, (size_t) ld * sizeof(float), (size_t) ld * ncols * sizeof(float),
+                    (size_t) ld * ncols * sizeof(float));
+        ctx->last_launches += a->ctx.last_launches;
+        MI_CHECK(hipMemcpy2DAsync(out, dst->nb[1], yl, (size_t) ld * sizeof(float), (size_t) rows * sizeof(float), (size_t) ncols,
+                                  hipMemcpyDeviceToDevice, a->ctx.stream));
+        MI_CHECK(hipEventRecord(a->done, a->ctx.stream));
+        waits.push_back(a);
+    }
+    mi_device_guard g(ctx->device);
+    for (mi_split_aux * a : waits) MI_CHECK(hipStreamWaitEvent(ctx->stream, a->done, 0));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -657,7 +931,7 @@ static bool overlaps(const ggml_tensor * a, const ggml_tensor * b) {
 }
 
 static bool fused_mv_eligible(const ggml_tensor * n) {
-    if (n->op != GGML_OP_MUL_MAT) return false;
+    if (n->op != GGML_OP_MUL_MAT || is_split_tensor(n->src[0])) return false;
     const ggml_tensor * a = n->src[0];
     const ggml_tensor * b = n->src[1];
     if (b->type != GGML_TYPE_F32 || !mi_mmv_fused_supported(a->type, a->ne[0], b->ne[1])) return false;
@@ -808,6 +1082,7 @@ static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const
     ggml_tensor * mm = g->nodes[i];
     const ggml_tensor * w = mm->src[0];
     const ggml_tensor * x = pro_x ? pro_x : mm->src[1];
+    if (is_split_tensor(w)) return -1;
     if (w->type != GGML_TYPE_F16 || x->type != GGML_TYPE_F32) return -1;
     if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1 || x->ne[1] > 8) return -1;
     if (w->nb[0] != 2 || w->nb[1] % 16 != 0 || (uintptr_t) w->data % 16 != 0 || x->nb[0] != sizeof(float)) return -1;
@@ -1162,6 +1437,11 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
             next_attn++;
             continue;
         }
+        if (node->op == GGML_OP_MUL_MAT && is_split_tensor(node->src[0])) {
+            op_mul_mat_split(ctx, node);
+            invalidate_activations(ctx, node);
+            continue;
+        }
         int last = -1;
         if (!no_node_fusion) {
             switch (node->op) {
@@ -1392,9 +1672,25 @@ ggml_backend_buffer_type_t ggml_backend_mi355x_host_buffer_type(void) {
 }
 
 ggml_backend_buffer_type_t ggml_backend_mi355x_split_buffer_type(const float * tensor_split) {
-    (void) tensor_split;
-    fprintf(stderr, "ggml-mi355x: the tensor-split row buffer type is not implemented yet\n");
-    return nullptr;
+    // one buffer type per distinct split, kept for the process lifetime (ggml-cuda.cu:941-975);
+    // tensor_split: GGML_MI355X_MAX_DEVICES proportions (all zero / null = equal rows per slot)
+    static std::mutex mutex;
+    static std::map<std::vector<float>, ggml_backend_buffer_type *> types;
+    std::lock_guard<std::mutex> lock(mutex);
+    const int n = split_slots();
+    std::vector<float> cum(n, 0.0f);
+    const bool all_zero = tensor_split == nullptr || std::all_of(tensor_split, tensor_split + n, [](float v) { return v == 0.0f; });
+    float sum = 0.0f;
+    for (int i = 0; i < n; i++) {
+        cum[i] = sum;
+        sum += all_zero ? 1.0f : std::max(tensor_split[i], 0.0f);
+    }
+    for (int i = 0; i < n; i++) cum[i] /= sum;
+    auto it = types.find(cum);
+    if (it != types.end()) return it->second;
+    auto * buft = new ggml_backend_buffer_type{k_mi_split_buft_i, new mi_split_buft_ctx{cum}};
+    types.emplace(cum, buft);
+    return buft;
 }
 
 bool ggml_backend_is_mi355x(ggml_backend_t backend) {

@@ -158,6 +158,7 @@ _SIGS = {
     "ggml_backend_is_mi355x": ([c_void_p], c_bool),
     "ggml_backend_mi355x_buffer_type": ([c_int], c_void_p),
     "ggml_backend_mi355x_host_buffer_type": ([], c_void_p),
+    "ggml_backend_mi355x_split_buffer_type": ([c_void_p], c_void_p),
     "ggml_backend_mi355x_get_device_count": ([], c_int),
     "ggml_backend_mi355x_get_device_description": ([c_int, c_char_p, c_size_t], None),
     "ggml_backend_mi355x_get_device_memory": ([c_int, POINTER(c_size_t), POINTER(c_size_t)], None),
