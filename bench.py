@@ -184,6 +184,103 @@ def shard_range(total: int, world: int, rank: int):
     return start, base + (1 if rank < rem else 0)
 
 
+def row_shard(N: int, world: int, rank: int, rounding: int = 64):
+    """Rows [r0, r1) of an N-row weight held by `rank` on the tensor-split row path: cumulative
+    equal fractions rounded down to the GEMM's 64-row tile, the last rank takes the rest (the
+    split of ggml_backend_mi355x_split_buffer_type / ggml-cuda.cu:660-676)."""
+    def start(r):
+        if r == 0:
+            return 0
+        v = (N * r) // world
+        return v - v % rounding
+    return start(rank), (N if rank == world - 1 else start(rank + 1))
+
+
+def reassemble_rows(y_all: np.ndarray, N: int, world: int, B: int) -> np.ndarray:
+    """Y [B, N] from the all-gathered row slices: y_all holds, per rank, a [B, rows_max] block
+    (ggml dst layout: rows contiguous per column), of which the first r1 - r0 rows are real."""
+    rows_max = y_all.size // (world * B)
+    blocks = y_all.reshape(world, B, rows_max)
+    out = np.empty((B, N), y_all.dtype)
+    for r in range(world):
+        r0, r1 = row_shard(N, world, r)
+        out[:, r0:r1] = blocks[r, :, :r1 - r0]
+    return out
+
+
+class _DevArray:
+    """__cuda_array_interface__ over a device pointer (ggml device buffer memory -> torch view)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (ptr, False), "version": 2, "strides": None}
+
+
+def torch_view(torch, lib, t, device):
+    """A torch f32 view of ggml tensor `t`'s device memory (no copy)."""
+    n = int(lib.ggml_nelements(t))
+    return torch.as_tensor(_DevArray(G.tensor_data_ptr(lib, t), n), device=device)
+
+
+def rowsplit_prefill(lib, backend, dist, world, rank, device, torch, steps=5, K=4096, N=4096, B=512):
+    """Optional tensor-split row path over RCCL (north_star "RCCL only for
+    the optional tensor-split row path"): rank r holds rows row_shard(N) of one Q4_K weight; per
+    step rank 0's prompt activations X (f32 [K, B]) are broadcast to every rank (RCCL over xGMI),
+    each rank computes its Y rows on its GPU, and the row slices are all-gathered (RCCL)."""
+    r0, r1 = row_shard(N, world, rank)
+    rows = r1 - r0
+    rows_max = max(row_shard(N, world, r)[1] - row_shard(N, world, r)[0] for r in range(world))
+    ovh = lib.ggml_tensor_overhead() * 8 + lib.ggml_graph_overhead()
+    ctx = G.Context(lib, ovh, no_alloc=True)
+    c = ctx.ctx
+    w = lib.ggml_new_tensor_2d(c, 12, K, rows)
+    x = lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F32, K, B)
+    y = lib.ggml_mul_mat(c, w, x)
+    ypad = lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F32, rows_max, B)  # all_gather needs equal slices
+    g = lib.ggml_new_graph(c)
+    lib.ggml_build_forward_expand(g, y)
+    buf = lib.ggml_backend_alloc_ctx_tensors(c, backend)
+    wf = synth.uniform(42, K * N)[r0 * K:r1 * K]
+    wq = np.empty(G.row_size(12, K) * rows, np.uint8)
+    lib.ggml_quantize_chunk(12, wf.ctypes.data, wq.ctypes.data, 0, rows, K, None)
+    G.tensor_set(lib, w, wq)
+    if rank == 0:
+        G.tensor_set(lib, x, synth.uniform(43, K * B))
+    x_t = torch_view(torch, lib, x, device)
+    y_t = torch_view(torch, lib, y, device).view(B, rows)
+    ypad_t = torch_view(torch, lib, ypad, device).view(B, rows_max)
+    y_all = torch.empty(world * B * rows_max, dtype=torch.float32, device=device)
+
+    def step():
+        dist.broadcast(x_t, src=0)
+        torch.cuda.current_stream().synchronize()  # X landed before the backend stream reads it
+        lib.ggml_backend_graph_compute(backend, g)
+        if rows != rows_max:
+            ypad_t[:, :rows].copy_(y_t)
+            dist.all_gather_into_tensor(y_all, ypad_t.reshape(-1))
+        else:
+            dist.all_gather_into_tensor(y_all, y_t.reshape(-1))
+
+    step()  # warm-up (RCCL communicator set-up)
+
+    def run():
+        for _ in range(steps):
+            step()
+
+    def sync():
+        lib.ggml_backend_synchronize(backend)
+        torch.cuda.synchronize()
+
+    dt = timed_region(run, sync, dist, device)
+    y_full = reassemble_rows(y_all.cpu().numpy(), N, world, B)
+    res = {"workload": f"Q4_K {K}x{N} x B={B}, rows split over {world} ranks: RCCL broadcast of X, local GEMM, RCCL all-gather of Y",
+           "rows_per_rank": rows, "TFLOP/s": round(2.0 * K * N * B * steps / dt / 1e12, 2),
+           "us_per_step": round(dt / steps * 1e6, 2),
+           "y_checksum": float(np.abs(y_full).sum())}
+    lib.ggml_backend_buffer_free(buf)
+    ctx.free()
+    return res
+
+
 def timed_region(run, sync, dist=None, device=None):
     """Barrier + sync on both sides of `run()`; returns the MAX wall time over ranks."""
     sync()
@@ -370,6 +467,13 @@ def main():
                                      "columns_per_rank": cnt, "TFLOP/s": round(2.0 * 4096 * 4096 * 512 * 8 * 5 / dtp / 1e12, 2),
                                      "us_per_mul_mat": round(dtp / 5 / 8 * 1e6, 2)}
         w4.free()
+
+    if world > 1 and not args.no_sweep:
+        # the optional tensor-split row path (RCCL): reported beside the main line, never fatal to it
+        try:
+            result["prefill_rowsplit_rccl"] = rowsplit_prefill(lib, backend, dist, world, rank, torch.device("cuda", local_rank), torch)
+        except Exception as e:  # noqa: BLE001
+            result["prefill_rowsplit_rccl"] = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0 and world == 1 and not args.no_gpt2:
         # BASELINE config 4 (the metric's "+ GPT-2 tokens/s" half)

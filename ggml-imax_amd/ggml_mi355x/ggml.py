@@ -255,6 +255,11 @@ def tensor_set(lib: Lib, t, arr: np.ndarray, offset: int = 0):
     lib.ggml_backend_tensor_set(t, arr.ctypes.data, offset, arr.nbytes)
 
 
+def tensor_data_ptr(lib: Lib, t) -> int:
+    """Device (or host) address of tensor t's data (ggml_tensor.data, offset 280)."""
+    return int(t.contents.data or 0)
+
+
 def tensor_get(lib: Lib, t, dtype=np.float32, count=None) -> np.ndarray:
     n = lib.ggml_nbytes(t)
     out = np.empty(n // np.dtype(dtype).itemsize, dtype=dtype)

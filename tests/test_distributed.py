@@ -88,3 +88,69 @@ def test_prompt_sharded_mul_mat_gloo(tmp_path, B):
     assert np.array_equal(sharded.view(np.uint32), full.view(np.uint32))
     dts = [float(np.load(tmp_path / f"dt{r}.npy")[0]) for r in range(world)]
     assert dts[0] == dts[1] > 0  # every rank reports the max over ranks
+
+
+# ------------------------------------------------------------------ tensor-split row path (RCCL leg)
+
+def test_row_shard_covers_exactly():
+    for N in (64, 1000, 4096, 11008):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                r0, r1 = bench.row_shard(N, world, r)
+                assert r0 % 64 == 0
+                seen.extend(range(r0, r1))
+            assert seen == list(range(N))
+
+
+def _rowsplit_worker(rank, world, port, K, N, B, out_dir):
+    """bench.rowsplit_prefill's exchange on gloo: broadcast X from rank 0, each rank computes its
+    rows of W.X with the reference CPU backend, all-gather the padded row slices, reassemble."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ref = G.Lib([REF_LIB], isolated=True)
+        cpu = ref.ggml_backend_cpu_init()
+        ref.ggml_backend_cpu_set_n_threads(cpu, 2)
+        r0, r1 = bench.row_shard(N, world, rank)
+        rows = r1 - r0
+        rows_max = max(bench.row_shard(N, world, r)[1] - bench.row_shard(N, world, r)[0] for r in range(world))
+        from ggml_mi355x import synth
+        x = torch.from_numpy(synth.uniform(43, K * B)) if rank == 0 else torch.zeros(K * B)
+        dist.broadcast(x, src=0)
+        wf = synth.uniform(42, K * N)
+        mine = bench.MulMatWorkload(ref, cpu, 12, K, rows, B, 1, seed=5)
+        wq = np.empty(G.row_size(12, K) * rows, np.uint8)
+        ref.ggml_quantize_chunk(12, wf[r0 * K:r1 * K].ctypes.data, wq.ctypes.data, 0, rows, K, None)
+        G.tensor_set(ref, mine.w[0], wq)
+        G.tensor_set(ref, mine.x[0], x.numpy())
+        ref.ggml_backend_graph_compute(cpu, mine.graph)
+        y = G.tensor_get(ref, mine.y[0]).reshape(B, rows)
+        ypad = np.zeros((B, rows_max), np.float32)
+        ypad[:, :rows] = y
+        y_all = torch.empty(world * B * rows_max)
+        dist.all_gather_into_tensor(y_all, torch.from_numpy(ypad).reshape(-1))
+        if rank == 0:
+            np.save(os.path.join(out_dir, "rowsplit.npy"), bench.reassemble_rows(y_all.numpy(), N, world, B))
+            full = bench.MulMatWorkload(ref, cpu, 12, K, N, B, 1, seed=5)
+            wq_full = np.empty(G.row_size(12, K) * N, np.uint8)
+            ref.ggml_quantize_chunk(12, wf.ctypes.data, wq_full.ctypes.data, 0, N, K, None)
+            G.tensor_set(ref, full.w[0], wq_full)
+            G.tensor_set(ref, full.x[0], x.numpy())
+            ref.ggml_backend_graph_compute(cpu, full.graph)
+            np.save(os.path.join(out_dir, "full.npy"), G.tensor_get(ref, full.y[0]).reshape(B, N))
+            full.free()
+        mine.free()
+        ref.ggml_backend_free(cpu)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(not os.path.exists(REF_LIB), reason="make -C oracle ref")
+@pytest.mark.parametrize("world,N", [(2, 512), (3, 320)])
+def test_rowsplit_exchange_gloo(tmp_path, world, N):
+    K, B = 512, 4
+    mp.spawn(_rowsplit_worker, args=(world, _free_port(), K, N, B, str(tmp_path)), nprocs=world, join=True)
+    full = np.load(tmp_path / "full.npy")
+    split = np.load(tmp_path / "rowsplit.npy")
+    assert np.array_equal(split.view(np.uint32), full.view(np.uint32))
