@@ -26,7 +26,8 @@ GGML_API bool ggml_backend_is_mi355x(ggml_backend_t backend);
 GGML_API ggml_backend_buffer_type_t ggml_backend_mi355x_buffer_type(int device);
 
 // ggml-cuda.h:29  ggml_backend_cuda_split_buffer_type(const float * tensor_split): rows of a
-// matrix split across devices (tensor-split row path)
+// matrix split across devices (tensor-split row path); tensor_split = GGML_MI355X_MAX_DEVICES
+// proportions (NULL / all zero = equal), slices rounded to 64-row GEMM tiles
 GGML_API ggml_backend_buffer_type_t ggml_backend_mi355x_split_buffer_type(const float * tensor_split);
 
 // ggml-cuda.h:32  ggml_backend_cuda_host_buffer_type(): pinned host memory for fast H2D/D2H
@@ -50,8 +51,8 @@ GGML_API int ggml_backend_mi355x_reg_devices(void);
 // hipStream_t the backend launches on (for external timing with HIP events / stream interop)
 GGML_API void * ggml_backend_mi355x_get_stream(ggml_backend_t backend);
 
-// hipGraph capture of repeated identical graphs (decode loops); on by default, env
-// GGML_MI355X_DISABLE_GRAPHS=1 turns it off (analogue of GGML_CUDA_DISABLE_GRAPHS).
+// Graph-replay switch kept for parity with GGML_CUDA_DISABLE_GRAPHS (env GGML_MI355X_DISABLE_GRAPHS);
+// replay is not implemented: the decode token keeps the GPU busy, so launch overhead is hidden.
 GGML_API void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable);
 
 // Number of kernels launched by the last graph_compute (for tests / profiling).
