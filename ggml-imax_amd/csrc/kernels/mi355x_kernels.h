@@ -85,6 +85,8 @@ struct mi_tuning {
     int f16_variant;  // decode F16 GEMV: 0 = 16 lanes per row (k_mmv_f16_w16), 1 = quad per row (k_mmv_f16_x)
     int f16_threads;  // k_mmv_f16_w16 workgroup size override (0 = automatic)
     int mmq_variant;  // prefill GEMM: 0 = k_mmq3 (activations in registers), 1 = k_mmq2 (activations via LDS)
+    int attn_variant; // attention block: 0 = k_attn_fast where it fits, 1 = k_attn_ordered
+    int attn_abl;     // timing ablations of k_attn_fast (0 = none; results invalid otherwise)
 };
 extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);

@@ -637,6 +637,159 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_ordered(mi_attn_desc a, c
     }
 }
 
+// One-round-trip variant of k_attn_ordered for decode-sized contexts (n_kv <= 32768 / D): every
+// global load of the block -- q, the K rows of all key rounds, the whole V slab of the head -- is
+// issued before any arithmetic, so the kernel pays one memory round trip instead of three (q ->
+// K -> V in k_attn_ordered). K rows stay in registers for the KQ dots; the V slab lands in LDS
+// (rows padded to D + 1 floats: conflict-free column walks) and the KQV chains read it from
+// there. Every dot, mask, soft_max and rounding step is k_attn_ordered's, so the result is the
+// same bit for bit.
+// KVCAP: the key-count bucket the launch was sized for (n_kv <= KVCAP), so only the key rounds and
+// V-slab loads the context needs are issued. q / K loads are 16-byte vector loads (host-checked
+// contiguity and alignment): at decode the load phase is issue-bound on only H workgroups.
+template <int D, int KVCAP, int ABL = 0>
+__global__ __launch_bounds__(512) void k_attn_fast(mi_attn_desc a, const uint16_t * __restrict__ exp_table) {
+    constexpr int KVMAX = KVCAP;               // keys this instantiation serves
+    constexpr int KR = KVMAX / 128;            // key rounds of the 128 quads
+    constexpr int QS = D / 32;                 // 32-element steps of one head-dim dot
+    constexpr int VS = D + 1;                  // padded LDS row stride of the V slab
+    constexpr int VREG = KVMAX * D / 512 / 4;  // float4 of the V slab per thread
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // vs[n_kv][VS] | p[n_kv]
+    __shared__ float shf[8];
+    __shared__ double shd[8];
+    const int h = blockIdx.x, t = blockIdx.y;
+    const int hk = h / a.r2;
+    const int tid = threadIdx.x, q = tid & 3, quad = tid >> 2;
+    const int n_kv = a.n_kv;
+    float * vs = sm;
+    float * p = sm + n_kv * VS;
+
+    // ---- 1. all loads up front (addresses clamped into the tensors instead of predicated)
+    float qv[QS][8];
+    const char * qrow = a.q + (size_t) t * a.q_nb[1] + (size_t) h * a.q_nb[2];
+#pragma unroll
+    for (int st = 0; st < QS; st++) {
+        const float4 u0 = *(const float4 *) (qrow + (size_t) (st * 32 + 8 * q) * 4);  // q_nb[0] == 4
+        const float4 u1 = *(const float4 *) (qrow + (size_t) (st * 32 + 8 * q + 4) * 4);
+        qv[st][0] = u0.x; qv[st][1] = u0.y; qv[st][2] = u0.z; qv[st][3] = u0.w;
+        qv[st][4] = u1.x; qv[st][5] = u1.y; qv[st][6] = u1.z; qv[st][7] = u1.w;
+    }
+    float kv[KR][QS][8];
+#pragma unroll
+    for (int r = 0; r < KR; r++) {
+        const int k = min(quad + 128 * r, n_kv - 1);
+        const char * krow = a.k + (size_t) k * a.k_nb[1] + (size_t) hk * a.k_nb[2];
+#pragma unroll
+        for (int st = 0; st < QS; st++) {
+            const float4 u0 = *(const float4 *) (krow + (size_t) (st * 32 + 8 * q) * 4);  // k_nb[0] == 4
+            const float4 u1 = *(const float4 *) (krow + (size_t) (st * 32 + 8 * q + 4) * 4);
+            kv[r][st][0] = u0.x; kv[r][st][1] = u0.y; kv[r][st][2] = u0.z; kv[r][st][3] = u0.w;
+            kv[r][st][4] = u1.x; kv[r][st][5] = u1.y; kv[r][st][6] = u1.z; kv[r][st][7] = u1.w;
+        }
+    }
+    float4 vr[VREG];
+    const char * vh = a.v + (size_t) hk * a.v_nb[2];
+#pragma unroll
+    for (int i = 0; i < VREG; i++) {
+        const int e = 4 * (tid + 512 * i);
+        const int k = min(e / D, n_kv - 1), d = e % D;  // 4 consecutive d of one key (D % 4 == 0)
+        vr[i] = *(const float4 *) (vh + (size_t) k * a.v_nb[0] + (size_t) d * 4);  // v_nb[1] == 4, 16-B aligned (host-checked)
+    }
+
+    // ---- 2. KQ from registers (ggml_vec_dot_f32 order per dot), pre-scale, causal mask, sm scale
+#pragma unroll
+    for (int r = 0; r < KR; r++) {
+        const int k = quad + 128 * r;
+        if (128 * r >= n_kv) break;  // block-uniform
+        float acc[8];
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc[l] = 0.0f;
+#pragma unroll
+        for (int st = 0; st < QS; st++)
+#pragma unroll
+            for (int l = 0; l < 8; l++) acc[l] = __fmaf_rn(kv[r][st][l], qv[st][l], acc[l]);
+        const float v = quad_reduce_avx(acc);
+        if (q == 0 && k < n_kv) {
+            float w = mul_rn(v, a.pre_scale);
+            if (k >= a.n_past && k > a.n_past + t) w = -INFINITY;
+            p[k] = mul_rn(w, a.sm_scale);
+        }
+    }
+    if constexpr (ABL == 3) {  // timing ablation: loads + KQ only
+        if (q == 0 && quad < n_kv) *(float *) (a.out + (size_t) quad * 4) = p[quad] + vr[0].x + vr[VREG - 1].w;
+        return;
+    }
+    // ---- 3. V slab into LDS
+#pragma unroll
+    for (int i = 0; i < VREG; i++) {
+        const int e = 4 * (tid + 512 * i);
+        const int k = e / D, d = e % D;
+        if (k < n_kv) {
+            float * dstv = vs + k * VS + d;
+            dstv[0] = vr[i].x;
+            dstv[1] = vr[i].y;
+            dstv[2] = vr[i].z;
+            dstv[3] = vr[i].w;
+        }
+    }
+    __syncthreads();
+
+    // ---- 4. soft_max over p (as k_attn_ordered)
+    const int nw = 8;
+    float mx = -INFINITY;
+    for (int k = tid; k < n_kv; k += 512) mx = fmaxf(mx, p[k]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    if ((tid & 63) == 0) shf[tid >> 6] = mx;
+    __syncthreads();
+    mx = -INFINITY;
+    for (int w = 0; w < nw; w++) mx = fmaxf(mx, shf[w]);
+    double ssum = 0.0;
+    for (int k = tid; k < n_kv; k += 512) {
+        const float w = p[k];
+        const float v = w == -INFINITY ? 0.0f : (ABL == 1 ? sub_rn(w, mx) : mi_h2f(exp_table[mi_f2h(sub_rn(w, mx))]));
+        p[k] = v;
+        ssum += (double) v;  // fp16 values: every partial double sum is exact
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ssum += __shfl_xor(ssum, off, 64);
+    if ((tid & 63) == 0) shd[tid >> 6] = ssum;
+    __syncthreads();
+    double sum = 0.0;
+    for (int w = 0; w < nw; w++) sum += shd[w];
+    const float inv = (float) (1.0 / sum);
+    for (int k = tid; k < n_kv; k += 512) p[k] = mul_rn(p[k], inv);
+    __syncthreads();
+
+    if constexpr (ABL == 2) {  // timing ablation: no KQV
+        if (tid < D) *(float *) (a.out + (size_t) tid * a.o_nb[0] + (size_t) t * a.o_nb[1] + (size_t) h * a.o_nb[2]) = p[tid];
+        return;
+    }
+    // ---- 5. KQV[d] = ggml_vec_dot_f32(n_kv, V_trans[:, d, h], p) from LDS, quad d
+    const int npv = n_kv & ~31;
+    for (int d0 = 0; d0 < D; d0 += 128) {
+        const int d = d0 + quad;
+        if (d >= D) break;
+        float acc[8];
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc[l] = 0.0f;
+        for (int i = 8 * q; i < npv; i += 32) {
+#pragma unroll
+            for (int l = 0; l < 8; l++) acc[l] = __fmaf_rn(vs[(i + l) * VS + d], p[i + l], acc[l]);
+        }
+        float r = quad_reduce_avx(acc);
+        if (q == 0) {
+            const int L = n_kv - npv;
+            const int fused_from = (L >= 8 ? (L / 8) * 8 : 0) + (((L >= 8 ? L % 8 : L) >= 4) ? 4 : 0);
+            for (int j = 0; j < L; j++) {
+                const float x = vs[(npv + j) * VS + d], y = p[npv + j];
+                r = j < fused_from ? add_rn(r, mul_rn(x, y)) : __fmaf_rn(x, y, r);
+            }
+            *(float *) (a.out + (size_t) d * a.o_nb[0] + (size_t) t * a.o_nb[1] + (size_t) h * a.o_nb[2]) = r;
+        }
+    }
+}
+
 ord_geom make_ord_geom(const mi_mm_desc & m, int NC) {
     ord_geom g;
     g.K = m.K;
@@ -698,6 +851,38 @@ void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, con
 bool mi_attn_supported(int D, int n_kv) { return D >= 1 && D <= 256 && n_kv >= 1 && (size_t) (D + n_kv) * 4 <= 60 * 1024; }
 
 void mi_attn_ordered(const mi_attn_desc & a, const uint16_t * exp_table, hipStream_t s) {
+    static const bool lds_ok = [] {  // the V slab needs more than the default 64 KB of dynamic LDS
+        bool ok = true;
+        for (const void * f : {(const void *) k_attn_fast<64, 128>, (const void *) k_attn_fast<64, 256>, (const void *) k_attn_fast<64, 512>,
+                               (const void *) k_attn_fast<128, 128>, (const void *) k_attn_fast<128, 256>,
+                               (const void *) k_attn_fast<64, 512, 1>, (const void *) k_attn_fast<64, 512, 2>, (const void *) k_attn_fast<64, 512, 3>})
+            ok &= hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess;
+        (void) hipGetLastError();
+        return ok;
+    }();
+    const bool fast_ok = lds_ok && g_mi_tuning.attn_variant == 0 && a.v_nb[1] == 4 && a.q_nb[0] == 4 && a.k_nb[0] == 4 &&
+                         ((uintptr_t) a.v | a.v_nb[0] | a.v_nb[2] | (uintptr_t) a.q | a.q_nb[1] | a.q_nb[2] | (uintptr_t) a.k | a.k_nb[1] |
+                          a.k_nb[2]) % 16 == 0;
+    const dim3 grid((unsigned) a.H, (unsigned) a.N);
+    if (fast_ok && a.D == 64 && a.n_kv <= 512) {
+        const size_t lds = (size_t) a.n_kv * (64 + 2) * sizeof(float);
+        switch (g_mi_tuning.attn_abl) {  // timing ablations only (results invalid)
+            case 1: hipLaunchKernelGGL((k_attn_fast<64, 512, 1>), grid, dim3(512), lds, s, a, exp_table); return;
+            case 2: hipLaunchKernelGGL((k_attn_fast<64, 512, 2>), grid, dim3(512), lds, s, a, exp_table); return;
+            case 3: hipLaunchKernelGGL((k_attn_fast<64, 512, 3>), grid, dim3(512), lds, s, a, exp_table); return;
+            default: break;
+        }
+        if (a.n_kv <= 128) hipLaunchKernelGGL((k_attn_fast<64, 128>), grid, dim3(512), lds, s, a, exp_table);
+        else if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_fast<64, 256>), grid, dim3(512), lds, s, a, exp_table);
+        else hipLaunchKernelGGL((k_attn_fast<64, 512>), grid, dim3(512), lds, s, a, exp_table);
+        return;
+    }
+    if (fast_ok && a.D == 128 && a.n_kv <= 256) {
+        const size_t lds = (size_t) a.n_kv * (128 + 2) * sizeof(float);
+        if (a.n_kv <= 128) hipLaunchKernelGGL((k_attn_fast<128, 128>), grid, dim3(512), lds, s, a, exp_table);
+        else hipLaunchKernelGGL((k_attn_fast<128, 256>), grid, dim3(512), lds, s, a, exp_table);
+        return;
+    }
     const size_t lds = (size_t) (a.D + a.n_kv) * sizeof(float);
     hipLaunchKernelGGL(k_attn_ordered, dim3((unsigned) a.H, (unsigned) a.N), dim3(kAttnThreads), lds, s, a, exp_table);
 }
