@@ -1122,6 +1122,27 @@ static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const
         }
     }
     if (out->type != GGML_TYPE_F32 || out->nb[0] != sizeof(float)) return -1;
+    // the graph's CPY nodes of row views of `out` that follow right away (GPT-2 writes the K and V
+    // rows of c_attn's output into its caches, main-backend.cpp:556-561): stored by the epilogue
+    int ncopy = 0;
+    for (int j = next_node(g, last); j >= 0 && ncopy < 2; j = next_node(g, j)) {
+        ggml_tensor * cp = g->nodes[j];
+        if (cp->op != GGML_OP_CPY) break;
+        const ggml_tensor * v = cp->src[0];
+        if (v->view_src != out || v->type != GGML_TYPE_F32 || v->nb[0] != sizeof(float) || v->view_offs % sizeof(float)) break;
+        if (v->ne[2] != 1 || v->ne[3] != 1 || v->ne[1] != out->ne[1] || (v->ne[1] > 1 && v->nb[1] != out->nb[1])) break;
+        const int64_t r0 = (int64_t) (v->view_offs / sizeof(float));
+        if (r0 + v->ne[0] > N) break;
+        if (cp->type != GGML_TYPE_F32 || !ggml_is_contiguous(cp) || ggml_nelements(cp) != ggml_nelements(v)) break;
+        if (overlaps(cp, w) || overlaps(cp, x) || overlaps(cp, out) || (bias_t && overlaps(cp, bias_t)) || (res_t && overlaps(cp, res_t))) break;
+        if (ncopy == 1 && overlaps(cp, g->nodes[last])) break;
+        e.copy[ncopy].row0 = r0;
+        e.copy[ncopy].row1 = r0 + v->ne[0];
+        e.copy[ncopy].ptr = (char *) cp->data;
+        e.copy[ncopy].col_stride = (size_t) v->ne[0] * sizeof(float);
+        ncopy++;
+        last = j;
+    }
     // every workgroup reads all of X and W; resid/bias are read per element. When the graph
     // allocator has placed `out` over X (X's last reader is this mul_mat), X is first converted
     // into the backend's scratch so no workgroup can see it overwritten.

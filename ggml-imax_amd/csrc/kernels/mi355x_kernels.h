@@ -136,6 +136,14 @@ struct mi_f16_epilogue {
     const char * resid = nullptr;        // [N, ncols] f32 (row stride resid_nb1), or null
     size_t resid_nb1 = 0;
     const uint16_t * gelu_table = nullptr;  // fp16 GELU table (applied after bias), or null
+    // up to two extra destinations of output row ranges (the graph's following CPY of a row view of
+    // the output, e.g. GPT-2's K/V cache writes): element (row, col) with row0 <= row < row1 is
+    // also stored at ptr + col * col_stride + (row - row0) * 4
+    struct row_copy {
+        int64_t row0 = 0, row1 = 0;
+        char * ptr = nullptr;
+        size_t col_stride = 0;
+    } copy[2];
 };
 // optional prologue: src1 = add(mul(norm|rms_norm(x, eps), g), b) computed in the kernel from x
 struct mi_norm_prologue {

@@ -256,6 +256,16 @@ __device__ __forceinline__ void stage_f16_activations(uint16_t * xs, double * sh
     }
 }
 
+// the epilogue's extra row-range copies (mi_f16_epilogue::copy)
+__device__ __forceinline__ void epi_row_copies(const mi_f16_epilogue & e, int64_t row, int64_t col, float v) {
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (e.copy[k].ptr && row >= e.copy[k].row0 && row < e.copy[k].row1) {
+            *(float *) (e.copy[k].ptr + col * e.copy[k].col_stride + (row - e.copy[k].row0) * sizeof(float)) = v;
+        }
+    }
+}
+
 // Decode-regime F16 GEMV with the activation conversion and the graph's epilogue fused in:
 //   - each workgroup converts its NC f32 activation columns to f16 in LDS (RNE, as the CPU's
 //     ggml_fp32_to_fp16_row, src/ggml.c:610-612), so no separate conversion launch;
@@ -341,6 +351,7 @@ __global__ __launch_bounds__(256) void k_mmv_f16_x(const uint8_t * __restrict__ 
             if (EPI == 2) v = add_rn(v, *(const float *) (e.resid + (i11 + c) * e.resid_nb1 + row * sizeof(float)));
             if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
             *(float *) ((char *) dst + (i11 + c) * ycol + row * sizeof(float)) = v;
+            epi_row_copies(e, row, i11 + c, v);
         }
     }
 }
@@ -433,6 +444,7 @@ __global__ __launch_bounds__(256) void k_mmv_f16_w16(const uint8_t * __restrict_
             if (EPI == 2) v = add_rn(v, *(const float *) (e.resid + (i11 + c) * e.resid_nb1 + row * sizeof(float)));
             if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
             *(float *) ((char *) dst + (i11 + c) * ycol + row * sizeof(float)) = v;
+            epi_row_copies(e, row, i11 + c, v);
         }
     }
 }
