@@ -505,7 +505,9 @@ static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
                     return false;
             }
         case GGML_OP_GET_ROWS:
-            return is_f16_or_f32(a) && b->type == GGML_TYPE_I32 && is_f32(op);
+            return (is_f16_or_f32(a) || a->type == GGML_TYPE_Q4_0 || a->type == GGML_TYPE_Q8_0 || a->type == GGML_TYPE_Q4_K ||
+                    a->type == GGML_TYPE_Q5_K) &&
+                   b->type == GGML_TYPE_I32 && is_f32(op);
         case GGML_OP_CPY:
         case GGML_OP_DUP:
         case GGML_OP_CONT:
@@ -1767,6 +1769,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "mmq_variant") == 0) {
         g_mi_tuning.mmq_variant = value;
+        return true;
+    }
+    if (strcmp(name, "mmv_order") == 0 && (value == 0 || value == 1)) {
+        g_mi_tuning.mmv_order = value;
         return true;
     }
     if (strcmp(name, "f16_threads") == 0 && (value == 0 || value == 64 || value == 128 || value == 256)) {

@@ -87,6 +87,7 @@ struct mi_tuning {
     int mmq_variant;  // prefill GEMM: 0 = k_mmq3 (activations in registers), 1 = k_mmq2 (activations via LDS)
     int attn_variant; // attention block: 0 = k_attn_fast where it fits, 1 = k_attn_ordered
     int attn_abl;     // timing ablations of k_attn_fast (0 = none; results invalid otherwise)
+    int mmv_order;    // quantized decode GEMV: 1 = the reference CPU's summation order (bit-identical, slower), 0 = tree sums
 };
 extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);

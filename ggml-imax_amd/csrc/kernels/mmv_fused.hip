@@ -32,7 +32,7 @@ static int env_int(const char * name, int def) {
 }
 
 // mmv_blocks == 0: size the grid from the kernel's residency (hipOccupancy...) per instance
-mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 0), env_int("GGML_MI355X_MMV_VARIANT", 0), env_int("GGML_MI355X_F16_VARIANT", 0), 0, env_int("GGML_MI355X_MMQ_VARIANT", 0), env_int("GGML_MI355X_ATTN_VARIANT", 0), env_int("GGML_MI355X_ATTN_ABL", 0)};
+mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 0), env_int("GGML_MI355X_MMV_VARIANT", 0), env_int("GGML_MI355X_F16_VARIANT", 0), 0, env_int("GGML_MI355X_MMQ_VARIANT", 0), env_int("GGML_MI355X_ATTN_VARIANT", 0), env_int("GGML_MI355X_ATTN_ABL", 0), env_int("GGML_MI355X_MMV_ORDER", 0)};
 
 namespace {
 
@@ -58,6 +58,13 @@ template <int QKA>
 __host__ __device__ constexpr size_t lds_bytes(int NC, int64_t K) {
     return (size_t) NC * (K + (K / QKA) * 4 + (K / 32) * 2);
 }
+
+// CPU-order combination scratch, after the activations: per wave and column kOrdCS words
+// (Q4_0/Q8_0: 9 rows of 68 for one 64-block chunk; K-quants: 16 superblock entries of 16);
+// kOrdCS = 8 (mod 32) keeps the eight columns' chain reads on distinct banks
+constexpr int kOrdCS = 648;
+__host__ __device__ constexpr size_t ord_offset(size_t act) { return (act + 15) & ~(size_t) 15; }
+__host__ __device__ constexpr size_t ord_bytes(int NC) { return (size_t) 4 * NC * kOrdCS * 4; }
 
 // one 256-element slice (four floats per lane) of column c into LDS
 template <int QKA>
@@ -186,6 +193,102 @@ struct FmtKQ {
             acc[c] += a.d[c * (K / 256) + s] * (dw * sumi - dmw * summ);
         }
     }
+
+    // CPU order (see ord_* below): per item (superblock s, 64-group j) the reference's eight int32
+    // lanes l -- sc[2j] * (bytes 4l..4l+3 of the low nibbles . q8) + sc[2j+1] * (high nibbles) --
+    // summed over the superblock's four items (a DPP quad: items 4s..4s+3 sit on adjacent lanes),
+    // plus the mins lane m[2j] * bsum32[2j] + m[2j+1] * bsum32[2j+1]. Entry of superblock sb in the
+    // scratch: [0..7] the eight int32 sums, [8..11] the four mins lanes (Q5_K: [8] their sum),
+    // [12] d = y.d * x.d, [13] dmin = -(y.d * x.dmin).
+    template <int NC>
+    __device__ static __forceinline__ void dot_ord(const Regs & r, int item, int slot, const lds_act & a, int64_t K, int ncols,
+                                                   uint32_t * scr) {
+        const int s = item >> 2, j = item & 3;
+        const uint32_t q[8] = {r.qa.x, r.qa.y, r.qa.z, r.qa.w, r.qb.x, r.qb.y, r.qb.z, r.qb.w};
+        uint32_t qlo[8], qhi[8];
+        if constexpr (Q5) {
+            const uint32_t h[8] = {r.ha.x, r.ha.y, r.ha.z, r.ha.w, r.hb.x, r.hb.y, r.hb.z, r.hb.w};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = (q[i] & 0x0F0F0F0Fu) | (((h[i] >> (2 * j)) & 0x01010101u) << 4);
+                qhi[i] = ((q[i] >> 4) & 0x0F0F0F0Fu) | (((h[i] >> (2 * j + 1)) & 0x01010101u) << 4);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = q[i] & 0x0F0F0F0Fu;
+                qhi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
+            }
+        }
+        const float dw = mi_h2f((uint16_t) (r.hdr.x & 0xFFFF));
+        const float dmw = mi_h2f((uint16_t) (r.hdr.x >> 16));
+        const uint32_t sh = 16u * (uint32_t) (j & 1);
+        const uint32_t x0 = r.hdr.y >> sh, x1 = r.hdr.z >> sh, x2 = r.hdr.w >> sh;
+        int sc0, m0, sc1, m1;
+        if (j < 2) {
+            sc0 = (int) (x0 & 63);
+            sc1 = (int) ((x0 >> 8) & 63);
+            m0 = (int) (x1 & 63);
+            m1 = (int) ((x1 >> 8) & 63);
+        } else {
+            sc0 = (int) ((x2 & 0xF) | (((x0 >> 6) & 3) << 4));
+            sc1 = (int) (((x2 >> 8) & 0xF) | (((x0 >> 14) & 3) << 4));
+            m0 = (int) (((x2 >> 4) & 0xF) | (((x1 >> 6) & 3) << 4));
+            m1 = (int) (((x2 >> 12) & 0xF) | (((x1 >> 14) & 3) << 4));
+        }
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) s * 256 + 64 * j);
+            const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            const int alo[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const int ahi[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            int v[8];
+#pragma unroll
+            for (int l = 0; l < 8; l++) {
+                // |products| < 2^23: the 24-bit multiplier is exact
+                v[l] = __mul24(sc0, mi_dot4((int) qlo[l], alo[l], 0)) + __mul24(sc1, mi_dot4((int) qhi[l], ahi[l], 0));
+                v[l] += mi_dpp<MI_DPP_QP_1032>(0, v[l]);
+                v[l] += mi_dpp<MI_DPP_QP_2301>(0, v[l]);
+            }
+            const int ss = *(const int *) (a.s32 + c * (K / 32) + s * 8 + 2 * j);
+            int pm = __mul24(m0, (int) (int16_t) (ss & 0xFFFF)) + __mul24(m1, ss >> 16);
+            if constexpr (Q5) {
+                pm += mi_dpp<MI_DPP_QP_1032>(0, pm);
+                pm += mi_dpp<MI_DPP_QP_2301>(0, pm);
+            }
+            uint32_t * e = scr + c * kOrdCS + (slot >> 2) * 16;
+            // lane j stores sums 2j and 2j+1 (all four lanes hold all eight after the quad sums)
+            const int w0 = j == 0 ? v[0] : j == 1 ? v[2] : j == 2 ? v[4] : v[6];
+            const int w1 = j == 0 ? v[1] : j == 1 ? v[3] : j == 2 ? v[5] : v[7];
+            *(uint2 *) (e + 2 * j) = make_uint2((uint32_t) w0, (uint32_t) w1);
+            if (!Q5 || j == 0) e[8 + j] = (uint32_t) pm;
+            const float yd = a.d[c * (K / 256) + s];
+            if (j == 2) e[12] = __float_as_uint(yd * dw);
+            if (j == 3) e[13] = __float_as_uint(-(yd * dmw));
+        }
+    }
+    // one chain step per superblock: acc[l] = fma(d, (float) sumi[l], acc[l]) (the reference's
+    // _mm256_fmadd_ps) and the mins accumulator: Q4_K four lanes acc_m[k] = fma(dmin, prod[k],
+    // acc_m[k]) (_mm_fmadd_ps), Q5_K one scalar summs += dmin * hsum(prod) (contracted by the
+    // reference's -mfma build)
+    __device__ static __forceinline__ void chain(const uint32_t * scr, int l, int n_items, float & A, float & M) {
+        const int nsb = n_items >> 2;
+        for (int sb = 0; sb < nsb; sb++) {
+            const uint32_t * e = scr + sb * 16;
+            A = fmaf(__uint_as_float(e[12]), (float) (int) e[l], A);
+            M = fmaf(__uint_as_float(e[13]), (float) (int) e[8 + (Q5 ? 0 : (l & 3))], M);
+        }
+    }
+    __device__ static __forceinline__ float finish(float A, float M) {
+        float z = A + __shfl_xor(A, 4, 8);
+        z = z + __shfl_xor(z, 2, 8);
+        z = z + __shfl_xor(z, 1, 8);
+        if constexpr (Q5) return z + M;
+        float m = M + __shfl_xor(M, 2, 8);
+        m = m + __shfl_xor(m, 1, 8);
+        return z + m;
+    }
 };
 
 // Q4_0 (18 B) / Q8_0 (34 B) blocks: 2-byte aligned. Load the dwords covering the quants
@@ -240,13 +343,71 @@ struct FmtQ0 {
             acc[c] += (float) sumi * (dw * a.d[c * (K / 32) + item]);
         }
     }
+
+    // CPU order: the reference's eight int32 lanes l of mul_sum_i8_pairs_float -- elements 4l..4l+3
+    // (Q4_0: low nibbles for l < 4, high nibbles of bytes 4(l-4).. for l >= 4, minus 8) -- and
+    // d = x.d * y.d, stored transposed: scratch [l][slot] (row stride 68 words), d at [8][slot].
+    template <int NC>
+    __device__ static __forceinline__ void dot_ord(const Regs & r, int item, int slot, const lds_act & a, int64_t K, int ncols,
+                                                   uint32_t * scr) {
+        uint32_t t[NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; i++) t[i] = r.off ? r.w[i + 1] : __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], 2);
+        const uint32_t dbits = (r.off ? r.w[0] >> 16 : r.w[0]) & 0xFFFF;
+        const float dw = mi_h2f((uint16_t) dbits);
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 32);
+            const int4 a0 = p[0], a1 = p[1];
+            const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            uint32_t * e = scr + c * kOrdCS + slot;
+#pragma unroll
+            for (int l = 0; l < 8; l++) {
+                int q;
+                if constexpr (Q8) {
+                    q = mi_dot4((int) t[l], av[l], 0);
+                } else {
+                    const uint32_t nib = l < 4 ? (t[l] & 0x0F0F0F0Fu) : ((t[l - 4] >> 4) & 0x0F0F0F0Fu);
+                    q = mi_dot4((int) nib, av[l], mi_dot4((int) 0xF8F8F8F8u, av[l], 0));  // (q - 8) . y
+                }
+                e[l * 68] = (uint32_t) q;
+            }
+            e[8 * 68] = __float_as_uint(dw * a.d[c * (K / 32) + item]);
+        }
+    }
+    // acc[l] = fma(d_i, (float) q[i][l], acc[l]) over the blocks in order (_mm256_fmadd_ps)
+    __device__ static __forceinline__ void chain(const uint32_t * scr, int l, int n_items, float & A, float & M) {
+        (void) M;
+        const uint32_t * q = scr + l * 68;
+        const float * d = (const float *) (scr + 8 * 68);
+        int i = 0;
+        for (; i + 4 <= n_items; i += 4) {
+            const uint4 qq = *(const uint4 *) (q + i);
+            const float4 dd = *(const float4 *) (d + i);
+            A = fmaf(dd.x, (float) (int) qq.x, A);
+            A = fmaf(dd.y, (float) (int) qq.y, A);
+            A = fmaf(dd.z, (float) (int) qq.z, A);
+            A = fmaf(dd.w, (float) (int) qq.w, A);
+        }
+        for (; i < n_items; i++) A = fmaf(d[i], (float) (int) q[i], A);
+    }
+    __device__ static __forceinline__ float finish(float A, float) {
+        // hsum_float_8: ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7))
+        float z = A + __shfl_xor(A, 4, 8);
+        z = z + __shfl_xor(z, 2, 8);
+        return z + __shfl_xor(z, 1, 8);
+    }
 };
 
 // ------------------------------------------------------------------ the streaming kernel
 
 // IPL = items per lane held in the prefetch ring (further items of long rows are loaded
 // in-line); PD = rows in flight ahead of the row being computed.
-template <class F, int NC, int PD, int IPL, bool TAIL>
+// ORD: combine in the reference CPU's order (bit-identical results, see dot_ord / chain): each
+// 64-item chunk of a row leaves its per-item lane sums in the wave's LDS scratch, then lane
+// (column c, CPU lane l) runs the reference's sequential fma chain over the chunk.
+template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD>
 __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int NB = PD + 1;  // ring slots
@@ -261,6 +422,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     const int nitems = (int) (K / F::ITEM);
     const int ncols = g.ncols;
     const lds_act act = lds_carve<F::QKA>(lds, NC, K);
+    uint32_t * scr = (uint32_t *) (lds + ord_offset(lds_bytes<F::QKA>(NC, K))) + wave * NC * kOrdCS;
 
     // 32-bit row bookkeeping (N < 2^31): scalar compares, no 64-bit VGPR temporaries in the loop
     const int Nr = (int) g.N;
@@ -323,6 +485,40 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
             const int k = k0 + u;
             if (k >= nrows) break;  // wave-uniform
             prefetch(ring[(u + PD) % NB], k + PD < klast ? k + PD : klast);
+            const int row = row_begin + 4 * k + wave;
+            if constexpr (ORD) {
+                const int cl = lane >> 3, ll = lane & 7;
+                float A = 0.0f, M = 0.0f;
+                auto chunk_done = [&](int base) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_wave_barrier();
+                    if (cl < ncols) F::chain(scr + cl * kOrdCS, ll, min(64, nitems - base), A, M);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_wave_barrier();
+                };
+#pragma unroll
+                for (int i = 0; i < IPL; i++) {
+                    if (64 * i >= nitems) break;  // wave-uniform
+                    const int item = lane + 64 * i;
+                    if (item < nitems) F::template dot_ord<NC>(ring[u][i], item, lane, act, K, ncols, scr);
+                    chunk_done(64 * i);
+                }
+                if constexpr (TAIL) {
+                    const uint8_t * wr = wrow_of(k);
+                    for (int base = 64 * IPL; base < nitems; base += 64) {
+                        const int item = base + lane;
+                        if (item < nitems) {
+                            typename F::Regs rr;
+                            F::load(rr, wr, item);
+                            F::template dot_ord<NC>(rr, item, lane, act, K, ncols, scr);
+                        }
+                        chunk_done(base);
+                    }
+                }
+                const float v = F::finish(A, M);
+                if (ll == 0 && cl < ncols) *(float *) ((char *) dst + cl * g.ycol + row * sizeof(float)) = v;
+                continue;
+            }
             float acc[NC];
 #pragma unroll
             for (int c = 0; c < NC; c++) acc[c] = 0.0f;
@@ -341,7 +537,6 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                     F::template dot<NC>(rr, item, act, K, ncols, acc);
                 }
             }
-            const int row = row_begin + 4 * k + wave;
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 const float v = mi_wave_sum_u(acc[c]);
@@ -369,10 +564,18 @@ int resident_blocks(const void * fn, size_t lds) {
     return n;
 }
 
-template <class F, int NC, int PD, int IPL, bool TAIL>
+template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD>
 void launch_one(mi_mmv_group g, hipStream_t s) {
-    const size_t lds = lds_bytes<F::QKA>(NC, g.K);
-    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL, TAIL>;
+    const size_t act = lds_bytes<F::QKA>(NC, g.K);
+    const size_t lds = ORD ? ord_offset(act) + ord_bytes(NC) : act;
+    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL, TAIL, ORD>;
+    if (lds > 64 * 1024) {
+        static bool attr_set = false;  // per instance
+        if (!attr_set) {
+            (void) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_set = true;
+        }
+    }
     const int target = g_mi_tuning.mmv_blocks > 0 ? g_mi_tuning.mmv_blocks : resident_blocks(fn, lds);
     int bpm = target / g.n;
     if (bpm < 1) bpm = 1;
@@ -380,40 +583,46 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
     rows = (rows + 3) / 4 * 4;
     g.rows_per_block = rows;
     g.blocks_per_member = (int) ((g.N + rows - 1) / rows);
-    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL, TAIL>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds, s,
-                       g);
+    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL, TAIL, ORD>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds,
+                       s, g);
 }
 
-template <class F, int NC, int PD, int IPL>
+template <class F, int NC, int PD, int IPL, bool ORD>
 void launch_tail(const mi_mmv_group & g, hipStream_t s) {
-    if (g.K / F::ITEM > 64 * IPL) launch_one<F, NC, PD, IPL, true>(g, s);
-    else launch_one<F, NC, PD, IPL, false>(g, s);
+    if (g.K / F::ITEM > 64 * IPL) launch_one<F, NC, PD, IPL, true, ORD>(g, s);
+    else launch_one<F, NC, PD, IPL, false, ORD>(g, s);
 }
 
-template <class F, int NC>
+template <class F, int NC, bool ORD>
 void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
     const int items = (int) (g.K / F::ITEM);
     if (items > 64) {
         // two items per lane in the ring (Q4_0 / Q8_0 at K=4096)
-        if (variant / 10 == 1) launch_tail<F, NC, 1, 2>(g, s);
-        else launch_tail<F, NC, 2, 2>(g, s);
+        if (variant / 10 == 1) launch_tail<F, NC, 1, 2, ORD>(g, s);
+        else launch_tail<F, NC, 2, 2, ORD>(g, s);
         return;
     }
     switch (variant / 10) {
-        case 1: launch_one<F, NC, 1, 1, false>(g, s); break;
-        case 3: launch_one<F, NC, 3, 1, false>(g, s); break;
-        default: launch_one<F, NC, 2, 1, false>(g, s); break;
+        case 1: launch_one<F, NC, 1, 1, false, ORD>(g, s); break;
+        case 3: launch_one<F, NC, 3, 1, false, ORD>(g, s); break;
+        default: launch_one<F, NC, 2, 1, false, ORD>(g, s); break;
+    }
+}
+
+template <class F, bool ORD>
+void launch_stream_nc(const mi_mmv_group & g, int variant, hipStream_t s) {
+    switch (g.ncols) {
+        case 1: launch_stream<F, 1, ORD>(g, variant, s); break;
+        case 2: launch_stream<F, 2, ORD>(g, variant, s); break;
+        case 3: case 4: launch_stream<F, 4, ORD>(g, variant, s); break;
+        default: launch_stream<F, 8, ORD>(g, variant, s); break;
     }
 }
 
 template <class F>
-void launch_stream_nc(const mi_mmv_group & g, int variant, hipStream_t s) {
-    switch (g.ncols) {
-        case 1: launch_stream<F, 1>(g, variant, s); break;
-        case 2: launch_stream<F, 2>(g, variant, s); break;
-        case 3: case 4: launch_stream<F, 4>(g, variant, s); break;
-        default: launch_stream<F, 8>(g, variant, s); break;
-    }
+void launch_stream_ord(const mi_mmv_group & g, int variant, hipStream_t s) {
+    if (g_mi_tuning.mmv_order) launch_stream_nc<F, true>(g, variant, s);
+    else launch_stream_nc<F, false>(g, variant, s);
 }
 
 int qka_of(int type) { return (type == 12 || type == 13) ? 256 : 32; }
@@ -428,21 +637,40 @@ size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols) {
 bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols) {
     if (type != 12 && type != 13 && type != 2 && type != 8) return false;
     if (ncols < 1 || ncols > 8 || K % 256 != 0) return false;
-    return mi_mmv_fused_lds_bytes(type, K, ncols) <= 64 * 1024;
+    // more than 4 columns whose activations do not fit run as two launches of <= 4 columns
+    return mi_mmv_fused_lds_bytes(type, K, ncols < 4 ? ncols : 4) <= 64 * 1024;  // + ord_bytes(4)
 }
 
 
 
+static void mi_mul_mat_q_fused_launch(mi_mmv_group & g, hipStream_t s);
+
 void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s) {
+    if (g.ncols > 4 && mi_mmv_fused_lds_bytes(g.type, g.K, g.ncols) > 64 * 1024) {
+        for (int c0 = 0; c0 < g.ncols; c0 += 4) {
+            mi_mmv_group h = g;
+            h.ncols = g.ncols - c0 < 4 ? g.ncols - c0 : 4;
+            for (int m = 0; m < g.n; m++) {
+                h.m[m].X = g.m[m].X + (size_t) c0 * g.xcol;
+                h.m[m].dst = (float *) ((char *) g.m[m].dst + (size_t) c0 * g.ycol);
+            }
+            mi_mul_mat_q_fused_launch(h, s);
+        }
+        return;
+    }
+    mi_mul_mat_q_fused_launch(g, s);
+}
+
+static void mi_mul_mat_q_fused_launch(mi_mmv_group & g, hipStream_t s) {
     // variant 0 = per-type default, from interleaved A/B runs on MI355X (tools/mmv_tune.py):
     // prefetch depth 2 for Q4_K / Q8_0, depth 1 for Q5_K / Q4_0 (fewer VGPRs, more waves)
     int variant = g_mi_tuning.mmv_variant;
     if (variant == 0) variant = (g.type == 12 || g.type == 8) ? 21 : 11;
     switch (g.type) {
-        case 12: launch_stream_nc<FmtKQ<false>>(g, variant, s); break;
-        case 13: launch_stream_nc<FmtKQ<true>>(g, variant, s); break;
-        case 2: launch_stream_nc<FmtQ0<false>>(g, variant, s); break;
-        case 8: launch_stream_nc<FmtQ0<true>>(g, variant, s); break;
+        case 12: launch_stream_ord<FmtKQ<false>>(g, variant, s); break;
+        case 13: launch_stream_ord<FmtKQ<true>>(g, variant, s); break;
+        case 2: launch_stream_ord<FmtQ0<false>>(g, variant, s); break;
+        case 8: launch_stream_ord<FmtQ0<true>>(g, variant, s); break;
         default: break;
     }
 }

@@ -2,7 +2,7 @@
 //
 // All are memory- or launch-bound. Each follows the reference CPU forward's rounding sequence so
 // that results are bit-identical where the CPU order is reproducible:
-//   get_rows   src/ggml.c:12920 (f16) / :13006 (f32)       -- exact
+//   get_rows   src/ggml.c:12920 (f16) / :13006 (f32) / :12874 (Q4_0, Q8_0, Q4_K, Q5_K) -- exact
 //   add / mul  src/ggml.c:8568 / :9687 (broadcast src1)      -- exact
 //   scale      src/ggml.c:12637                              -- exact
 //   norm       src/ggml.c:11353-11406 (double sums)          -- sums in double, then the same f32 ops
@@ -134,6 +134,59 @@ __global__ __launch_bounds__(256) void k_get_rows(mi_tensor_desc d, mi_tensor_de
         const int32_t i01 = *(const int32_t *) (idx.data + i10 * idx.nb[0] + i11 * idx.nb[1] + i12 * idx.nb[2]);
         const float v = ld_f(a.data + c * a.nb[0] + (size_t) i01 * a.nb[1] + i11 * a.nb[2] + i12 * a.nb[3], a.type);
         st_f(d.data + c * d.nb[0] + i10 * d.nb[1] + i11 * d.nb[2] + i12 * d.nb[3], d.type, v);
+    }
+}
+
+// GET_ROWS of a quantized src0 (ggml_compute_forward_get_rows_q, src/ggml.c:12874-12918): each
+// output element is the reference dequantize_row_* value, as its x86 build computes it --
+// Q4_0 ((q & 15) - 8) * d (src/ggml-quants.c:980-998), Q8_0 q * d (:1074-1088), Q4_K / Q5_K
+// fma(d * sc, q, -(dmin * m)) (:2181-2218, :2464-2507; the -mfma build emits vfmsub132ps there).
+template <int TYPE>
+__device__ __forceinline__ float dequant_elem(const uint8_t * row, int64_t c) {
+    if constexpr (TYPE == 2 || TYPE == 8) {  // Q4_0 (18 B) / Q8_0 (34 B) blocks of 32
+        constexpr int BS = TYPE == 2 ? 18 : 34;
+        const uint8_t * blk = row + (c >> 5) * BS;
+        const int j = (int) (c & 31);
+        uint16_t dh;
+        __builtin_memcpy(&dh, blk, 2);
+        const float d = mi_h2f(dh);
+        if constexpr (TYPE == 2) {
+            const uint8_t b = blk[2 + (j & 15)];
+            return (float) ((j < 16 ? (b & 0x0F) : (b >> 4)) - 8) * d;
+        } else {
+            return (float) (int8_t) blk[2 + j] * d;
+        }
+    } else {  // Q4_K (144 B) / Q5_K (176 B) superblocks of 256
+        constexpr bool Q5 = TYPE == 13;
+        const uint8_t * blk = row + (c >> 8) * (Q5 ? 176 : 144);
+        const int e = (int) (c & 255), g = e >> 6, l = e & 31, hi = (e >> 5) & 1;
+        uint16_t dh, mh;
+        __builtin_memcpy(&dh, blk, 2);
+        __builtin_memcpy(&mh, blk + 2, 2);
+        uint32_t sc3[3];
+        __builtin_memcpy(sc3, blk + 4, 12);
+        int sc, m;
+        mi_scale_min_k4(2 * g + hi, sc3[0], sc3[1], sc3[2], sc, m);
+        const float d1 = mul_rn(mi_h2f(dh), (float) sc), m1 = mul_rn(mi_h2f(mh), (float) m);
+        const uint8_t * qs = blk + (Q5 ? 48 : 16) + 32 * g;
+        int q = hi ? (qs[l] >> 4) : (qs[l] & 0x0F);
+        if constexpr (Q5) q += (blk[16 + l] >> (2 * g + hi)) & 1 ? 16 : 0;
+        return __fmaf_rn(d1, (float) q, -m1);
+    }
+}
+
+template <int TYPE>
+__global__ __launch_bounds__(256) void k_get_rows_q(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc idx, int64_t n) {
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        const int64_t c = i % d.ne[0];
+        int64_t r = i / d.ne[0];
+        const int64_t i10 = r % idx.ne[0];
+        r /= idx.ne[0];
+        const int64_t i11 = r % idx.ne[1];
+        const int64_t i12 = r / idx.ne[1];
+        const int32_t i01 = *(const int32_t *) (idx.data + i10 * idx.nb[0] + i11 * idx.nb[1] + i12 * idx.nb[2]);
+        const uint8_t * row = (const uint8_t *) a.data + (size_t) i01 * a.nb[1] + i11 * a.nb[2] + i12 * a.nb[3];
+        st_f(d.data + c * d.nb[0] + i10 * d.nb[1] + i11 * d.nb[2] + i12 * d.nb[3], d.type, dequant_elem<TYPE>(row, c));
     }
 }
 
@@ -347,7 +400,13 @@ void mi_op_cpy(const mi_tensor_desc & d, const mi_tensor_desc & a, hipStream_t s
 
 void mi_op_get_rows(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & idx, hipStream_t s) {
     const int64_t n = d.ne[0] * d.ne[1] * d.ne[2] * d.ne[3];
-    hipLaunchKernelGGL(k_get_rows, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n);
+    switch (a.type) {
+        case 2: hipLaunchKernelGGL(k_get_rows_q<2>, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n); break;
+        case 8: hipLaunchKernelGGL(k_get_rows_q<8>, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n); break;
+        case 12: hipLaunchKernelGGL(k_get_rows_q<12>, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n); break;
+        case 13: hipLaunchKernelGGL(k_get_rows_q<13>, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n); break;
+        default: hipLaunchKernelGGL(k_get_rows, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n); break;
+    }
 }
 
 void mi_op_diag_mask(const mi_tensor_desc & d, const mi_tensor_desc & a, int n_past, float value, hipStream_t s) {

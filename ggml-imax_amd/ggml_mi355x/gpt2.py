@@ -129,6 +129,66 @@ def ensure_model(path: str | None = None, seed: int = 117) -> str:
     return path
 
 
+# examples/gpt-2/quantize.cpp:114-128 (tensors quantized); names as common-ggml.cpp:6-17 spells them
+QUANT_TENSORS = [r"model/wte", r"model/lm_head", r"model/h.*/attn/c_attn/w", r"model/h.*/attn/c_proj/w",
+                 r"model/h.*/mlp/c_fc/w", r"model/h.*/mlp/c_proj/w"]
+FTYPES = {"q4_0": (2, G.GGML_TYPE_Q4_0), "q8_0": (7, G.GGML_TYPE_Q8_0), "q4_k": (12, G.GGML_TYPE_Q4_K),
+          "q5_k": (13, G.GGML_TYPE_Q5_K)}
+GGML_QNT_VERSION, GGML_QNT_VERSION_FACTOR = 2, 1000
+
+
+def quantize_model(lib: G.Lib, src: str, dst: str, qtype: str) -> str:
+    """The reference's examples/gpt-2/quantize.cpp on a legacy GPT-2 file (common-ggml.cpp:19-236
+    ggml_common_quantize_0): the header's ftype becomes the target (+ GGML_QNT_VERSION * 1000), the
+    2-D tensors named in QUANT_TENSORS are converted to f32 and quantized row by row with
+    ggml_quantize_chunk (imatrix = NULL), everything else is copied."""
+    import re
+    ftype, ttype_q = FTYPES[qtype.lower()]
+    pats = [re.compile(p) for p in QUANT_TENSORS]
+    tmp = dst + ".tmp"
+    os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
+    with open(src, "rb") as fi, open(tmp, "wb") as fo:
+        hdr = struct.unpack("7i", fi.read(28))  # magic, n_vocab, n_ctx, n_embd, n_head, n_layer, ftype
+        fo.write(struct.pack("7i", *hdr[:6], ftype + GGML_QNT_VERSION * GGML_QNT_VERSION_FACTOR))
+        n_vocab = struct.unpack("i", fi.read(4))[0]
+        fo.write(struct.pack("i", n_vocab))
+        for _ in range(n_vocab):
+            (ln,) = struct.unpack("i", fi.read(4))
+            fo.write(struct.pack("i", ln))
+            fo.write(fi.read(ln))
+        while True:
+            head = fi.read(12)
+            if len(head) < 12:
+                break
+            n_dims, name_len, ttype = struct.unpack("3i", head)
+            ne = list(struct.unpack(f"{n_dims}i", fi.read(4 * n_dims)))
+            name = fi.read(name_len)
+            nel = int(np.prod(ne))
+            quant = n_dims == 2 and any(p.fullmatch(name.decode()) for p in pats)
+            if quant:
+                assert ttype in (0, 1), f"{name!r}: cannot quantize type {ttype}"
+                data = np.fromfile(fi, dtype=np.float16 if ttype == 1 else np.float32, count=nel).astype(np.float32)
+                out = np.empty(G.row_size(ttype_q, ne[0]) * (nel // ne[0]), np.uint8)
+                lib.ggml_quantize_chunk(ttype_q, data.ctypes.data, out.ctypes.data, 0, nel // ne[0], ne[0], None)
+                ttype = ttype_q
+            else:
+                out = np.fromfile(fi, dtype=np.uint8, count=nel * (4 if ttype == 0 else 2))
+            fo.write(struct.pack("3i", n_dims, name_len, ttype))
+            fo.write(struct.pack(f"{n_dims}i", *ne))
+            fo.write(name)
+            out.tofile(fo)
+    os.replace(tmp, dst)
+    return dst
+
+
+def ensure_quantized_model(lib: G.Lib, qtype: str, path: str | None = None) -> str:
+    base = ensure_model()
+    path = path or base.replace("-f16.bin", f"-{qtype.lower()}.bin")
+    if not os.path.exists(path):
+        quantize_model(lib, base, path, qtype)
+    return path
+
+
 class Model:
     """One loaded GPT-2 on a backend (gpt2_model_load); eval() returns logits as numpy."""
 

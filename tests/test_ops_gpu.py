@@ -170,6 +170,40 @@ def test_get_rows_plus_add_exact(libs, src_type):
     assert_exact(a, b, "get_rows+add")
 
 
+@pytest.mark.parametrize("qtype", [G.GGML_TYPE_Q4_0, G.GGML_TYPE_Q8_0, G.GGML_TYPE_Q4_K, G.GGML_TYPE_Q5_K])
+def test_get_rows_quantized_exact(libs, qtype):
+    """get_rows of a quantized wte (a quantized GPT-2's embedding, ggml.c:12874-12918 dequantizes the
+    picked rows with the type's to_float) + get_rows(wpe f32): identical bits."""
+    import pyoracle as orc
+    E, V, N = 768, 997, 9
+    wq = orc.quantize(qtype, rnd(16, E * V, 0.1), E)
+    p = rnd(7, E * 64, 0.1)
+    ids = np.array([5, 996, 0, 17, 17, 300, 2, 9, 500], dtype=np.int32)
+    pos = np.arange(N, dtype=np.int32) + 3
+
+    def build(L, c):
+        wt = L.ggml_new_tensor_2d(c, qtype, E, V)
+        pt = L.ggml_new_tensor_2d(c, F32, E, 64)
+        it = L.ggml_new_tensor_1d(c, I32, N)
+        qt = L.ggml_new_tensor_1d(c, I32, N)
+        out = L.ggml_add(c, L.ggml_get_rows(c, wt, it), L.ggml_get_rows(c, pt, qt))
+        return [(wt, wq), (pt, p), (it, ids), (qt, pos)], out
+
+    a, b = both(libs, build)
+    assert_exact(a, b, f"get_rows(type {qtype})+add")
+    # and the picked rows alone against the oracle's dequantization
+    rt, be, _, _ = libs
+
+    def build_rows(c):
+        wt = rt.ggml_new_tensor_2d(c, qtype, E, V)
+        it = rt.ggml_new_tensor_1d(c, I32, N)
+        return [(wt, wq), (it, ids)], rt.ggml_get_rows(c, wt, it)
+
+    rows = G.graph_once(rt, be, build_rows).reshape(N, E)
+    deq = orc.dequantize(qtype, wq, E * V).reshape(V, E)[ids]
+    assert np.array_equal(rows.view(np.uint32), deq.view(np.uint32))
+
+
 def test_layernorm_affine_exact(libs):
     """norm -> mul(g) -> add(b) with row broadcast, as every GPT-2 layer norm."""
     E, N = 768, 6
