@@ -117,13 +117,14 @@ def _cpu_model():
 GPT2_PROMPT = "Once upon a time the cat sat on the mat and the dog ran away from the big red house"
 
 
-def gpt2_bench(lib, backend, n_decode=128, n_batch=8):
+def gpt2_bench(lib, backend, n_decode=128, n_batch=8, path=None, label="GPT-2-117M f16 (synthetic seeded weights, 239.08 MB)",
+               parity="decode-path logits bit-identical to the reference CPU (tests/test_gpt2.py)"):
     """BASELINE config 4: GPT-2-117M f16 (synthetic seeded weights, legacy ggml file) on MI355X.
     Prompt in n_batch chunks, then n_decode greedy single-token steps, logits read back each step
     (as examples/gpt-2/main-backend.cpp's gpt2_eval does). Returns decode tokens/s and the
     reference program's ms/token definition (predict time / n_past, prompt tokens included)."""
     from ggml_mi355x import gpt2
-    path = gpt2.ensure_model()
+    path = path or gpt2.ensure_model()
     m = gpt2.Model(lib, path, backend, n_ctx=1024, n_batch=n_batch)
     try:
         toks = m.tokenize(GPT2_PROMPT)
@@ -146,18 +147,35 @@ def gpt2_bench(lib, backend, n_decode=128, n_batch=8):
         t_dec = time.perf_counter() - t0
         st = m.stats()
         t_pred = t_prompt + t_dec
-        return {"model": "GPT-2-117M f16 (synthetic seeded weights, 239.08 MB)", "decode_tokens_per_s": round(n_decode / t_dec, 1),
+        return {"model": label, "decode_tokens_per_s": round(n_decode / t_dec, 1),
                 "ms_per_decode_token": round(t_dec / n_decode * 1e3, 4),
                 "prompt_tokens": len(toks), "prompt_tokens_per_s": round(len(toks) / t_prompt, 1),
                 "ms_per_token_reference_definition": round(t_pred / n_past * 1e3, 4),
                 "graph_nodes": st["nodes"], "kernel_launches_per_token": lib.ggml_backend_mi355x_last_launch_count(backend),
                 "host_us_per_token": {k: st[k] for k in ("us_build", "us_alloc", "us_inputs")},
-                "parity": "decode-path logits bit-identical to the reference CPU (tests/test_gpt2.py)"}
+                "parity": parity}
     finally:
         m.free()
 
 
-def gpt2_cpu_baseline(threads, n_predict=64):
+def gpt2_q4k_bench(lib, backend, n_decode):
+    """The same decode loop on the model quantized to Q4_K by gpt2.quantize_model (byte-identical
+    to examples/gpt-2/quantize.cpp): default (tree-order) GEMV, and mmv_order=1 (the reference
+    CPU's combination order: bit-identical logits) for the cost of exactness."""
+    from ggml_mi355x import gpt2
+    path = gpt2.ensure_quantized_model(lib, "q4_k")
+    r = gpt2_bench(lib, backend, n_decode, path=path, label="GPT-2-117M Q4_K (quantize.cpp q4_k of the synthetic model)",
+                   parity="default order: logits within the reference's own 1-ulp sensitivity (tests/test_gpt2.py)")
+    lib.ggml_backend_mi355x_set_tuning(b"mmv_order", 1)
+    try:
+        ro = gpt2_bench(lib, backend, n_decode, path=path, label="same, mmv_order=1", parity="logits bit-identical")
+    finally:
+        lib.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
+    r["mmv_order_1"] = {k: ro[k] for k in ("decode_tokens_per_s", "ms_per_decode_token", "parity")}
+    return r
+
+
+def gpt2_cpu_baseline(threads, n_predict=64, path=None):
     """The reference's own examples/gpt-2/main-backend.cpp (oracle/_ref/gpt-2-backend, built from
     the reference sources) on the same synthetic model, CPU backend: its printed ms per token."""
     import re
@@ -166,7 +184,7 @@ def gpt2_cpu_baseline(threads, n_predict=64):
     if not os.path.exists(exe):
         return None
     from ggml_mi355x import gpt2
-    p = subprocess.run([exe, "-m", gpt2.ensure_model(), "-p", GPT2_PROMPT, "-n", str(n_predict), "-s", "1", "-t", str(threads)],
+    p = subprocess.run([exe, "-m", path or gpt2.ensure_model(), "-p", GPT2_PROMPT, "-n", str(n_predict), "-s", "1", "-t", str(threads)],
                        capture_output=True, text=True, timeout=600)
     mt = re.search(r"predict time =\s*([\d.]+) ms /\s*([\d.]+) ms per token", p.stdout)
     if p.returncode != 0 or not mt:
@@ -478,11 +496,16 @@ def main():
     if rank == 0 and world == 1 and not args.no_gpt2:
         # BASELINE config 4 (the metric's "+ GPT-2 tokens/s" half)
         result["gpt2"] = gpt2_bench(lib, backend, args.gpt2_tokens)
+        result["gpt2_q4_k"] = gpt2_q4k_bench(lib, backend, args.gpt2_tokens)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(t, K, N, B, args.cpu_seconds)
+        threads = int(os.environ.get("BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
         if "gpt2" in result:
-            result["gpt2"]["cpu_baseline"] = gpt2_cpu_baseline(int(os.environ.get("BENCH_CPU_THREADS", min(16, os.cpu_count() or 1))))
+            result["gpt2"]["cpu_baseline"] = gpt2_cpu_baseline(threads)
+        if "gpt2_q4_k" in result:
+            from ggml_mi355x import gpt2
+            result["gpt2_q4_k"]["cpu_baseline"] = gpt2_cpu_baseline(threads, path=gpt2.ensure_quantized_model(lib, "q4_k"))
 
     wl.free()
     lib.ggml_backend_free(backend)
