@@ -56,6 +56,10 @@ class ggml_init_params(Structure):
     _fields_ = [("mem_size", c_size_t), ("mem_buffer", c_void_p), ("no_alloc", c_bool)]
 
 
+class gguf_init_params(Structure):
+    _fields_ = [("no_alloc", c_bool), ("ctx", POINTER(c_void_p))]
+
+
 class ggml_cgraph(Structure):
     _fields_ = [("size", c_int), ("n_nodes", c_int), ("n_leafs", c_int),
                 ("nodes", POINTER(POINTER(ggml_tensor))), ("grads", c_void_p), ("leafs", POINTER(POINTER(ggml_tensor))),
@@ -115,6 +119,66 @@ _SIGS = {
     "ggml_quantize_chunk": ([c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p], c_size_t),
     "ggml_fp32_to_fp16": ([c_float], ctypes.c_uint16),
     "ggml_fp16_to_fp32": ([ctypes.c_uint16], c_float),
+    # GGUF (include/ggml/ggml.h:2247-2380)
+    "gguf_init_empty": ([], c_void_p),
+    "gguf_init_from_file": ([c_char_p, gguf_init_params], c_void_p),
+    "gguf_free": ([c_void_p], None),
+    "gguf_type_name": ([c_int], c_char_p),
+    "gguf_get_version": ([c_void_p], c_int),
+    "gguf_get_alignment": ([c_void_p], c_size_t),
+    "gguf_get_data_offset": ([c_void_p], c_size_t),
+    "gguf_get_data": ([c_void_p], c_void_p),
+    "gguf_get_n_kv": ([c_void_p], c_int),
+    "gguf_find_key": ([c_void_p, c_char_p], c_int),
+    "gguf_get_key": ([c_void_p, c_int], c_char_p),
+    "gguf_get_kv_type": ([c_void_p, c_int], c_int),
+    "gguf_get_arr_type": ([c_void_p, c_int], c_int),
+    "gguf_get_val_u8": ([c_void_p, c_int], ctypes.c_uint8),
+    "gguf_get_val_i8": ([c_void_p, c_int], ctypes.c_int8),
+    "gguf_get_val_u16": ([c_void_p, c_int], ctypes.c_uint16),
+    "gguf_get_val_i16": ([c_void_p, c_int], ctypes.c_int16),
+    "gguf_get_val_u32": ([c_void_p, c_int], ctypes.c_uint32),
+    "gguf_get_val_i32": ([c_void_p, c_int], ctypes.c_int32),
+    "gguf_get_val_f32": ([c_void_p, c_int], c_float),
+    "gguf_get_val_u64": ([c_void_p, c_int], ctypes.c_uint64),
+    "gguf_get_val_i64": ([c_void_p, c_int], c_int64),
+    "gguf_get_val_f64": ([c_void_p, c_int], ctypes.c_double),
+    "gguf_get_val_bool": ([c_void_p, c_int], c_bool),
+    "gguf_get_val_str": ([c_void_p, c_int], c_char_p),
+    "gguf_get_val_data": ([c_void_p, c_int], c_void_p),
+    "gguf_get_arr_n": ([c_void_p, c_int], c_int),
+    "gguf_get_arr_data": ([c_void_p, c_int], c_void_p),
+    "gguf_get_arr_str": ([c_void_p, c_int, c_int], c_char_p),
+    "gguf_get_n_tensors": ([c_void_p], c_int),
+    "gguf_find_tensor": ([c_void_p, c_char_p], c_int),
+    "gguf_get_tensor_offset": ([c_void_p, c_int], c_size_t),
+    "gguf_get_tensor_name": ([c_void_p, c_int], c_char_p),
+    "gguf_get_tensor_type": ([c_void_p, c_int], c_int),
+    "gguf_remove_key": ([c_void_p, c_char_p], None),
+    "gguf_set_val_u8": ([c_void_p, c_char_p, ctypes.c_uint8], None),
+    "gguf_set_val_i8": ([c_void_p, c_char_p, ctypes.c_int8], None),
+    "gguf_set_val_u16": ([c_void_p, c_char_p, ctypes.c_uint16], None),
+    "gguf_set_val_i16": ([c_void_p, c_char_p, ctypes.c_int16], None),
+    "gguf_set_val_u32": ([c_void_p, c_char_p, ctypes.c_uint32], None),
+    "gguf_set_val_i32": ([c_void_p, c_char_p, ctypes.c_int32], None),
+    "gguf_set_val_f32": ([c_void_p, c_char_p, c_float], None),
+    "gguf_set_val_u64": ([c_void_p, c_char_p, ctypes.c_uint64], None),
+    "gguf_set_val_i64": ([c_void_p, c_char_p, c_int64], None),
+    "gguf_set_val_f64": ([c_void_p, c_char_p, ctypes.c_double], None),
+    "gguf_set_val_bool": ([c_void_p, c_char_p, c_bool], None),
+    "gguf_set_val_str": ([c_void_p, c_char_p, c_char_p], None),
+    "gguf_set_arr_data": ([c_void_p, c_char_p, c_int, c_void_p, c_int], None),
+    "gguf_set_arr_str": ([c_void_p, c_char_p, POINTER(c_char_p), c_int], None),
+    "gguf_set_kv": ([c_void_p, c_void_p], None),
+    "gguf_add_tensor": ([c_void_p, T], None),
+    "gguf_set_tensor_type": ([c_void_p, c_char_p, c_int], None),
+    "gguf_set_tensor_data": ([c_void_p, c_char_p, c_void_p, c_size_t], None),
+    "gguf_write_to_file": ([c_void_p, c_char_p, c_bool], None),
+    "gguf_get_meta_size": ([c_void_p], c_size_t),
+    "gguf_get_meta_data": ([c_void_p, c_void_p], None),
+    "ggml_get_first_tensor": ([c_void_p], T),
+    "ggml_get_next_tensor": ([c_void_p, T], T),
+    "ggml_get_tensor": ([c_void_p, c_char_p], T),
     # backend
     "ggml_backend_name": ([c_void_p], c_char_p),
     "ggml_backend_free": ([c_void_p], None),
