@@ -74,6 +74,10 @@ struct mi_mmv_group {
     size_t nb01;            // weight row stride (bytes)
     size_t xcol;            // src1 column stride (bytes)
     size_t ycol;            // dst column stride (bytes)
+    int abl = 0;            // timing ablation of the reference-order chain (mmv_order 2: no chain; results invalid)
+    int ord_rows = 0;       // reference order: rows per chain pass (0: one pass per 64-item chunk of a row)
+    int ord_cs = 0;         // reference order: scratch words per (row, column)
+    int ord_s = 0;          // reference order: Q4_0/Q8_0 lane-row stride in the scratch
     mi_mmv_member m[kMiMaxMembers];
 };
 bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols);

@@ -59,12 +59,8 @@ __host__ __device__ constexpr size_t lds_bytes(int NC, int64_t K) {
     return (size_t) NC * (K + (K / QKA) * 4 + (K / 32) * 2);
 }
 
-// CPU-order combination scratch, after the activations: per wave and column kOrdCS words
-// (Q4_0/Q8_0: 9 rows of 68 for one 64-block chunk; K-quants: 16 superblock entries of 16);
-// kOrdCS = 8 (mod 32) keeps the eight columns' chain reads on distinct banks
-constexpr int kOrdCS = 648;
+// reference-order scratch (per wave: rows x columns x F::ord_words), after the activations
 __host__ __device__ constexpr size_t ord_offset(size_t act) { return (act + 15) & ~(size_t) 15; }
-__host__ __device__ constexpr size_t ord_bytes(int NC) { return (size_t) 4 * NC * kOrdCS * 4; }
 
 // one 256-element slice (four floats per lane) of column c into LDS
 template <int QKA>
@@ -202,7 +198,7 @@ struct FmtKQ {
     // [12] d = y.d * x.d, [13] dmin = -(y.d * x.dmin).
     template <int NC>
     __device__ static __forceinline__ void dot_ord(const Regs & r, int item, int slot, const lds_act & a, int64_t K, int ncols,
-                                                   uint32_t * scr) {
+                                                   uint32_t * scr, int cs, int) {
         const int s = item >> 2, j = item & 3;
         const uint32_t q[8] = {r.qa.x, r.qa.y, r.qa.z, r.qa.w, r.qb.x, r.qb.y, r.qb.z, r.qb.w};
         uint32_t qlo[8], qhi[8];
@@ -257,12 +253,13 @@ struct FmtKQ {
                 pm += mi_dpp<MI_DPP_QP_1032>(0, pm);
                 pm += mi_dpp<MI_DPP_QP_2301>(0, pm);
             }
-            uint32_t * e = scr + c * kOrdCS + (slot >> 2) * 16;
-            // lane j stores sums 2j and 2j+1 (all four lanes hold all eight after the quad sums)
+            uint32_t * e = scr + c * cs + (slot >> 2) * 16;
+            // lane j stores sums 2j and 2j+1 (all four lanes hold all eight after the quad sums),
+            // as floats (exact: |sum| < 2^24), i.e. the reference's _mm256_cvtepi32_ps
             const int w0 = j == 0 ? v[0] : j == 1 ? v[2] : j == 2 ? v[4] : v[6];
             const int w1 = j == 0 ? v[1] : j == 1 ? v[3] : j == 2 ? v[5] : v[7];
-            *(uint2 *) (e + 2 * j) = make_uint2((uint32_t) w0, (uint32_t) w1);
-            if (!Q5 || j == 0) e[8 + j] = (uint32_t) pm;
+            *(uint2 *) (e + 2 * j) = make_uint2(__float_as_uint((float) w0), __float_as_uint((float) w1));
+            if (!Q5 || j == 0) e[8 + j] = __float_as_uint((float) pm);
             const float yd = a.d[c * (K / 256) + s];
             if (j == 2) e[12] = __float_as_uint(yd * dw);
             if (j == 3) e[13] = __float_as_uint(-(yd * dmw));
@@ -272,13 +269,19 @@ struct FmtKQ {
     // _mm256_fmadd_ps) and the mins accumulator: Q4_K four lanes acc_m[k] = fma(dmin, prod[k],
     // acc_m[k]) (_mm_fmadd_ps), Q5_K one scalar summs += dmin * hsum(prod) (contracted by the
     // reference's -mfma build)
-    __device__ static __forceinline__ void chain(const uint32_t * scr, int l, int n_items, float & A, float & M) {
+    __device__ static __forceinline__ void chain(const uint32_t * scr, int l, int n_items, int, float & A, float & M) {
+        const float * e = (const float *) scr;
         const int nsb = n_items >> 2;
-        for (int sb = 0; sb < nsb; sb++) {
-            const uint32_t * e = scr + sb * 16;
-            A = fmaf(__uint_as_float(e[12]), (float) (int) e[l], A);
-            M = fmaf(__uint_as_float(e[13]), (float) (int) e[8 + (Q5 ? 0 : (l & 3))], M);
+        const int lm = 8 + (Q5 ? 0 : (l & 3));
+        for (int sb = 0; sb < nsb; sb++, e += 16) {
+            A = fmaf(e[12], e[l], A);
+            M = fmaf(e[13], e[lm], M);
         }
+    }
+    // scratch words per (row, column): one 16-word entry per superblock (+8: bank spread)
+    static int ord_words(int nitems, int & stride) {
+        stride = 0;
+        return 16 * (nitems / 4) + 8;
     }
     __device__ static __forceinline__ float finish(float A, float M) {
         float z = A + __shfl_xor(A, 4, 8);
@@ -349,7 +352,7 @@ struct FmtQ0 {
     // d = x.d * y.d, stored transposed: scratch [l][slot] (row stride 68 words), d at [8][slot].
     template <int NC>
     __device__ static __forceinline__ void dot_ord(const Regs & r, int item, int slot, const lds_act & a, int64_t K, int ncols,
-                                                   uint32_t * scr) {
+                                                   uint32_t * scr, int cs, int S) {
         uint32_t t[NQ];
 #pragma unroll
         for (int i = 0; i < NQ; i++) t[i] = r.off ? r.w[i + 1] : __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], 2);
@@ -361,7 +364,7 @@ struct FmtQ0 {
             const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 32);
             const int4 a0 = p[0], a1 = p[1];
             const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            uint32_t * e = scr + c * kOrdCS + slot;
+            uint32_t * e = scr + c * cs + slot;
 #pragma unroll
             for (int l = 0; l < 8; l++) {
                 int q;
@@ -371,26 +374,34 @@ struct FmtQ0 {
                     const uint32_t nib = l < 4 ? (t[l] & 0x0F0F0F0Fu) : ((t[l - 4] >> 4) & 0x0F0F0F0Fu);
                     q = mi_dot4((int) nib, av[l], mi_dot4((int) 0xF8F8F8F8u, av[l], 0));  // (q - 8) . y
                 }
-                e[l * 68] = (uint32_t) q;
+                e[l * S] = __float_as_uint((float) q);  // exact; _mm256_cvtepi32_ps
             }
-            e[8 * 68] = __float_as_uint(dw * a.d[c * (K / 32) + item]);
+            e[8 * S] = __float_as_uint(dw * a.d[c * (K / 32) + item]);
         }
     }
     // acc[l] = fma(d_i, (float) q[i][l], acc[l]) over the blocks in order (_mm256_fmadd_ps)
-    __device__ static __forceinline__ void chain(const uint32_t * scr, int l, int n_items, float & A, float & M) {
+    __device__ static __forceinline__ void chain(const uint32_t * scr, int l, int n_items, int S, float & A, float & M) {
         (void) M;
-        const uint32_t * q = scr + l * 68;
-        const float * d = (const float *) (scr + 8 * 68);
+        const float * q = (const float *) scr + l * S;
+        const float * d = (const float *) scr + 8 * S;
         int i = 0;
         for (; i + 4 <= n_items; i += 4) {
-            const uint4 qq = *(const uint4 *) (q + i);
+            const float4 qq = *(const float4 *) (q + i);
             const float4 dd = *(const float4 *) (d + i);
-            A = fmaf(dd.x, (float) (int) qq.x, A);
-            A = fmaf(dd.y, (float) (int) qq.y, A);
-            A = fmaf(dd.z, (float) (int) qq.z, A);
-            A = fmaf(dd.w, (float) (int) qq.w, A);
+            A = fmaf(dd.x, qq.x, A);
+            A = fmaf(dd.y, qq.y, A);
+            A = fmaf(dd.z, qq.z, A);
+            A = fmaf(dd.w, qq.w, A);
         }
-        for (; i < n_items; i++) A = fmaf(d[i], (float) (int) q[i], A);
+        for (; i < n_items; i++) A = fmaf(d[i], q[i], A);
+    }
+    // scratch words per (row, column): 9 rows (8 lanes + d) of S >= nitems words; S = 4 (mod 32)
+    // keeps the eight lanes' 16-byte chain reads on distinct banks
+    static int ord_words(int nitems, int & stride) {
+        int S = (nitems + 3) & ~3;
+        while (S % 32 != 4) S += 4;
+        stride = S;
+        return 9 * S;
     }
     __device__ static __forceinline__ float finish(float A, float) {
         // hsum_float_8: ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7))
@@ -422,7 +433,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     const int nitems = (int) (K / F::ITEM);
     const int ncols = g.ncols;
     const lds_act act = lds_carve<F::QKA>(lds, NC, K);
-    uint32_t * scr = (uint32_t *) (lds + ord_offset(lds_bytes<F::QKA>(NC, K))) + wave * NC * kOrdCS;
+    uint32_t * scr = (uint32_t *) (lds + ord_offset(lds_bytes<F::QKA>(NC, K))) + wave * (g.ord_rows ? g.ord_rows : 1) * NC * g.ord_cs;
 
     // 32-bit row bookkeeping (N < 2^31): scalar compares, no 64-bit VGPR temporaries in the loop
     const int Nr = (int) g.N;
@@ -487,36 +498,73 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
             prefetch(ring[(u + PD) % NB], k + PD < klast ? k + PD : klast);
             const int row = row_begin + 4 * k + wave;
             if constexpr (ORD) {
-                const int cl = lane >> 3, ll = lane & 7;
-                float A = 0.0f, M = 0.0f;
-                auto chunk_done = [&](int base) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    __builtin_amdgcn_wave_barrier();
-                    if (cl < ncols) F::chain(scr + cl * kOrdCS, ll, min(64, nitems - base), A, M);
+                const int R = g.ord_rows, cs = g.ord_cs, S = g.ord_s;
+                auto sync = [] {
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     __builtin_amdgcn_wave_barrier();
                 };
+                if (R == 0) {
+                    // rows too long for the scratch: one chain pass per 64-item chunk of the row
+                    const int cl = lane >> 3, ll = lane & 7;
+                    float A = 0.0f, M = 0.0f;
+                    auto chunk_done = [&](int base) {
+                        sync();
+                        if (cl < ncols && !g.abl) F::chain(scr + cl * cs, ll, min(64, nitems - base), S, A, M);
+                        sync();
+                    };
+#pragma unroll
+                    for (int i = 0; i < IPL; i++) {
+                        if (64 * i >= nitems) break;  // wave-uniform
+                        const int item = lane + 64 * i;
+                        if (item < nitems) F::template dot_ord<NC>(ring[u][i], item, lane, act, K, ncols, scr, cs, S);
+                        chunk_done(64 * i);
+                    }
+                    if constexpr (TAIL) {
+                        const uint8_t * wr = wrow_of(k);
+                        for (int base = 64 * IPL; base < nitems; base += 64) {
+                            const int item = base + lane;
+                            if (item < nitems) {
+                                typename F::Regs rr;
+                                F::load(rr, wr, item);
+                                F::template dot_ord<NC>(rr, item, lane, act, K, ncols, scr, cs, S);
+                            }
+                            chunk_done(base);
+                        }
+                    }
+                    const float v = F::finish(A, M);
+                    if (ll == 0 && cl < ncols) *(float *) ((char *) dst + cl * g.ycol + row * sizeof(float)) = v;
+                    continue;
+                }
+                // whole rows in the scratch: R rows' lane sums are collected, then one chain pass
+                // runs them all, lane = (row r, column c, CPU lane l), 8 * NC * R <= 64
+                const int slot = k % R;
+                uint32_t * srow = scr + slot * NC * cs;
 #pragma unroll
                 for (int i = 0; i < IPL; i++) {
-                    if (64 * i >= nitems) break;  // wave-uniform
                     const int item = lane + 64 * i;
-                    if (item < nitems) F::template dot_ord<NC>(ring[u][i], item, lane, act, K, ncols, scr);
-                    chunk_done(64 * i);
+                    if (item < nitems) F::template dot_ord<NC>(ring[u][i], item, item, act, K, ncols, srow, cs, S);
                 }
                 if constexpr (TAIL) {
                     const uint8_t * wr = wrow_of(k);
-                    for (int base = 64 * IPL; base < nitems; base += 64) {
-                        const int item = base + lane;
-                        if (item < nitems) {
-                            typename F::Regs rr;
-                            F::load(rr, wr, item);
-                            F::template dot_ord<NC>(rr, item, lane, act, K, ncols, scr);
-                        }
-                        chunk_done(base);
+                    for (int item = lane + 64 * IPL; item < nitems; item += 64) {
+                        typename F::Regs rr;
+                        F::load(rr, wr, item);
+                        F::template dot_ord<NC>(rr, item, item, act, K, ncols, srow, cs, S);
                     }
                 }
-                const float v = F::finish(A, M);
-                if (ll == 0 && cl < ncols) *(float *) ((char *) dst + cl * g.ycol + row * sizeof(float)) = v;
+                if (slot == R - 1 || k == nrows - 1) {  // wave-uniform
+                    sync();
+                    const int r = lane / (8 * NC), cl = (lane >> 3) % NC, ll = lane & 7;
+                    const bool mine = r <= slot && cl < ncols;
+                    float A = 0.0f, M = 0.0f;
+                    if (mine && !g.abl) F::chain(scr + (r * NC + cl) * cs, ll, nitems, S, A, M);
+                    const float v = F::finish(A, M);
+                    if (ll == 0 && mine) {
+                        const int rr = row_begin + 4 * (k - slot + r) + wave;
+                        *(float *) ((char *) dst + cl * g.ycol + rr * sizeof(float)) = v;
+                    }
+                    sync();
+                }
                 continue;
             }
             float acc[NC];
@@ -567,7 +615,26 @@ int resident_blocks(const void * fn, size_t lds) {
 template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD>
 void launch_one(mi_mmv_group g, hipStream_t s) {
     const size_t act = lds_bytes<F::QKA>(NC, g.K);
-    const size_t lds = ORD ? ord_offset(act) + ord_bytes(NC) : act;
+    size_t lds = act;
+    if (ORD) {
+        // whole rows in the scratch when R >= 1 rows per wave fit a 36 KB budget (the kernel is
+        // VGPR-limited to ~4 workgroups per CU anyway), else one chunk of 64 items per wave
+        const int nitems = (int) (g.K / F::ITEM);
+        int S = 0;
+        const int cs = F::ord_words(nitems, S);
+        int R = (int) ((36 * 1024) / ((size_t) 4 * NC * cs * 4));
+        if (R > 8 / NC) R = 8 / NC;
+        if (R >= 1) {
+            g.ord_rows = R;
+            g.ord_cs = cs;
+            g.ord_s = S;
+        } else {
+            g.ord_rows = 0;
+            g.ord_cs = F::ord_words(64, S);
+            g.ord_s = S;
+        }
+        lds = ord_offset(act) + (size_t) 4 * (g.ord_rows ? g.ord_rows : 1) * NC * g.ord_cs * 4;
+    }
     const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL, TAIL, ORD>;
     if (lds > 64 * 1024) {
         static bool attr_set = false;  // per instance
@@ -621,8 +688,12 @@ void launch_stream_nc(const mi_mmv_group & g, int variant, hipStream_t s) {
 
 template <class F>
 void launch_stream_ord(const mi_mmv_group & g, int variant, hipStream_t s) {
-    if (g_mi_tuning.mmv_order) launch_stream_nc<F, true>(g, variant, s);
-    else launch_stream_nc<F, false>(g, variant, s);
+    if (g_mi_tuning.mmv_order) {
+        mi_mmv_group h = g;
+        h.abl = g_mi_tuning.mmv_order == 2;
+        launch_stream_nc<F, true>(h, variant, s);
+    } else
+        launch_stream_nc<F, false>(g, variant, s);
 }
 
 int qka_of(int type) { return (type == 12 || type == 13) ? 256 : 32; }
@@ -638,7 +709,7 @@ bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols) {
     if (type != 12 && type != 13 && type != 2 && type != 8) return false;
     if (ncols < 1 || ncols > 8 || K % 256 != 0) return false;
     // more than 4 columns whose activations do not fit run as two launches of <= 4 columns
-    return mi_mmv_fused_lds_bytes(type, K, ncols < 4 ? ncols : 4) <= 64 * 1024;  // + ord_bytes(4)
+    return mi_mmv_fused_lds_bytes(type, K, ncols < 4 ? ncols : 4) <= 64 * 1024;  // + <= 36 KB of order scratch
 }
 
 
