@@ -1077,20 +1077,16 @@ static int try_fuse_softmax(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const 
     return k;
 }
 
-// pro / pro_x: the src1 of this mul_mat is the output of a norm chain (norm -> mul g -> add b)
-// that the kernel computes itself from pro_x
-static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u,
-                             const mi_norm_prologue * pro = nullptr, const ggml_tensor * pro_x = nullptr) {
+// The graph's nodes right after mul_mat g->nodes[i] that a GEMV epilogue absorbs: ADD(bias[N]),
+// then ADD(resid) or GELU, then up to two CPY nodes of row views of the result (GPT-2's K/V cache
+// writes, main-backend.cpp:556-561). Fills `e` (mi_f16_epilogue or mi_mmv_group::epilogue: same
+// fields), *out_p = the node holding the final value; returns the last absorbed node, or -1.
+template <class E>
+static int collect_epilogue(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u, const ggml_tensor * w,
+                            const ggml_tensor * x, E & e, ggml_tensor ** out_p, const ggml_tensor ** bias_p,
+                            const ggml_tensor ** res_p) {
     ggml_tensor * mm = g->nodes[i];
-    const ggml_tensor * w = mm->src[0];
-    const ggml_tensor * x = pro_x ? pro_x : mm->src[1];
-    if (is_split_tensor(w)) return -1;
-    if (w->type != GGML_TYPE_F16 || x->type != GGML_TYPE_F32) return -1;
-    if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1 || x->ne[1] > 8) return -1;
-    if (w->nb[0] != 2 || w->nb[1] % 16 != 0 || (uintptr_t) w->data % 16 != 0 || x->nb[0] != sizeof(float)) return -1;
-    if (!mi_mul_mat_f16_fused_supported(w->ne[0], x->ne[1])) return -1;
     const int64_t N = w->ne[1];
-    mi_f16_epilogue e;
     const ggml_tensor * bias_t = nullptr, * res_t = nullptr;
     ggml_tensor * out = mm;
     int last = i;
@@ -1145,6 +1141,30 @@ static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const
         ncopy++;
         last = j;
     }
+    *out_p = out;
+    *bias_p = bias_t;
+    *res_p = res_t;
+    return last;
+}
+
+// pro / pro_x: the src1 of this mul_mat is the output of a norm chain (norm -> mul g -> add b)
+// that the kernel computes itself from pro_x
+static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u,
+                             const mi_norm_prologue * pro = nullptr, const ggml_tensor * pro_x = nullptr) {
+    ggml_tensor * mm = g->nodes[i];
+    const ggml_tensor * w = mm->src[0];
+    const ggml_tensor * x = pro_x ? pro_x : mm->src[1];
+    if (is_split_tensor(w)) return -1;
+    if (w->type != GGML_TYPE_F16 || x->type != GGML_TYPE_F32) return -1;
+    if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1 || x->ne[1] > 8) return -1;
+    if (w->nb[0] != 2 || w->nb[1] % 16 != 0 || (uintptr_t) w->data % 16 != 0 || x->nb[0] != sizeof(float)) return -1;
+    if (!mi_mul_mat_f16_fused_supported(w->ne[0], x->ne[1])) return -1;
+    const int64_t N = w->ne[1];
+    mi_f16_epilogue e;
+    const ggml_tensor * bias_t = nullptr, * res_t = nullptr;
+    ggml_tensor * out = mm;
+    const int last = collect_epilogue(ctx, g, i, u, w, x, e, &out, &bias_t, &res_t);
+    if (last < 0) return -1;
     // every workgroup reads all of X and W; resid/bias are read per element. When the graph
     // allocator has placed `out` over X (X's last reader is this mul_mat), X is first converted
     // into the backend's scratch so no workgroup can see it overwritten.
@@ -1162,6 +1182,39 @@ static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const
     const mi_norm_prologue none;
     mi_mul_mat_f16_fused(w->data, w->nb[1], w->ne[0], N, src_cols(x), xh, x->ne[1], (float *) out->data, out->nb[1], e,
                          pro ? *pro : none, ctx->stream);
+    ctx->last_launches++;
+    return last;
+}
+
+// Q4_0/Q8_0/Q4_K/Q5_K decode GEMV with the graph's bias / residual / GELU and K/V row copies in
+// the streaming kernel's store (a one-member k_mmv_stream group); -1 if nothing follows that it
+// can absorb (then the node goes through the grouped path).
+static int try_fuse_q_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
+    ggml_tensor * mm = g->nodes[i];
+    if (!fused_mv_eligible(mm)) return -1;
+    const ggml_tensor * w = mm->src[0];
+    const ggml_tensor * x = mm->src[1];
+    mi_mmv_group grp;
+    const ggml_tensor * bias_t = nullptr, * res_t = nullptr;
+    ggml_tensor * out = mm;
+    const int last = collect_epilogue(ctx, g, i, u, w, x, grp.epi, &out, &bias_t, &res_t);
+    if (last <= i) return -1;
+    // every workgroup quantizes all of X in its prologue and reads resid/bias per element: the
+    // output may not overlap W, X or the bias, and may alias the residual only element for element
+    if (overlaps(out, w) || overlaps(out, x) || (bias_t && overlaps(out, bias_t)) || !safe_alias(out, res_t)) return -1;
+    if (out->nb[1] % sizeof(float) != 0) return -1;
+    grp.type = w->type;
+    grp.n = 1;
+    grp.ncols = (int) x->ne[1];
+    grp.K = w->ne[0];
+    grp.N = w->ne[1];
+    grp.nb01 = w->nb[1];
+    grp.xcol = x->nb[1];
+    grp.ycol = out->nb[1];
+    grp.m[0].W = w->data;
+    grp.m[0].X = (const char *) x->data;
+    grp.m[0].dst = (float *) out->data;
+    mi_mul_mat_q_fused(grp, ctx->stream);
     ctx->last_launches++;
     return last;
 }
@@ -1471,7 +1524,10 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
                 case GGML_OP_NORM:
                 case GGML_OP_RMS_NORM: last = (fuse_mask & 1) ? try_fuse_norm(ctx, cgraph, i, uses) : -1; break;
                 case GGML_OP_SCALE: last = (fuse_mask & 2) ? try_fuse_softmax(ctx, cgraph, i, uses) : -1; break;
-                case GGML_OP_MUL_MAT: last = (fuse_mask & 4) ? try_fuse_f16_gemv(ctx, cgraph, i, uses) : -1; break;
+                case GGML_OP_MUL_MAT:
+                    last = (fuse_mask & 4) ? try_fuse_f16_gemv(ctx, cgraph, i, uses) : -1;
+                    if (last < 0 && (fuse_mask & 32) && !no_fuse) last = try_fuse_q_gemv(ctx, cgraph, i, uses);
+                    break;
                 case GGML_OP_CPY:
                 case GGML_OP_DUP:
                 case GGML_OP_CONT: last = (fuse_mask & 8) ? try_fuse_copies(ctx, cgraph, i) : -1; break;

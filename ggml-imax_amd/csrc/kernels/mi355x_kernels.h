@@ -78,6 +78,19 @@ struct mi_mmv_group {
     int ord_rows = 0;       // reference order: rows per chain pass (0: one pass per 64-item chunk of a row)
     int ord_cs = 0;         // reference order: scratch words per (row, column)
     int ord_s = 0;          // reference order: Q4_0/Q8_0 lane-row stride in the scratch
+    // the graph's following bias / residual / GELU and K/V row copies (one-member groups; same
+    // fields and rounding as mi_f16_epilogue)
+    struct epilogue {
+        const float * bias = nullptr;
+        const char * resid = nullptr;
+        size_t resid_nb1 = 0;
+        const uint16_t * gelu_table = nullptr;
+        struct row_copy {
+            int64_t row0 = 0, row1 = 0;
+            char * ptr = nullptr;
+            size_t col_stride = 0;
+        } copy[2];
+    } epi;
     mi_mmv_member m[kMiMaxMembers];
 };
 bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols);

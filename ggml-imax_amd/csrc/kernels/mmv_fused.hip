@@ -415,6 +415,23 @@ struct FmtQ0 {
 
 // IPL = items per lane held in the prefetch ring (further items of long rows are loaded
 // in-line); PD = rows in flight ahead of the row being computed.
+// one output element, through the graph's epilogue: + bias[row], then + resid or GELU (the fp16
+// table lookup of ggml_vec_gelu_f32 with its +-10 clamps), then the K/V-cache row copies -- each
+// step rounded as its own node would round it
+__device__ __forceinline__ void store_out(const mi_mmv_group & g, float * dst, int c, int row, float v) {
+    const mi_mmv_group::epilogue & e = g.epi;
+    if (e.bias) v = v + e.bias[row];
+    if (e.resid) v = v + *(const float *) (e.resid + c * e.resid_nb1 + (size_t) row * sizeof(float));
+    else if (e.gelu_table) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
+    *(float *) ((char *) dst + c * g.ycol + (size_t) row * sizeof(float)) = v;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (e.copy[k].ptr && row >= e.copy[k].row0 && row < e.copy[k].row1) {
+            *(float *) (e.copy[k].ptr + c * e.copy[k].col_stride + (size_t) (row - e.copy[k].row0) * sizeof(float)) = v;
+        }
+    }
+}
+
 // ORD: combine in the reference CPU's order (bit-identical results, see dot_ord / chain): each
 // 64-item chunk of a row leaves its per-item lane sums in the wave's LDS scratch, then lane
 // (column c, CPU lane l) runs the reference's sequential fma chain over the chunk.
@@ -532,7 +549,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                         }
                     }
                     const float v = F::finish(A, M);
-                    if (ll == 0 && cl < ncols) *(float *) ((char *) dst + cl * g.ycol + row * sizeof(float)) = v;
+                    if (ll == 0 && cl < ncols) store_out(g, dst, cl, row, v);
                     continue;
                 }
                 // whole rows in the scratch: R rows' lane sums are collected, then one chain pass
@@ -560,8 +577,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                     if (mine && !g.abl) F::chain(scr + (r * NC + cl) * cs, ll, nitems, S, A, M);
                     const float v = F::finish(A, M);
                     if (ll == 0 && mine) {
-                        const int rr = row_begin + 4 * (k - slot + r) + wave;
-                        *(float *) ((char *) dst + cl * g.ycol + rr * sizeof(float)) = v;
+                        store_out(g, dst, cl, row_begin + 4 * (k - slot + r) + wave, v);
                     }
                     sync();
                 }
@@ -588,7 +604,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 const float v = mi_wave_sum_u(acc[c]);
-                if (lane == 0 && c < ncols) *(float *) ((char *) dst + c * g.ycol + row * sizeof(float)) = v;
+                if (lane == 0 && c < ncols) store_out(g, dst, c, row, v);
             }
         }
     }
@@ -725,6 +741,9 @@ void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s) {
                 h.m[m].X = g.m[m].X + (size_t) c0 * g.xcol;
                 h.m[m].dst = (float *) ((char *) g.m[m].dst + (size_t) c0 * g.ycol);
             }
+            if (h.epi.resid) h.epi.resid += (size_t) c0 * h.epi.resid_nb1;
+            for (auto & cp : h.epi.copy)
+                if (cp.ptr) cp.ptr += (size_t) c0 * cp.col_stride;
             mi_mul_mat_q_fused_launch(h, s);
         }
         return;
