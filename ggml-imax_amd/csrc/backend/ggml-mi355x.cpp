@@ -1189,16 +1189,30 @@ static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const
 // Q4_0/Q8_0/Q4_K/Q5_K decode GEMV with the graph's bias / residual / GELU and K/V row copies in
 // the streaming kernel's store (a one-member k_mmv_stream group); -1 if nothing follows that it
 // can absorb (then the node goes through the grouped path).
-static int try_fuse_q_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
+static int fuse_mask_q() {
+    static const int m = getenv("GGML_MI355X_NO_FUSED_MMV") ? 0 : (getenv("GGML_MI355X_FUSE_MASK") ? atoi(getenv("GGML_MI355X_FUSE_MASK")) : 0xff);
+    return m;
+}
+
+// pro / pro_x: as for try_fuse_f16_gemv (the norm chain producing src1, computed in the kernel)
+static int try_fuse_q_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u,
+                           const mi_norm_prologue * pro = nullptr, const ggml_tensor * pro_x = nullptr) {
     ggml_tensor * mm = g->nodes[i];
     if (!fused_mv_eligible(mm)) return -1;
     const ggml_tensor * w = mm->src[0];
-    const ggml_tensor * x = mm->src[1];
+    const ggml_tensor * x = pro_x ? pro_x : mm->src[1];
+    if (pro && (w->ne[0] > kMiMmvProMaxK || x->nb[1] % sizeof(float) != 0 || x->ne[1] != mm->src[1]->ne[1])) return -1;
     mi_mmv_group grp;
+    if (pro) {
+        grp.pro.g = pro->g;
+        grp.pro.b = pro->b;
+        grp.pro.eps = pro->eps;
+        grp.pro.mode = pro->mode;
+    }
     const ggml_tensor * bias_t = nullptr, * res_t = nullptr;
     ggml_tensor * out = mm;
     const int last = collect_epilogue(ctx, g, i, u, w, x, grp.epi, &out, &bias_t, &res_t);
-    if (last <= i) return -1;
+    if (last < 0 || (last == i && !pro)) return -1;
     // every workgroup quantizes all of X in its prologue and reads resid/bias per element: the
     // output may not overlap W, X or the bias, and may alias the residual only element for element
     if (overlaps(out, w) || overlaps(out, x) || (bias_t && overlaps(out, bias_t)) || !safe_alias(out, res_t)) return -1;
@@ -1248,7 +1262,8 @@ static int try_fuse_norm(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_
         pro.b = bias;
         pro.eps = op_param_f(norm, 0);
         pro.mode = norm->op == GGML_OP_RMS_NORM ? 2 : 1;
-        const int r = try_fuse_f16_gemv(ctx, g, m, u, &pro, norm->src[0]);
+        int r = try_fuse_f16_gemv(ctx, g, m, u, &pro, norm->src[0]);
+        if (r < 0 && (fuse_mask_q() & 32)) r = try_fuse_q_gemv(ctx, g, m, u, &pro, norm->src[0]);
         if (r >= 0) return r;
     }
     if (!safe_alias(out, norm->src[0]) || overlaps(out, mul->src[1]) || (bias && overlaps(out, g->nodes[last]->src[1]))) return -1;

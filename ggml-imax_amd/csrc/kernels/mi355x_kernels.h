@@ -91,9 +91,19 @@ struct mi_mmv_group {
             size_t col_stride = 0;
         } copy[2];
     } epi;
+    // the graph's norm|rms_norm -> mul(g) -> add(b) producing src1, computed by the kernel from X
+    // (one-member groups, K <= 768; same semantics as mi_norm_prologue)
+    struct prologue {
+        const float * g = nullptr;
+        const float * b = nullptr;
+        float eps = 0.0f;
+        int mode = 0;  // 0 none, 1 norm, 2 rms_norm
+    } pro;
+    int pro_off = 0;   // set by the launcher: LDS byte offset of the normalized columns
     mi_mmv_member m[kMiMaxMembers];
 };
 bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols);
+constexpr int64_t kMiMmvProMaxK = 768;  // norm prologue: the column is held in one wave's registers
 
 // launch-shape knobs of the streaming kernels (defaults tuned on MI355X; settable for A/B runs)
 struct mi_tuning {

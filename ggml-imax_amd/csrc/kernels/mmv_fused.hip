@@ -24,6 +24,11 @@
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
 
+// the norm prologue replays the CPU's rounding (cpu_order.h turns FMA contraction off); the rest
+// of this file keeps the default contraction
+#include "cpu_order.h"
+#pragma clang fp contract(fast)
+
 #include <stdlib.h>
 
 static int env_int(const char * name, int def) {
@@ -415,6 +420,48 @@ struct FmtQ0 {
 
 // IPL = items per lane held in the prefetch ring (further items of long rows are loaded
 // in-line); PD = rows in flight ahead of the row being computed.
+// norm|rms_norm -> mul(g) -> add(b) of the group's activation columns into LDS (f32), by wave 0
+// with each column in registers -- the arithmetic of k_norm (ops.hip) and of the F16 GEMV's
+// prologue: certified double means, then every step rounded separately
+__device__ void norm_prologue(const mi_mmv_group & g, const char * X, int ncols, float * xn) {
+    constexpr int kJ = (int) (kMiMmvProMaxK / 64);
+    const int lane = threadIdx.x & 63;
+    const int64_t K = g.K;
+    for (int c = 0; c < ncols; c++) {
+        const float * xc = (const float *) (X + c * g.xcol);
+        float v[kJ], gv[kJ], bv[kJ];
+#pragma unroll
+        for (int j = 0; j < kJ; j++) {
+            const int64_t k = (int64_t) j * 64 + lane;
+            const bool in = k < K;
+            v[j] = in ? xc[k] : 0.0f;
+            gv[j] = in && g.pro.g ? g.pro.g[k] : 1.0f;
+            bv[j] = in && g.pro.b ? g.pro.b[k] : 0.0f;
+        }
+        float scale;
+        if (g.pro.mode == 2) {
+            const float mean = wave_mean_cpu_order<true, kJ>(v, K);
+            scale = 1.0f / sqrtf(add_rn(mean, g.pro.eps));
+        } else {
+            const float mean = wave_mean_cpu_order<false, kJ>(v, K);
+#pragma unroll
+            for (int j = 0; j < kJ; j++) v[j] = sub_rn(v[j], mean);
+            const float variance = wave_mean_cpu_order<true, kJ>(v, K);
+            scale = 1.0f / sqrtf(add_rn(variance, g.pro.eps));
+        }
+#pragma unroll
+        for (int j = 0; j < kJ; j++) {
+            const int64_t k = (int64_t) j * 64 + lane;
+            if (k < K) {
+                float y = mul_rn(v[j], scale);
+                if (g.pro.g) y = mul_rn(y, gv[j]);
+                if (g.pro.b) y = add_rn(y, bv[j]);
+                xn[c * K + k] = y;
+            }
+        }
+    }
+}
+
 // one output element, through the graph's epilogue: + bias[row], then + resid or GELU (the fp16
 // table lookup of ggml_vec_gelu_f32 with its +-10 clamps), then the K/V-cache row copies -- each
 // step rounded as its own node would round it
@@ -435,7 +482,7 @@ __device__ __forceinline__ void store_out(const mi_mmv_group & g, float * dst, i
 // ORD: combine in the reference CPU's order (bit-identical results, see dot_ord / chain): each
 // 64-item chunk of a row leaves its per-item lane sums in the wave's LDS scratch, then lane
 // (column c, CPU lane l) runs the reference's sequential fma chain over the chunk.
-template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD>
+template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO>
 __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int NB = PD + 1;  // ring slots
@@ -480,7 +527,17 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
 #pragma unroll
     for (int u = 0; u < PD; u++) prefetch(ring[u], u < klast ? u : klast);
 
-    // 2) quantize the member's activation columns into LDS (wave w: 256-slices w, w+4, ...)
+    // 2) quantize the member's activation columns into LDS (wave w: 256-slices w, w+4, ...),
+    //    from the normalized columns when the graph's norm chain is fused in
+    const char * Xq = X;
+    size_t xcolq = g.xcol;
+    if constexpr (PRO) {
+        float * xn = (float *) (lds + g.pro_off);
+        if (wave == 0) norm_prologue(g, X, ncols, xn);
+        __syncthreads();
+        Xq = (const char *) xn;
+        xcolq = (size_t) K * sizeof(float);
+    }
     {
         const int nsl = (int) (K / 256);
         const int total = nsl * ncols;
@@ -491,7 +548,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
             for (int u = 0; u < 4; u++) {
                 const int p = min(p0 + 4 * u, total - 1);
                 const int c = p / nsl, sl = p - c * nsl;
-                v[u] = *(const float4 *) (X + c * g.xcol + ((size_t) sl * 256 + lane * 4) * sizeof(float));
+                v[u] = *(const float4 *) (Xq + c * xcolq + ((size_t) sl * 256 + lane * 4) * sizeof(float));
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -628,7 +685,7 @@ int resident_blocks(const void * fn, size_t lds) {
     return n;
 }
 
-template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD>
+template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO = false>
 void launch_one(mi_mmv_group g, hipStream_t s) {
     const size_t act = lds_bytes<F::QKA>(NC, g.K);
     size_t lds = act;
@@ -651,7 +708,11 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
         }
         lds = ord_offset(act) + (size_t) 4 * (g.ord_rows ? g.ord_rows : 1) * NC * g.ord_cs * 4;
     }
-    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL, TAIL, ORD>;
+    if (PRO) {
+        g.pro_off = (int) ord_offset(lds);
+        lds = (size_t) g.pro_off + (size_t) NC * g.K * sizeof(float);
+    }
+    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL, TAIL, ORD, PRO>;
     if (lds > 64 * 1024) {
         static bool attr_set = false;  // per instance
         if (!attr_set) {
@@ -666,7 +727,7 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
     rows = (rows + 3) / 4 * 4;
     g.rows_per_block = rows;
     g.blocks_per_member = (int) ((g.N + rows - 1) / rows);
-    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL, TAIL, ORD>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds,
+    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL, TAIL, ORD, PRO>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds,
                        s, g);
 }
 
@@ -679,6 +740,12 @@ void launch_tail(const mi_mmv_group & g, hipStream_t s) {
 template <class F, int NC, bool ORD>
 void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
     const int items = (int) (g.K / F::ITEM);
+    if (g.pro.mode) {
+        // norm prologue (K <= 768: at most 24 items per row), its own instance so the prologue's
+        // registers do not weigh on the plain kernels
+        launch_one<F, NC, 1, 1, false, ORD, true>(g, s);
+        return;
+    }
     if (items > 64) {
         // two items per lane in the ring (Q4_0 / Q8_0 at K=4096)
         if (variant / 10 == 1) launch_tail<F, NC, 1, 2, ORD>(g, s);
