@@ -465,7 +465,12 @@ __device__ void norm_prologue(const mi_mmv_group & g, const char * X, int ncols,
 // one output element, through the graph's epilogue: + bias[row], then + resid or GELU (the fp16
 // table lookup of ggml_vec_gelu_f32 with its +-10 clamps), then the K/V-cache row copies -- each
 // step rounded as its own node would round it
+template <bool X>
 __device__ __forceinline__ void store_out(const mi_mmv_group & g, float * dst, int c, int row, float v) {
+    if constexpr (!X) {
+        *(float *) ((char *) dst + c * g.ycol + (size_t) row * sizeof(float)) = v;
+        return;
+    }
     const mi_mmv_group::epilogue & e = g.epi;
     if (e.bias) v = v + e.bias[row];
     if (e.resid) v = v + *(const float *) (e.resid + c * e.resid_nb1 + (size_t) row * sizeof(float));
@@ -482,6 +487,7 @@ __device__ __forceinline__ void store_out(const mi_mmv_group & g, float * dst, i
 // ORD: combine in the reference CPU's order (bit-identical results, see dot_ord / chain): each
 // 64-item chunk of a row leaves its per-item lane sums in the wave's LDS scratch, then lane
 // (column c, CPU lane l) runs the reference's sequential fma chain over the chunk.
+// PRO: the graph's norm prologue (g.pro) and store epilogue (g.epi) are compiled in
 template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO>
 __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -531,7 +537,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     //    from the normalized columns when the graph's norm chain is fused in
     const char * Xq = X;
     size_t xcolq = g.xcol;
-    if constexpr (PRO) {
+    if (PRO && g.pro.mode) {
         float * xn = (float *) (lds + g.pro_off);
         if (wave == 0) norm_prologue(g, X, ncols, xn);
         __syncthreads();
@@ -606,7 +612,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                         }
                     }
                     const float v = F::finish(A, M);
-                    if (ll == 0 && cl < ncols) store_out(g, dst, cl, row, v);
+                    if (ll == 0 && cl < ncols) store_out<PRO>(g, dst, cl, row, v);
                     continue;
                 }
                 // whole rows in the scratch: R rows' lane sums are collected, then one chain pass
@@ -634,7 +640,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                     if (mine && !g.abl) F::chain(scr + (r * NC + cl) * cs, ll, nitems, S, A, M);
                     const float v = F::finish(A, M);
                     if (ll == 0 && mine) {
-                        store_out(g, dst, cl, row_begin + 4 * (k - slot + r) + wave, v);
+                        store_out<PRO>(g, dst, cl, row_begin + 4 * (k - slot + r) + wave, v);
                     }
                     sync();
                 }
@@ -661,7 +667,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 const float v = mi_wave_sum_u(acc[c]);
-                if (lane == 0 && c < ncols) store_out(g, dst, c, row, v);
+                if (lane == 0 && c < ncols) store_out<PRO>(g, dst, c, row, v);
             }
         }
     }
@@ -708,7 +714,7 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
         }
         lds = ord_offset(act) + (size_t) 4 * (g.ord_rows ? g.ord_rows : 1) * NC * g.ord_cs * 4;
     }
-    if (PRO) {
+    if (PRO && g.pro.mode) {
         g.pro_off = (int) ord_offset(lds);
         lds = (size_t) g.pro_off + (size_t) NC * g.K * sizeof(float);
     }
@@ -740,10 +746,13 @@ void launch_tail(const mi_mmv_group & g, hipStream_t s) {
 template <class F, int NC, bool ORD>
 void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
     const int items = (int) (g.K / F::ITEM);
-    if (g.pro.mode) {
-        // norm prologue (K <= 768: at most 24 items per row), its own instance so the prologue's
-        // registers do not weigh on the plain kernels
-        launch_one<F, NC, 1, 1, false, ORD, true>(g, s);
+    const mi_mmv_group::epilogue & e = g.epi;
+    if (g.pro.mode || e.bias || e.resid || e.gelu_table || e.copy[0].ptr || e.copy[1].ptr) {
+        // the graph's norm prologue and/or epilogue: instances of their own (prefetch depth 1) so
+        // that their registers and per-row branches do not weigh on the plain kernels
+        if (items > 128) launch_one<F, NC, 1, 2, true, ORD, true>(g, s);
+        else if (items > 64) launch_one<F, NC, 1, 2, false, ORD, true>(g, s);
+        else launch_one<F, NC, 1, 1, false, ORD, true>(g, s);
         return;
     }
     if (items > 64) {
