@@ -35,6 +35,7 @@ from ggml_mi355x import ggml as G  # noqa: E402
 from ggml_mi355x import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense f16/bf16 MFMA
 TYPE_NAMES = {"q4_K": 12, "q5_K": 13, "q4_0": 2, "q8_0": 8, "f16": 1}
 
 
@@ -75,14 +76,46 @@ class MulMatWorkload:
         self.ctx.free()
 
 
+def host_cpus():
+    """CPUs this process may run on: the affinity mask, capped by the cgroup CPU quota (on the GPU
+    box the mask lists the whole machine, the quota is this job's share), plus the host topology."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model, cores, sockets = "unknown", None, set()
+    try:
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name":
+                model = v
+            elif k == "cpu cores":
+                cores = int(v)
+            elif k == "physical id":
+                sockets.add(v)
+    except OSError:
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"threads": int(os.environ.get("BENCH_CPU_THREADS", usable)), "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+            "model": model, "physical_cores_per_socket": cores, "sockets": len(sockets) or None,
+            "logical_cpus": os.cpu_count()}
+
+
 def cpu_baseline(t, K, N, B, seconds=10.0):
     """The reference ggml CPU backend (oracle/_ref/libggml_ref.so, compiled from the reference
-    sources with its own x86 flags) on a bounded sample of the same workload."""
+    sources with its own x86 flags) on a bounded sample of the same workload, with one thread per
+    CPU this job may use (host_cpus)."""
     ref_path = os.path.join(REPO, "oracle", "_ref", "libggml_ref.so")
     if not os.path.exists(ref_path):
         return None
     ref = G.Lib([ref_path], isolated=True)
-    threads = int(os.environ.get("BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    hc = host_cpus()
+    threads = hc["threads"]
     cpu = ref.ggml_backend_cpu_init()
     ref.ggml_backend_cpu_set_n_threads(cpu, threads)
     R = 32  # same rotation depth as the GPU run: the weights do not fit the CPU caches either
@@ -100,18 +133,9 @@ def cpu_baseline(t, K, N, B, seconds=10.0):
         "value": round(units * unit_bytes(t, K, N, B) / dt / 1e9, 2), "unit": "GB/s",
         "cores": threads, "kind": "reference",
         "sample": f"{units} mul_mats ({n} graphs x {R}) of the same workload in {dt:.1f} s; "
-                  f"us/mul_mat={dt / units * 1e6:.1f}; host={_cpu_model()}",
+                  f"us/mul_mat={dt / units * 1e6:.1f}",
+        "host": hc,
     }
-
-
-def _cpu_model():
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
 
 
 GPT2_PROMPT = "Once upon a time the cat sat on the mat and the dog ran away from the big red house"
@@ -160,18 +184,21 @@ def gpt2_bench(lib, backend, n_decode=128, n_batch=8, path=None, label="GPT-2-11
 
 def gpt2_q4k_bench(lib, backend, n_decode):
     """The same decode loop on the model quantized to Q4_K by gpt2.quantize_model (byte-identical
-    to examples/gpt-2/quantize.cpp): default (tree-order) GEMV, and mmv_order=1 (the reference
-    CPU's combination order: bit-identical logits) for the cost of exactness."""
+    to examples/gpt-2/quantize.cpp). The headline figure runs the quantized GEMV in mmv_order=1
+    (the reference CPU's combination order), whose logits are bit-identical to the reference's
+    (tests/test_gpt2.py) and so meet the 1e-3 logit bar; the tree-order mode is reported beside
+    it with its measured deviation (it does NOT meet 1e-3 on this model)."""
     from ggml_mi355x import gpt2
     path = gpt2.ensure_quantized_model(lib, "q4_k")
-    r = gpt2_bench(lib, backend, n_decode, path=path, label="GPT-2-117M Q4_K (quantize.cpp q4_k of the synthetic model)",
-                   parity="default order: logits within the reference's own 1-ulp sensitivity (tests/test_gpt2.py)")
     lib.ggml_backend_mi355x_set_tuning(b"mmv_order", 1)
     try:
-        ro = gpt2_bench(lib, backend, n_decode, path=path, label="same, mmv_order=1", parity="logits bit-identical")
+        r = gpt2_bench(lib, backend, n_decode, path=path, label="GPT-2-117M Q4_K (quantize.cpp q4_k of the synthetic model), mmv_order=1",
+                       parity="logits bit-identical to the reference CPU at every teacher-forced step (max |d| = 0 <= 1e-3)")
     finally:
         lib.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
-    r["mmv_order_1"] = {k: ro[k] for k in ("decode_tokens_per_s", "ms_per_decode_token", "parity")}
+    tree = gpt2_bench(lib, backend, n_decode, path=path, label="same, tree-order GEMV",
+                      parity="NOT within 1e-3: 1.4-1.9e-2 of max|logit| (the model re-quantizes activations every layer)")
+    r["tree_order"] = {k: tree[k] for k in ("decode_tokens_per_s", "ms_per_decode_token", "parity")}
     return r
 
 
@@ -331,9 +358,10 @@ def event_time_per_step(torch, wl, stream_ptr, iters=20):
     return e0.elapsed_time(e1) / iters
 
 
-def load_traffic(kernel_hint: str):
-    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary
-    (tools/pmc_traffic.py -> profiles/*_pmc_traffic.json), or None."""
+def load_traffic(kernel_prefix: str):
+    """Per-launch HBM bytes of the dominant kernel from the newest committed PMC summary
+    (tools/pmc_traffic.py -> profiles/*_pmc_traffic.json): (bytes, source file, kernel name), or
+    (None, None, None). Not measured in this run: rocprofv3 counters need their own process."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")))
     for f in reversed(files):
         try:
@@ -341,9 +369,26 @@ def load_traffic(kernel_hint: str):
         except (OSError, ValueError):
             continue
         for k, v in d.get("kernels", {}).items():
-            if kernel_hint in k:
-                return v.get("hbm_bytes_per_launch")
-    return None
+            if k.startswith(kernel_prefix):
+                return v.get("hbm_bytes_per_launch"), os.path.relpath(f, REPO), k
+    return None, None, None
+
+
+class RotatedSingle:
+    """ONE mul_mat per graph (the shape a dependent decode layer presents): R graphs over R weight
+    copies, computed round-robin, so every launch streams a weight the caches do not hold."""
+
+    def __init__(self, lib, backend, t, K, N, B, R):
+        self.wls = [MulMatWorkload(lib, backend, t, K, N, B, 1, seed=42) for _ in range(R)]
+        self.i = 0
+
+    def step(self):
+        self.wls[self.i].step()
+        self.i = (self.i + 1) % len(self.wls)
+
+    def free(self):
+        for w in self.wls:
+            w.free()
 
 
 def main():
@@ -414,7 +459,7 @@ def main():
     launches = max(launches, 1)
     bytes_per_launch = R * ub / launches
     achieved = bytes_per_launch / (step_ms / 1e3 / launches) / 1e9
-    traffic = load_traffic("k_mmv_stream")
+    traffic, traffic_src, traffic_kernel = load_traffic("void (anonymous namespace)::k_mmv_stream<(anonymous namespace)::FmtKQ<false>")
 
     result = {
         "metric": "Q4_K 4096x4096 mul_mat GB/s-effective (+ GPT-2 tokens/s), 1 GPU",
@@ -434,6 +479,8 @@ def main():
                    "rotated_copies": R, "parallelism": f"replica x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": {"file": traffic_src, "kernel": traffic_kernel,
+                                        "note": "PMC FETCH_SIZE/WRITE_SIZE passes of the same bench command, committed profile; not this run"},
                      "kernel_launches_per_step": launches, "event_ms_per_step": round(step_ms, 4),
                      "algorithmic_bytes_per_launch": int(bytes_per_launch),
                      "note": "achieved = algorithmic bytes per launch (R mul_mats x (N*K/256*144 + 4K + 4N) / launches) "
@@ -454,17 +501,36 @@ def main():
             sweep[name] = {"GB/s": round(r * unit_bytes(tt, k, n, 1) / (ms / 1e3) / 1e9, 1),
                            "us_per_mul_mat": round(ms * 1e3 / r, 2)}
             w2.free()
-        # configs[4]: batched B=512 prefill Q4_K 4096x4096 on MFMA tiles (per GPU; the 8-GPU run
-        # shards the 512 prompt columns, 64 per GPU)
-        for bb in (512, 64):
+        # one Q4_K 4096^2 GEMV per graph (no grouping), 32 rotated weights
+        w1 = RotatedSingle(lib, backend, 12, 4096, 4096, 1, 32)
+        for _ in range(64):
+            w1.step()
+        lib.ggml_backend_synchronize(backend)
+        ms = event_time_per_step(torch, w1, stream_ptr, iters=256)
+        sweep["q4_K_4096x4096_single_graph"] = {
+            "GB/s": round(unit_bytes(12, 4096, 4096, 1) / (ms / 1e3) / 1e9, 1), "us_per_mul_mat": round(ms * 1e3, 2),
+            "launches_per_graph": lib.ggml_backend_mi355x_last_launch_count(backend),
+            "note": "one mul_mat per graph_compute, 32 weight copies round-robin; HIP events over 256 graphs"}
+        w1.free()
+        # configs[4]: batched prefill Q4_K 4096x4096 on MFMA tiles (per GPU; the 8-GPU run shards
+        # the 512 prompt columns, 64 per GPU), plus the mid-batch sizes
+        for bb in (512, 64, 32, 16):
             w3 = MulMatWorkload(lib, backend, 12, 4096, 4096, bb, 8)
             for _ in range(3):
                 w3.step()
             lib.ggml_backend_synchronize(backend)
             ms = event_time_per_step(torch, w3, stream_ptr, iters=10)
             flops = 2.0 * 4096 * 4096 * bb * 8
-            sweep[f"q4_K_4096x4096_b{bb}_prefill"] = {"TFLOP/s": round(flops / (ms / 1e3) / 1e12, 2),
-                                                       "us_per_mul_mat": round(ms * 1e3 / 8, 2)}
+            us = ms * 1e3 / 8
+            e = {"TFLOP/s": round(flops / (ms / 1e3) / 1e12, 2), "us_per_mul_mat": round(us, 2),
+                 "GB/s_effective": round(unit_bytes(12, 4096, 4096, bb) / (us / 1e6) / 1e9, 1),
+                 "launches_per_mul_mat": lib.ggml_backend_mi355x_last_launch_count(backend) / 8}
+            if bb == 512:
+                e["roofline"] = {"bound": "mfma", "achieved": round(flops / 8 / (us / 1e6) / 1e12, 2), "peak": MFMA_PEAK_TFLOPS,
+                                 "unit": "TFLOP/s", "frac": round(flops / 8 / (us / 1e6) / 1e12 / MFMA_PEAK_TFLOPS, 4),
+                                 "note": "2*N*K*B / HIP-event time of the whole mul_mat (activation quantizer + GEMM) vs the "
+                                         "dense f16 MFMA peak (the GEMM's operands are exact-integer f16)"}
+            sweep[f"q4_K_4096x4096_b{bb}_prefill"] = e
             w3.free()
         result["sweep"] = sweep
 
@@ -500,7 +566,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(t, K, N, B, args.cpu_seconds)
-        threads = int(os.environ.get("BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
+        threads = host_cpus()["threads"]
         if "gpt2" in result:
             result["gpt2"]["cpu_baseline"] = gpt2_cpu_baseline(threads)
         if "gpt2_q4_k" in result:

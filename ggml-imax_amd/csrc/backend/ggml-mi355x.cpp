@@ -224,7 +224,12 @@ static ggml_backend_buffer_t mi_host_buft_alloc(ggml_backend_buffer_type_t buft,
 }
 
 static size_t mi_host_buft_align(ggml_backend_buffer_type_t) { return 64; }
-static bool mi_host_buft_supports(ggml_backend_buffer_type_t, ggml_backend_t backend) { return false; }
+// pinned host memory is ordinary CPU memory to the scheduler: whatever backend can use a CPU
+// buffer can use this one (ggml-cuda.cu:1037-1038 delegates the same way)
+static bool mi_host_buft_supports(ggml_backend_buffer_type_t, ggml_backend_t backend) {
+    ggml_backend_buffer_type_t cpu = ggml_backend_cpu_buffer_type();
+    return cpu->iface.supports_backend(cpu, backend);
+}
 static bool mi_host_buft_is_host(ggml_backend_buffer_type_t) { return true; }
 
 // ---------------------------------------------------------------------------------------------
@@ -419,7 +424,6 @@ struct mi_backend_ctx {
     size_t scratch_size = 0;
     size_t scratch_used = 0;
     std::vector<mi_act_cache_entry> act_cache;
-    bool graph_capture = true;
     int last_launches = 0;
     uint16_t * tables = nullptr;  // device: exp, gelu, silu fp16 tables (3 x 65536)
     hipEvent_t split_ready = nullptr;  // src1 of a split mul_mat is ready on `stream`
@@ -543,8 +547,10 @@ static int act_kind(ggml_type wtype) {
 }
 
 // kinds: 0 q8_0, 1 q8_K, 2 f16, 3/4 q8_0/q8_K quants expanded to f16(d * q) (mmq.hip operand),
-// 5/6/7 = 2/3/4 in the GEMM's K-blocked layout [K/16][ncols][16]
+// 5/6/7 = 2/3/4 in the GEMM's K-blocked layout [K/16][ncols][16], 8 q8_K in the int8-MFMA
+// layouts of the exact prefill GEMM (mmq_exact.hip)
 static size_t act_bytes(int kind, int64_t K, int64_t ncols) {
+    if (kind == 8) return mi_act_mmx_bytes(K, ncols);
     if (kind >= 2) return (size_t) K * ncols * 2;
     return mi_act_q8_bytes(K, ncols, kind == 1);
 }
@@ -573,7 +579,9 @@ static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, in
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
     void * dev = scratch_take(ctx, act_bytes(kind, K, ncols));
     const mi_src_cols x = src_cols(src1);
-    if (kind == 2 || kind == 5) {
+    if (kind == 8) {
+        mi_quantize_q8_K_mmx(x, K, mi_act_mmx_carve(dev, K, ncols), ctx->stream);
+    } else if (kind == 2 || kind == 5) {
         mi_convert_f16(x, K, (uint16_t *) dev, ctx->stream, kind == 5);
     } else if (kind >= 3) {
         mi_quantize_expand_f16(x, K, ncols, kind == 4 || kind == 7, (uint16_t *) dev, ctx->stream, kind >= 6);
@@ -643,7 +651,14 @@ static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const vo
         static const bool no_mmq = getenv("GGML_MI355X_NO_MMQ") != nullptr;
         const bool batched = !no_mmq && src1->ne[1] > 8 && m.ne02 == 1 && m.ne03 == 1 && m.ne12 == 1 && m.ne13 == 1 &&
                              mi_mmq_supported(m.type, m.K, m.nb01, m.nb1) && ((uintptr_t) m.W % 16) == 0;
-        if (batched) {
+        // Q4_K / Q5_K: the exact-integer int8 MFMA GEMM (mmq_exact.hip); GGML_MI355X_MMQ_VARIANT
+        // bit 32 selects the f16 GEMM below instead (A/B timing)
+        const bool exact = batched && kind == 1 && (g_mi_tuning.mmq_variant & 32) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1);
+        if (exact) {
+            const int64_t nc = ncols;
+            mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, mi_act_mmx_carve(get_activations(ctx, src1, 8, m.K), m.K, nc), m.dst,
+                            m.nb1, ctx->stream);
+        } else if (batched) {
             // the GEMM's activation operand: f16 for F16 weights, else f16(d * q) of the q8 quants
             // written by the quantizer itself (kinds 3/4)
             const bool blk = mi_mmq_wants_blocked();
@@ -713,7 +728,9 @@ static void op_mul_mat_split(mi_backend_ctx * ctx, ggml_tensor * dst) {
     for (const auto & sl : extra->slices) {
         const int64_t rows = sl.row_high - sl.row_low;
         float * out = (float *) ((char *) dst->data + sl.row_low * sizeof(float));
-        if (sl.slot == ctx->device) {
+        // the backend's own slot (the first slot placed on its device) runs in place; further
+        // slots on the same device (GGML_MI355X_SPLIT_SLOTS > device count) take the copy path
+        if (sl.device == ctx->device && sl.slot == ctx->device % split_slots()) {
             mul_mat_run(ctx, src0, sl.ptr, rows, src1, out, dst->nb[1], dst->nb[2], dst->nb[3]);
             continue;
         }
@@ -919,7 +936,10 @@ static size_t graph_scratch_bytes(const ggml_cgraph * cgraph) {
         const int64_t ncols = b->ne[1] * b->ne[2] * b->ne[3];
         // q8 blocks and/or their f16 expansion (batched) -- both counted, the choice is made at run time
         total += (act_bytes(kind, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
-        if (ncols > 8) total += (act_bytes(kind + 3, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+        if (ncols > 8) {
+            const size_t big = std::max(act_bytes(kind + 3, b->ne[0], ncols), kind == 1 ? act_bytes(8, b->ne[0], ncols) : 0);
+            total += (big + kBufferAlign - 1) & ~(kBufferAlign - 1);
+        }
     }
     return total;
 }
@@ -1001,9 +1021,15 @@ static int run_fused_group(mi_backend_ctx * ctx, ggml_cgraph * cgraph, int i) {
 // An intermediate may be skipped only if the next node is its sole consumer and it is not a graph
 // output; views of a tensor count as consumers of it.
 
+// A graph handed over by ggml_backend_sched is a view of one split (ggml_graph_view,
+// ggml-backend.c:1549; size == 0, no hash table): a tensor may also be read by a later split that
+// this backend never sees, so no use count taken over the view proves an intermediate private and
+// every node output is stored (`partial`).
 struct mi_uses {
     std::unordered_map<const ggml_tensor *, int> n;
+    bool partial = false;
     int of(const ggml_tensor * t) const {
+        if (partial) return 1 << 20;
         auto it = n.find(t);
         return it == n.end() ? 0 : it->second;
     }
@@ -1013,6 +1039,7 @@ struct mi_uses {
 // counts once for X (as the view) and once per consumer for V
 static void count_uses(const ggml_cgraph * g, mi_uses & u) {
     u.n.clear();
+    u.partial = g->size == 0 && g->visited_hash_table.size == 0;
     for (int i = 0; i < g->n_nodes; i++) {
         const ggml_tensor * t = g->nodes[i];
         for (int s = 0; s < GGML_MAX_SRC; s++) {
@@ -1435,6 +1462,27 @@ static void plan_attention(const ggml_cgraph * g, const mi_uses & u, std::vector
             pl.q_src.ne[3] = 1;
             pl.q_src.nb[3] = 0;
         }
+        // Q, K and V are now read at the KQV node instead of at cont(Q) (or the copy that replaces
+        // it), KQ and cont(V): no node that still runs in between may write over them
+        std::vector<uint8_t> mine(g->n_nodes, 0);
+        for (int a : absorbed_ids) mine[a] = 1;
+        auto clobbered = [&](int from, const char * xlo, const char * xhi) {
+            for (int k = from + 1; k < j; k++) {
+                const ggml_tensor * n = g->nodes[k];
+                if (mine[k] || absorbed_nodes[k] || is_noop(n) || !n->data) continue;
+                const char * nlo = (const char *) n->data;
+                if (nlo < xhi && xlo < nlo + ggml_nbytes(n)) return true;
+            }
+            return false;
+        };
+        strided_range(d.k, kne, d.k_nb, 3, &lo, &hi);
+        if (clobbered(node_index(g, kq, idx), lo, hi)) MI_ATTN_SKIP("check 18")
+        strided_range(d.v, vne, d.v_nb, 3, &lo, &hi);
+        if (clobbered(node_index(g, vt, idx), lo, hi)) MI_ATTN_SKIP("check 19")
+        if (pl.q_copy_at < 0) {
+            strided_range(d.q, qne, d.q_nb, 3, &lo, &hi);
+            if (clobbered(node_index(g, qc, idx), lo, hi)) MI_ATTN_SKIP("check 20")
+        }
         for (int a : absorbed_ids) absorbed_nodes[a] = 1;
         plans.push_back(pl);
     }
@@ -1804,8 +1852,6 @@ ggml_backend_t ggml_backend_mi355x_init(int device) {
         MI_CHECK(hipStreamCreate(&ctx->stream));
         op_tables(ctx);
     }
-    const char * no_graphs = getenv("GGML_MI355X_DISABLE_GRAPHS");
-    ctx->graph_capture = !(no_graphs && atoi(no_graphs) != 0);
     auto * backend = new ggml_backend{mi_guid(), k_mi_backend_i, ctx};
     return backend;
 }
@@ -1813,11 +1859,6 @@ ggml_backend_t ggml_backend_mi355x_init(int device) {
 void * ggml_backend_mi355x_get_stream(ggml_backend_t backend) {
     MI_ASSERT(ggml_backend_is_mi355x(backend));
     return ((mi_backend_ctx *) backend->context)->stream;
-}
-
-void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable) {
-    MI_ASSERT(ggml_backend_is_mi355x(backend));
-    ((mi_backend_ctx *) backend->context)->graph_capture = enable;
 }
 
 int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend) {

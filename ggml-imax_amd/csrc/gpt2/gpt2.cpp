@@ -69,6 +69,7 @@ struct gpt2_model {
     ggml_tensor * embd_in = nullptr, * pos_in = nullptr;  // persistent input tensors
     void * sched = nullptr;                     // ggml_backend_sched_t
     int n_gpu_layers = 0;
+    int sched_flags = 0;                        // GPT2_SCHED_*
 };
 
 namespace {
@@ -86,7 +87,13 @@ bool place_weights_sched(gpt2_model & m) {
         ggml_backend_t b = cpu;
         if (name == "model/wte" || name == "model/wpe") b = m.n_gpu_layers > m.hp.n_layer ? gpu : cpu;
         else if (name == "model/ln_f/g" || name == "model/ln_f/b" || name == "model/lm_head") b = m.n_gpu_layers > 0 ? gpu : cpu;
-        else if (name.compare(0, 7, "model/h") == 0) b = std::stoi(name.substr(7, 2)) >= first_gpu_layer ? gpu : cpu;
+        else if (name.compare(0, 7, "model/h") == 0) {
+            const int il = std::stoi(name.substr(7, 2));
+            b = il >= first_gpu_layer ? gpu : cpu;
+            // GPT2_SCHED_SPLIT_MID: the previous layer's attention half on the GPU too
+            if ((m.sched_flags & GPT2_SCHED_SPLIT_MID) && il == first_gpu_layer - 1 &&
+                (name.find("/attn/") != std::string::npos || name.find("/ln_1/") != std::string::npos)) b = gpu;
+        }
         where[kv.second] = b;
     }
     for (ggml_backend_t b : m.backends) {
@@ -414,6 +421,11 @@ gpt2_model * gpt2_model_load(const char * fname, ggml_backend_t backend, int n_c
 
 gpt2_model * gpt2_model_load_sched(const char * fname, ggml_backend_t * backends, int n_backends, int n_gpu_layers, int n_ctx,
                                    int n_batch) {
+    return gpt2_model_load_sched_ex(fname, backends, n_backends, n_gpu_layers, n_ctx, n_batch, 0, nullptr);
+}
+
+gpt2_model * gpt2_model_load_sched_ex(const char * fname, ggml_backend_t * backends, int n_backends, int n_gpu_layers,
+                                      int n_ctx, int n_batch, int flags, ggml_backend_buffer_type_t input_buft) {
 #ifdef GPT2_WITH_SCHED
     if (!backends || n_backends < 1) {
         fprintf(stderr, "gpt2_model_load_sched: no backends\n");
@@ -423,6 +435,7 @@ gpt2_model * gpt2_model_load_sched(const char * fname, ggml_backend_t * backends
     m->backends.assign(backends, backends + n_backends);
     m->backend = backends[n_backends - 1];
     m->n_gpu_layers = n_backends > 1 ? n_gpu_layers : 0;
+    m->sched_flags = flags;
     if (!load_file(*m, fname, n_ctx)) {
         gpt2_model_free(m);
         return nullptr;
@@ -436,13 +449,14 @@ gpt2_model * gpt2_model_load_sched(const char * fname, ggml_backend_t * backends
         ggml_set_name(m->embd_in, "in/embd");
         ggml_set_name(m->pos_in, "in/position");
         ggml_backend_t be_in = m->n_gpu_layers >= m->hp.n_layer ? m->backends.front() : m->backends.back();
-        m->buffer_input = ggml_backend_alloc_ctx_tensors(m->ctx_in, be_in);
+        m->buffer_input = input_buft ? ggml_backend_alloc_ctx_tensors_from_buft(m->ctx_in, input_buft)
+                                     : ggml_backend_alloc_ctx_tensors(m->ctx_in, be_in);
         if (!m->buffer_input) {
             gpt2_model_free(m);
             return nullptr;
         }
     }
-    auto * sched = ggml_backend_sched_new(m->backends.data(), nullptr, n_backends, kMaxNodes, false);
+    auto * sched = ggml_backend_sched_new(m->backends.data(), nullptr, n_backends, kMaxNodes, (flags & GPT2_SCHED_PARALLEL) != 0);
     m->sched = sched;
     const int n_tokens = std::min(m->hp.n_ctx, n_batch > 0 ? n_batch : 8);
     ggml_cgraph * gf = build_graph(*m, m->hp.n_ctx - n_tokens, n_tokens);
@@ -453,7 +467,8 @@ gpt2_model * gpt2_model_load_sched(const char * fname, ggml_backend_t * backends
     }
     return m;
 #else
-    (void) fname; (void) backends; (void) n_backends; (void) n_gpu_layers; (void) n_ctx; (void) n_batch;
+    (void) fname; (void) backends; (void) n_backends; (void) n_gpu_layers; (void) n_ctx; (void) n_batch; (void) flags;
+    (void) input_buft;
     fprintf(stderr, "gpt2_model_load_sched: this build has no ggml_backend_sched (link the driver against a libggml "
                     "that provides it, e.g. oracle/_ref/libgpt2_ref.so)\n");
     return nullptr;

@@ -130,6 +130,25 @@ size_t mi_mmq_scratch_bytes(int type, int64_t K, int64_t ncols);
 void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_q8 & act, const uint16_t * xh,
                     int64_t ncols, float * dst, size_t ycol, uint16_t * scratch, hipStream_t s);
 
+// ---- exact-integer prefill GEMM for Q4_K / Q5_K (mmq_exact.hip) ----
+// q8_K activation quants in the int8-MFMA layouts: xq [K/64][ncols][64] int8, xd [K/256][ncols]
+// f32 scale, xu [K/256][ncols][16] f16 (S_j & 63, S_j >> 6; S_j = sum of the 32 quants of
+// sub-block j) -- the bytes of quantize_row_q8_K_reference, rearranged
+struct mi_act_mmx {
+    int8_t * xq;
+    float * xd;
+    uint16_t * xu;
+    int64_t K;
+    int64_t ncols;
+};
+size_t mi_act_mmx_bytes(int64_t K, int64_t ncols);
+mi_act_mmx mi_act_mmx_carve(void * base, int64_t K, int64_t ncols);
+void mi_quantize_q8_K_mmx(const mi_src_cols & x, int64_t K, const mi_act_mmx & act, hipStream_t s);
+bool mi_mmqx_supported(int type, int64_t K, size_t ycol);
+// 2-D Q4_K / Q5_K weights [K, N] x act.ncols columns -> dst (column stride ycol bytes)
+void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_mmx & act, float * dst,
+                     size_t ycol, hipStream_t s);
+
 // ---- companion ops (ops.hip) ----
 // a tensor view as the element-wise kernels see it: f32 (type 0), f16 (1) or i32 (26) elements
 struct mi_tensor_desc {

@@ -228,7 +228,6 @@ _SIGS = {
     "ggml_backend_mi355x_get_device_memory": ([c_int, POINTER(c_size_t), POINTER(c_size_t)], None),
     "ggml_backend_mi355x_reg_devices": ([], c_int),
     "ggml_backend_mi355x_get_stream": ([c_void_p], c_void_p),
-    "ggml_backend_mi355x_set_graph_capture": ([c_void_p, c_bool], None),
     "ggml_backend_mi355x_last_launch_count": ([c_void_p], c_int),
     "ggml_backend_mi355x_set_tuning": ([c_char_p, c_int], c_bool),
     "ggml_backend_mi355x_quantize_activations": ([c_void_p, c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p], c_bool),
@@ -236,6 +235,7 @@ _SIGS = {
     "gpt2_model_load": ([c_char_p, c_void_p, c_int, c_int], c_void_p),
     "gpt2_model_free": ([c_void_p], None),
     "gpt2_model_load_sched": ([c_char_p, c_void_p, c_int, c_int, c_int, c_int], c_void_p),
+    "gpt2_model_load_sched_ex": ([c_char_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p], c_void_p),
     "gpt2_sched_n_splits": ([c_void_p], c_int),
     "gpt2_model_hparams": ([c_void_p, c_void_p], None),
     "gpt2_model_size": ([c_void_p], c_size_t),

@@ -51,10 +51,6 @@ GGML_API int ggml_backend_mi355x_reg_devices(void);
 // hipStream_t the backend launches on (for external timing with HIP events / stream interop)
 GGML_API void * ggml_backend_mi355x_get_stream(ggml_backend_t backend);
 
-// Graph-replay switch kept for parity with GGML_CUDA_DISABLE_GRAPHS (env GGML_MI355X_DISABLE_GRAPHS);
-// replay is not implemented: the decode token keeps the GPU busy, so launch overhead is hidden.
-GGML_API void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable);
-
 // Number of kernels launched by the last graph_compute (for tests / profiling).
 GGML_API int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend);
 

@@ -34,6 +34,18 @@ GGML_API struct gpt2_model * gpt2_model_load(const char * fname, ggml_backend_t 
 // other builds return NULL with a message.
 GGML_API struct gpt2_model * gpt2_model_load_sched(const char * fname, ggml_backend_t * backends, int n_backends, int n_gpu_layers,
                                                    int n_ctx, int n_batch);
+// The same with scheduler options (all off = gpt2_model_load_sched):
+//   GPT2_SCHED_PARALLEL   ggml_backend_sched_new(..., parallel = true): input copies + backend
+//                         events (ggml-backend.c:1647-1710, :1751-1755)
+//   GPT2_SCHED_SPLIT_MID  the attention weights of the last CPU layer go to the GPU as well, so a
+//                         split boundary falls inside a layer (between attention and MLP)
+// input_buft: buffer type of the persistent input tensors (NULL = main-sched.cpp's choice), e.g.
+// ggml_backend_mi355x_host_buffer_type() for pinned host inputs read by both backends.
+#define GPT2_SCHED_PARALLEL  1
+#define GPT2_SCHED_SPLIT_MID 2
+GGML_API struct gpt2_model * gpt2_model_load_sched_ex(const char * fname, ggml_backend_t * backends, int n_backends,
+                                                      int n_gpu_layers, int n_ctx, int n_batch, int flags,
+                                                      ggml_backend_buffer_type_t input_buft);
 GGML_API int gpt2_sched_n_splits(const struct gpt2_model * model);
 GGML_API void gpt2_model_free(struct gpt2_model * model);
 GGML_API void gpt2_model_hparams(const struct gpt2_model * model, struct gpt2_hparams_c * out);

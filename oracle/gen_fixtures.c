@@ -165,6 +165,14 @@ int main(int argc, char ** argv) {
     run_case("L_q8_0_4096x11008", GGML_TYPE_Q8_0, 4096, 11008, 1, 42, 43, 1, 8);
     run_case("L_f32_256x256", GGML_TYPE_F32, 256, 256, 256, 42, 43, 1, 8);
     run_case("L_q4_K_4096x4096_b8", GGML_TYPE_Q4_K, 4096, 4096, 8, 42, 43, 1, 8);
+    // prefill (configs[4], B=512) and the mid-batch sizes: Y is kept as its SHA-256 plus sampled
+    // columns (tests/golden/make_golden.py); X = the first B columns of the seed-43 stream
+    run_case("P_q4_K_4096x4096_b512", GGML_TYPE_Q4_K, 4096, 4096, 512, 42, 43, 1, 8);
+    run_case("P_q4_K_4096x4096_b64", GGML_TYPE_Q4_K, 4096, 4096, 64, 42, 43, 1, 8);
+    run_case("P_q4_K_4096x4096_b32", GGML_TYPE_Q4_K, 4096, 4096, 32, 42, 43, 1, 8);
+    run_case("P_q4_K_4096x4096_b16", GGML_TYPE_Q4_K, 4096, 4096, 16, 42, 43, 1, 8);
+    run_case("P_q4_K_4096x4096_b9", GGML_TYPE_Q4_K, 4096, 4096, 9, 42, 43, 1, 8);
+    run_case("P_q5_K_4096x11008_b64", GGML_TYPE_Q5_K, 4096, 11008, 64, 42, 43, 1, 8);
 
     fprintf(g_manifest, "\n]\n");
     fclose(g_manifest);

@@ -4,7 +4,10 @@ MI355X backend plugin and the GPT-2 driver built against the reference, all in o
 reference scheduler with n_gpu_layers of the 12 layers on MI355X0 and the rest on the reference
 CPU backend, and writes the logits of each configuration to <out>/<tag>.npy.
 
-usage: python tests/_sched_child.py <model> <out_dir> <n_gpu_layers>[,<n_gpu_layers>...]
+usage: python tests/_sched_child.py <model> <out_dir> <spec>[,<spec>...]
+  spec = n_gpu_layers[:flags[:h]] -- flags = GPT2_SCHED_* bits (1 parallel scheduler with events,
+  2 split inside a layer); h = persistent inputs in ggml_backend_mi355x_host_buffer_type() (pinned).
+  Output file: <out_dir>/ngl<spec with ':' -> '_'>.npy
 """
 import os
 import sys
@@ -20,16 +23,21 @@ REF = os.path.join(REPO, "oracle", "_ref")
 
 
 def main():
-    model_path, out_dir, layers = sys.argv[1], sys.argv[2], [int(v) for v in sys.argv[3].split(",")]
+    model_path, out_dir, specs = sys.argv[1], sys.argv[2], sys.argv[3].split(",")
+    layers = [int(v.split(":")[0]) for v in specs]
     lib = G.Lib([os.path.join(REF, "libggml_ref.so"), G.BACKEND_LIB, os.path.join(REF, "libgpt2_ref.so")])
     cpu = lib.ggml_backend_cpu_init()
     lib.ggml_backend_cpu_set_n_threads(cpu, min(16, os.cpu_count() or 1))
     gpu = lib.ggml_backend_mi355x_init(0) if max(layers) > 0 else None
     assert gpu or max(layers) == 0, "ggml_backend_mi355x_init failed"
     prompt = "Once upon a time the cat sat on the mat and the dog"
-    for ngl in layers:
+    for spec in specs:
+        parts = spec.split(":")
+        ngl = int(parts[0])
+        flags = int(parts[1]) if len(parts) > 1 else 0
+        in_buft = lib.ggml_backend_mi355x_host_buffer_type() if len(parts) > 2 and parts[2] == "h" else None
         arr = (G.c_void_p * 2)(gpu, cpu) if ngl > 0 else (G.c_void_p * 1)(cpu)
-        m = lib.gpt2_model_load_sched(model_path.encode(), arr, 2 if ngl > 0 else 1, ngl, 1024, 8)
+        m = lib.gpt2_model_load_sched_ex(model_path.encode(), arr, 2 if ngl > 0 else 1, ngl, 1024, 8, flags, in_buft)
         assert m, "gpt2_model_load_sched failed"
         splits = lib.gpt2_sched_n_splits(m)
         wrap = gpt2.Model.__new__(gpt2.Model)
@@ -46,8 +54,8 @@ def main():
             n_past += 1
             nxt = int(np.argmax(lg[-1]))
         splits = max(splits, lib.gpt2_sched_n_splits(m))
-        np.save(os.path.join(out_dir, f"ngl{ngl}.npy"), np.concatenate(outs))
-        print(f"n_gpu_layers={ngl}: splits={splits}")
+        np.save(os.path.join(out_dir, "ngl" + spec.replace(":", "_") + ".npy"), np.concatenate(outs))
+        print(f"n_gpu_layers={spec}: splits={splits}")
         lib.gpt2_model_free(m)
         wrap.m = None
     if gpu:

@@ -22,8 +22,10 @@ def load_manifest():
         return json.load(f)
 
 
-def golden_cases(large=None):
-    cs = load_manifest()["cases"]
+def golden_cases(large=None, prefill=False):
+    """Golden mul_mat cases; prefill=True selects the P_* cases (prefill-sized Y kept as its
+    SHA-256 + sampled columns), which the other selections leave out."""
+    cs = [c for c in load_manifest()["cases"] if c["name"].startswith("P_") == prefill]
     if large is None:
         return cs
     return [c for c in cs if bool(c["large"]) == large]

@@ -21,6 +21,8 @@ import subprocess
 import sys
 import tempfile
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 
@@ -35,11 +37,19 @@ def main() -> int:
             wq = os.path.join(tmp, c["name"] + ".wq.bin")
             c["wq_sha256"] = hashlib.sha256(open(wq, "rb").read()).hexdigest()
             c["wq_bytes"] = os.path.getsize(wq)
+            if c["name"].startswith("P_"):
+                # prefill-sized outputs: SHA-256 of the whole Y [B][N] plus every step-th column
+                y = np.fromfile(os.path.join(tmp, c["name"] + ".y.f32"), np.float32).reshape(c["B"], c["N"])
+                c["y_sha256"] = hashlib.sha256(y.tobytes()).hexdigest()
+                c["y_col_step"] = step = max(1, c["B"] // 32)
+                np.ascontiguousarray(y[::step]).tofile(os.path.join(HERE, c["name"] + ".ys.f32"))
         for fn in sorted(os.listdir(tmp)):
             if fn == "cases.json":
                 continue
-            if fn.startswith("L_") and fn.endswith(".wq.bin"):
+            if fn.startswith(("L_", "P_")) and fn.endswith(".wq.bin"):
                 continue  # large weights: hash only
+            if fn.startswith("P_") and fn.endswith(".y.f32"):
+                continue  # hash + sampled columns only
             shutil.copy(os.path.join(tmp, fn), os.path.join(HERE, fn))
         manifest = {
             "generator": "oracle/gen_fixtures.c linked to oracle/_ref/libggml_ref.so",

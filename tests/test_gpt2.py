@@ -371,3 +371,22 @@ def test_gpt2_partial_offload_under_reference_scheduler(model_path, tmp_path):
     import re
     splits = {int(a): int(b) for a, b in re.findall(r"n_gpu_layers=(\d+): splits=(\d+)", out)}
     assert splits[6] > 1 and splits[3] > 1  # the graph really crosses devices
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+def test_gpt2_scheduler_options_host_inputs_events_mid_layer_split(model_path, tmp_path):
+    """The rest of the scheduler contract: the pinned host buffer type holding the persistent
+    inputs (its supports_backend delegates to the CPU buffer type, ggml-cuda.cu:1037-1038),
+    parallel=true (input copies + the backend event vtable, ggml-backend.c:1647-1710) and a split
+    boundary inside a layer (attention on MI355X0, MLP on the CPU), where a tensor read by both
+    splits must be stored by the first. Logits bit-identical to the CPU-only run."""
+    specs = ["0", "6:0:h", "6:1", "6:1:h", "6:2", "12:1:h"]
+    out = _run_sched_child(model_path, tmp_path, specs)
+    print(out)
+    base = np.load(tmp_path / "ngl0.npy")
+    for spec in specs[1:]:
+        got = np.load(tmp_path / ("ngl" + spec.replace(":", "_") + ".npy"))
+        diff = float(np.max(np.abs(got - base)))
+        print(f"{spec}: max |d| = {diff:.3e}")
+        assert np.array_equal(got.view(np.uint32), base.view(np.uint32)), (spec, diff)

@@ -92,6 +92,25 @@ def test_large_weights_hash_and_output(c):
         assert err <= 1e-5, err
 
 
+PREFILL = golden_cases(large=True, prefill=True)
+
+
+@pytest.mark.parametrize("c", PREFILL, ids=[c["name"] for c in PREFILL])
+def test_prefill_fixture_columns_vs_restatement(c):
+    """The P_* fixtures (prefill-sized Y: SHA-256 + every step-th column) against the CPU
+    restatement on those columns: same weight bytes, outputs within 1e-5."""
+    K, N, B = c["K"], c["N"], c["B"]
+    w, x = _inputs(c)
+    q = orc.quantize(c["type"], w, K)
+    assert hashlib.sha256(q.tobytes()).hexdigest() == c["wq_sha256"]
+    step = c["y_col_step"]
+    xs = np.ascontiguousarray(x.reshape(B, K)[::step])
+    ys = golden_blob(c["name"] + ".ys.f32", np.float32).reshape(-1, N)
+    y = orc.mul_mat(c["type"], q, K, N, xs.ravel(), xs.shape[0]).reshape(-1, N)
+    err = np.abs(y - ys).max() / np.abs(ys).max()
+    assert err <= 1e-5, err
+
+
 def test_mul_mat_exact_plumbing():
     """tests/test-mul-mat.cpp:262-298 style: integer-valued f32 operands give exact results."""
     rng = np.random.default_rng(0)

@@ -1,0 +1,135 @@
+"""Batched (prompt / prefill) GGML_OP_MUL_MAT at BASELINE sizes: configs[4] (Q4_K 4096x4096,
+B=512, prompt-sharded over GPUs) and the mid-batch sizes B in {9, 16, 32, 64}.
+
+The reference outputs are the P_* golden cases (tests/golden/make_golden.py, written by the
+reference CPU mul_mat, ggml.c:11808-12097 -> vec_dot_q4_K_q8_K, ggml-quants.c:7089-7152): the
+SHA-256 of the whole Y plus every step-th column. Three checks:
+  * the sampled columns, element-wise, within 1e-5 of max|y| (the prefill GEMM computes the
+    reference's exact integer block sums; only the f32 combine order differs);
+  * the WHOLE Y at full size: the decode GEMV in mmv_order=1 is bit-identical to the reference
+    CPU (test_mul_mat_gpu.py), so its 8-column slices reassemble the reference Y -- its SHA-256
+    must equal the fixture's -- and every element of the prefill Y is checked against it;
+  * prompt sharding (configs[4] on 8 GPUs, 64 columns each): the column shards computed alone
+    concatenate to the unsharded result bit for bit.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import golden_blob, golden_cases
+import pyoracle as orc
+from ggml_mi355x import ggml as G
+from ggml_mi355x import synth
+
+pytestmark = pytest.mark.gpu
+
+PREFILL = golden_cases(large=True, prefill=True)
+EXACT_TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def rt():
+    return G.runtime()
+
+
+@pytest.fixture(scope="module")
+def backend(rt):
+    b = G.mi355x_backend(rt, 0)
+    yield b
+    rt.ggml_backend_free(b)
+
+
+def rel_err(y, ref):
+    return float(np.abs(y.astype(np.float64) - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+def _inputs(rt, c):
+    K, N, B = c["K"], c["N"], c["B"]
+    w = synth.uniform(c["wseed"], K * N)
+    wq = np.empty(c["wq_bytes"], np.uint8)
+    rt.ggml_quantize_chunk(c["type"], w.ctypes.data, wq.ctypes.data, 0, N, K, None)
+    assert hashlib.sha256(wq.tobytes()).hexdigest() == c["wq_sha256"], "runtime quantizer != reference bytes"
+    return wq, synth.uniform(c["xseed"], K * B)
+
+
+def _reference_y_by_gemv(rt, backend, t, wq, K, N, x, B):
+    """Y [B, N] from the bit-exact decode path (mmv_order=1), 8 columns per mul_mat."""
+    assert rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 1)
+    try:
+        xs = x.reshape(B, K)
+        cols = [G.mul_mat_once(rt, backend, t, wq, K, N, np.ascontiguousarray(xs[c0:c0 + 8]).ravel(), min(8, B - c0))
+                for c0 in range(0, B, 8)]
+    finally:
+        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
+    return np.concatenate(cols).reshape(B, N)
+
+
+@pytest.mark.parametrize("c", PREFILL, ids=[c["name"] for c in PREFILL])
+def test_prefill_matches_reference_at_full_size(rt, backend, c):
+    K, N, B, t = c["K"], c["N"], c["B"], c["type"]
+    wq, x = _inputs(rt, c)
+    y = G.mul_mat_once(rt, backend, t, wq, K, N, x, B).reshape(B, N)
+    step = c["y_col_step"]
+    ys = golden_blob(c["name"] + ".ys.f32", np.float32).reshape(-1, N)
+    err_s = rel_err(y[::step], ys)
+    yref = _reference_y_by_gemv(rt, backend, t, wq, K, N, x, B)
+    assert hashlib.sha256(yref.tobytes()).hexdigest() == c["y_sha256"], "GEMV reassembly != reference Y"
+    err = rel_err(y, yref)
+    same = float(np.mean(y.view(np.uint32) == yref.view(np.uint32)))
+    print(f"{c['name']}: sampled columns {err_s:.2e}, whole Y {err:.2e}, bit-identical elements {same:.3f}")
+    assert err_s <= EXACT_TOL, err_s
+    assert err <= EXACT_TOL, err
+
+
+@pytest.mark.parametrize("world", [8, 3])
+def test_prompt_sharded_prefill_equals_whole(rt, backend, world):
+    """configs[4] prompt sharding: shard_range(512, world, r) columns per rank, each computed alone
+    (as each GPU does), concatenate to the whole B=512 product bit for bit."""
+    import bench
+    c = next(cc for cc in PREFILL if cc["B"] == 512)
+    K, N, B, t = c["K"], c["N"], c["B"], c["type"]
+    wq, x = _inputs(rt, c)
+    whole = G.mul_mat_once(rt, backend, t, wq, K, N, x, B).reshape(B, N)
+    xs = x.reshape(B, K)
+    parts = []
+    for r in range(world):
+        s0, cnt = bench.shard_range(B, world, r)
+        parts.append(G.mul_mat_once(rt, backend, t, wq, K, N, np.ascontiguousarray(xs[s0:s0 + cnt]).ravel(), cnt).reshape(cnt, N))
+    sharded = np.concatenate(parts)
+    assert np.array_equal(sharded.view(np.uint32), whole.view(np.uint32)), rel_err(sharded, whole)
+
+
+@pytest.mark.parametrize("tname", ["q4_K", "q5_K"])
+@pytest.mark.parametrize("K,N,B", [(256, 64, 9), (512, 100, 130), (768, 2304, 24), (3072, 768, 40), (1280, 96, 257)])
+def test_prefill_exact_gemm_shapes_vs_oracle(rt, backend, tname, K, N, B):
+    """Ragged tiles (N, B not multiples of 64 / 128), odd superblock counts (the canonical chain
+    split puts the extra superblock in the second half), one-superblock rows."""
+    t = orc.TYPES_BY_NAME[tname]
+    w = synth.uniform(K * 7 + N, K * N)
+    x = synth.uniform(K * 3 + B, K * B)
+    wq = orc.quantize(t, w, K)
+    y = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
+    ref = orc.mul_mat(t, wq, K, N, x, B)
+    err = rel_err(y, ref)
+    print(f"{tname} {K}x{N}x{B}: {err:.2e}")
+    assert err <= EXACT_TOL, err
+
+
+def test_prefill_edge_values(rt, backend):
+    """All-zero activation superblocks (d = 0), constant weight rows (d_w = 0, mins only) and
+    saturated quants: the exact-integer path against the oracle."""
+    t, K, N, B = orc.Q4_K, 1024, 96, 40
+    w = synth.uniform(5, K * N).reshape(N, K)
+    w[3] = 0.25          # constant rows: every sub-block scale 0, mins carry the value
+    w[7] = 0.0
+    w[11, :256] = 1.0    # one constant superblock
+    x = synth.uniform(6, K * B).reshape(B, K)
+    x[2] = 0.0           # all-zero columns / superblocks
+    x[5, 256:512] = 0.0
+    x[9] = np.where(np.arange(K) % 2, 1e3, -1e3)  # saturated quants
+    wq = orc.quantize(t, np.ascontiguousarray(w).ravel(), K)
+    y = G.mul_mat_once(rt, backend, t, wq, K, N, np.ascontiguousarray(x).ravel(), B)
+    ref = orc.mul_mat(t, wq, K, N, np.ascontiguousarray(x).ravel(), B)
+    assert np.all(np.isfinite(y))
+    assert rel_err(y, ref) <= EXACT_TOL

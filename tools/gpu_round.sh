@@ -20,3 +20,8 @@ find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \
 head -8 "$OUT/kernel_stats.csv" | cut -c1-200
 timeout -k 10 300 python tools/pmc_traffic.py --tag "$TAG" > "$OUT/pmc.log" 2>&1
 tail -5 "$OUT/pmc.log"
+# GPT-2 decode kernel trace (per-token launch mix)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_gpt2" -o run --output-format csv -- \
+  python3 tools/gpt2_prof.py 64 > "$OUT/gpt2_prof.log" 2>&1
+find "$OUT/prof_gpt2" -name '*kernel_stats.csv' -exec cp {} "$OUT/gpt2_kernel_stats.csv" \;
+cat "$OUT/gpt2_prof.log" | tail -4
