@@ -653,7 +653,7 @@ static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const vo
                              mi_mmq_supported(m.type, m.K, m.nb01, m.nb1) && ((uintptr_t) m.W % 16) == 0;
         // Q4_K / Q5_K: the exact-integer int8 MFMA GEMM (mmq_exact.hip); GGML_MI355X_MMQ_VARIANT
         // bit 32 selects the f16 GEMM below instead (A/B timing)
-        const bool exact = batched && kind == 1 && (g_mi_tuning.mmq_variant & 32) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1);
+        const bool exact = batched && kind == 1 && (g_mi_tuning.mmq_variant & 32) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01);
         if (exact) {
             const int64_t nc = ncols;
             mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, mi_act_mmx_carve(get_activations(ctx, src1, 8, m.K), m.K, nc), m.dst,

@@ -144,7 +144,7 @@ struct mi_act_mmx {
 size_t mi_act_mmx_bytes(int64_t K, int64_t ncols);
 mi_act_mmx mi_act_mmx_carve(void * base, int64_t K, int64_t ncols);
 void mi_quantize_q8_K_mmx(const mi_src_cols & x, int64_t K, const mi_act_mmx & act, hipStream_t s);
-bool mi_mmqx_supported(int type, int64_t K, size_t ycol);
+bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t nb01);
 // 2-D Q4_K / Q5_K weights [K, N] x act.ncols columns -> dst (column stride ycol bytes)
 void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_mmx & act, float * dst,
                      size_t ycol, hipStream_t s);

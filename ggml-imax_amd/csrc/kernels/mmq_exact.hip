@@ -17,20 +17,20 @@
 //     (<= 4032), B = [S_j & 63, S_j >> 6] where S_j = sum of 32 q8 (the activation quantizer
 //     writes these), so every product and partial sum is an integer < 2^24: exact.
 // The float combine per superblock and the order of the superblock chain are fixed (mmqx_term
-// and the two-halves chain below) and shared by every kernel of this file, so column shards of a
+// and one chain in superblock order) and shared by every kernel of this file, so column shards of a
 // prompt (prompt-sharded multi-GPU) give the same bits as the whole prompt. Against the
 // reference CPU the only difference is the f32 combine order (reference: 8-lane partial chains
 // + hsum): ~1e-7 relative.
 //
-// Workgroup = 2 groups x 4 wave64s, tile 64 weight rows x 128 columns; group g owns half of the
-// superblocks of K (the canonical chain split) and dequantizes its 64 x 128 weight slab of a stage
-// (half a superblock) into double-buffered LDS planes once for its four waves; each wave owns all
-// 64 rows x its own 32 columns (two 32x32 MFMA tiles sharing one activation fragment), which it
-// loads straight from HBM/L2 into a register ring (16 B per lane per 32-deep K step).
+// Workgroup and pipeline: k_mmqx below. Activation fragments come straight from HBM/L2 into a
+// register ring (16 B per lane per 32-deep K step); the dequantized weight planes are shared by
+// the workgroup's waves through LDS.
 // Roofline: 2*N*K*B flops; at B=512 MFMA-bound. The NP planes make the int8 rate per weight
 // 2 (Q4_K) or 3 (Q5_K) i8 MFMAs per 32 K, i.e. Q4_K runs at the dense f16 rate (2.5 PF/s).
 
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
@@ -170,24 +170,29 @@ void mi_quantize_q8_K_mmx(const mi_src_cols & x, int64_t K, const mi_act_mmx & a
 namespace {
 
 // ---- the GEMM -----------------------------------------------------------------------------------
-// SK = 2: two groups of 4 waves (512 threads, 2 waves per SIMD), group g sums chain half g;
-// SK = 1: one group of 4 waves (256 threads, 1 wave per SIMD with the whole register file), each
-// wave runs both chain halves in turn. PF = stages of weight and activation loads in flight.
-template <int TYPE, int SK, int PF, bool XCD>
-__global__ __launch_bounds__(256 * SK) void k_mmqx(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
-                                                   mi_act_mmx act, float * __restrict__ dst, size_t ycol) {
+// One workgroup = 8 wave64s (two per SIMD), tile 64 weight rows x 128 columns; wave (rw, cw) owns
+// rows 32 rw.. x columns 32 cw.. (one 32x32 tile: one int8 MFMA per plane per 32-deep K step).
+// A stage is one superblock (256 K): the 512 threads dequantize the next superblock's 64 rows
+// (eight lanes per row, each a contiguous 16-byte chunk of its quants: coalesced loads) into
+// the other LDS plane buffer, plus the row operands of the combine. Activations and weights arrive a stage ahead (vmcnt is in-order: every load is
+// consumed in the order it was issued, each with one stage of lead). Two waves per SIMD: while
+// one issues its MFMAs the other runs its dequantization / combine VALU.
+// Canonical combine order (shared by every kernel of this file): one f32 chain over the
+// superblocks in increasing order, y = mmqx_term(y, ...) from y = +0.
+template <int TYPE, bool XCD, int ABL = 0>
+__global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                              mi_act_mmx act, float * __restrict__ dst, size_t ycol) {
     using F = XFmt<TYPE>;
     constexpr int NP = F::NP;
-    constexpr int kPlane = XBM * XROW;                       // one plane of a stage
-    constexpr int kAu = XBM * 32;                            // U operand rows (16 halves each)
-    constexpr int kBuf = NP * kPlane + kAu + XBM * 8;        // + d_w, dmin_w per row
-    constexpr int kRed = 256 * 32 * 4;                       // group 1's partial tile
-    constexpr int kLds = 2 * SK * kBuf > kRed ? 2 * SK * kBuf : kRed;
-    __shared__ __attribute__((aligned(16))) char lds[kLds];
+    constexpr int XR = 256 + 16;             // LDS row stride of a plane (bytes): conflict-free b128 reads / writes
+    constexpr int kPlane = XBM * XR;         // one plane of a superblock
+    constexpr int kRow = XBM * 32 + XBM * 8; // row operands of the combine: U halves, d_w, dmin_w
+    constexpr int kBuf = NP * kPlane + kRow;
+    __shared__ __attribute__((aligned(16))) char lds[2 * kBuf];
 
-    const int grp = SK == 2 ? (int) threadIdx.x >> 8 : 0;
-    const int tid = (int) threadIdx.x & 255;
+    const int tid = (int) threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
+    const int rw = wave & 1, cw = wave >> 1;
     const int64_t ncols = act.ncols;
     int64_t n0, b0;
     {
@@ -203,246 +208,239 @@ __global__ __launch_bounds__(256 * SK) void k_mmqx(const uint8_t * __restrict__ 
         n0 = (t % nrt) * XBM;
         b0 = (t / nrt) * XBN;
     }
-    char * const lds_g = lds + grp * 2 * kBuf;
-
-    // canonical chain split: half 0 sums superblocks [0, S/2), half 1 [S/2, S)
     const int S = (int) (K / 256);
-    const int half = S / 2;
-    const int sb_first = grp ? half : 0;
-    const int n_sb = SK == 1 ? S : (grp ? S - half : half);
-    const int n_sb_max = SK == 1 ? S : S - half;
-    const int nst = 2 * n_sb;  // stages of this group (2 per superblock)
 
-    // staging role: row ar, quarter q of the stage's 128 K (16 bytes of one 64-group's quants)
-    const int ar = tid >> 2, q4 = tid & 3;
-    const int64_t arow = std::min<int64_t>(n0 + ar, N - 1);
-    const uint8_t * wrow = W + arow * nb01;
+    // All global loads go through buffer descriptors with 32-bit per-lane offsets (the host
+    // checks the sizes): one address register per load instead of a 64-bit pointer.
+    // staging role: row ar = tid / 8, 16-byte quant chunk c = tid % 8 of the superblock (eight
+    // lanes read a row's 128 quant bytes contiguously): elements 16 (c & 1).. of sub-blocks
+    // 2 (c / 2) (low nibbles) and 2 (c / 2) + 1 (high nibbles)
+    const int ar = tid >> 3, c8 = tid & 7;
+    const int nrows = (int) std::min<int64_t>(XBM, N - n0);
+    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
+    const uint32_t wrow = (uint32_t) (std::min(ar, nrows - 1) * nb01);
+    const uint32_t qoff = (F::Q5 ? 48 : 16) + 16 * c8;
+    const int j0 = 2 * (c8 >> 1), hf = c8 & 1;
 
-    // activation fragments: column b0 + 32 wave + (lane & 31), 16 bytes at 16 (lane >> 5)
+    // activation fragments: column b0 + 32 cw + (lane & 31), 16 bytes at 16 (lane >> 5)
     const int r = lane & 31, h = lane >> 5;
-    const int64_t bcol = std::min<int64_t>(b0 + 32 * wave + r, ncols - 1);
-    const int8_t * xcol = act.xq + bcol * 64 + 16 * h;
-    const int64_t xstep = ncols * 64;  // bytes per 64-deep K block
+    const uint32_t bcol = (uint32_t) std::min<int64_t>(b0 + 32 * cw + r, ncols - 1);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
+    const uint32_t xcol = bcol * 64 + 16 * h;
+    const uint32_t xstep = (uint32_t) ncols * 64;  // bytes per 64-deep K block
 
-    auto clamp_st = [&](int st) { return st < nst ? st : (nst > 0 ? nst - 1 : 0); };
-    auto load_raw = [&](XRaw<TYPE> & raw, int st) {
-        st = clamp_st(st);
-        const int sb = sb_first + (st >> 1), hs = st & 1;
-        const uint8_t * blk = wrow + (int64_t) sb * F::BS;
-        const int j = 2 * hs + (q4 >> 1);
-        raw.hdr = *(const uint4 *) blk;
-        raw.qs = *(const uint4 *) (blk + (F::Q5 ? 48 : 16) + 32 * j + 16 * (q4 & 1));
-        if constexpr (F::Q5) raw.qh = *(const uint4 *) (blk + 16 + 16 * (q4 & 1));
+    struct Raw {
+        uint4 hdr, qs, qh;
     };
-    // activations of stage st; the second stage of a superblock also brings the superblock's U
-    // operand and scale (one ring, so every load is consumed in issue order: vmcnt is in-order)
-    auto load_x = [&](i32x4 (&xv)[4], half8 & bu, float & da, int st) {
-        st = clamp_st(st);
-        const int sb = sb_first + (st >> 1);
-        const int64_t kb = (int64_t) sb * 4 + 2 * (st & 1);  // first 64-block
+    auto load_raw = [&](Raw & raw, int sb) {
+        sb = sb < S ? sb : S - 1;
+        const uint32_t blk = wrow + (uint32_t) sb * F::BS;
+        raw.hdr = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, blk, 0, 0));
+        raw.qs = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, blk + qoff, 0, 0));
+        if constexpr (F::Q5) raw.qh = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, blk + 16 + 16 * hf, 0, 0));
+    };
+    struct Xs {
+        i32x4 q[8];
+        half8 bu;
+        float da;
+    };
+    auto load_x = [&](Xs & xs, int sb) {
+        sb = sb < S ? sb : S - 1;
+        const uint32_t kb = (uint32_t) sb * 4;  // first 64-block
 #pragma unroll
-        for (int kk = 0; kk < 4; kk++) xv[kk] = *(const i32x4 *) (xcol + (kb + (kk >> 1)) * xstep + 32 * (kk & 1));
-        if (st & 1) {
-            bu = *(const half8 *) (act.xu + ((int64_t) sb * ncols + bcol) * 16 + 8 * h);
-            da = act.xd[(int64_t) sb * ncols + bcol];
-        }
+        for (int kk = 0; kk < 8; kk++)
+            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kb + (kk >> 1)) * xstep + 32 * (kk & 1), 0, 0));
+        const uint32_t sc = (uint32_t) sb * (uint32_t) ncols + bcol;
+        xs.bu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, sc * 32 + 16 * h, 0, 0));
+        xs.da = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, sc * 4, 0, 0));
     };
-    // dequantize this thread's share of stage `st` into LDS buffer `buf`
-    auto store_stage = [&](int buf, const XRaw<TYPE> & raw, int st) {
-        char * base = lds_g + buf * kBuf;
-        const int hs = st & 1;
-        const int j = 2 * hs + (q4 >> 1);
-        int sc0, m0, sc1, m1;
-        mi_scale_min_k4(2 * j, raw.hdr.y, raw.hdr.z, raw.hdr.w, sc0, m0);
-        mi_scale_min_k4(2 * j + 1, raw.hdr.y, raw.hdr.z, raw.hdr.w, sc1, m1);
-        const uint32_t qs[4] = {raw.qs.x, raw.qs.y, raw.qs.z, raw.qs.w};
+    // 6-bit scale / min of sub-block j from the 12 scale bytes (words w0 w1 w2), as
+    // get_scale_min_k4 (ggml-quants.c): field positions fixed per thread, so each is two
+    // bit-field extracts and an or
+    struct KSel {
+        bool hi;
+        uint32_t sh, w, shh, wh;
+    };
+    auto ksel = [](int j) { const int jj = j & 3; const bool hi = j >= 4; return KSel{hi, (uint32_t) (8 * jj), hi ? 4u : 6u, (uint32_t) (8 * jj + 6), hi ? 2u : 0u}; };
+    const KSel k0 = ksel(j0), k1 = ksel(j0 + 1), kc = ksel(c8);
+    auto kscale = [](const KSel & k, uint32_t w0, uint32_t w2) {
+        return __builtin_amdgcn_ubfe(k.hi ? w2 : w0, k.sh, k.w) | (__builtin_amdgcn_ubfe(w0, k.shh, k.wh) << 4);
+    };
+    auto kmin = [](const KSel & k, uint32_t w1, uint32_t w2) {
+        return __builtin_amdgcn_ubfe(k.hi ? w2 : w1, k.hi ? k.sh + 4 : k.sh, k.w) | (__builtin_amdgcn_ubfe(w1, k.shh, k.wh) << 4);
+    };
+    auto store_stage = [&](int buf, const Raw & raw) {
+        if constexpr ((ABL & 1) != 0) return;  // timing ablation: no dequantization
+        char * base = lds + buf * kBuf;
+        const uint32_t sc0 = kscale(k0, raw.hdr.y, raw.hdr.w), sc1 = kscale(k1, raw.hdr.y, raw.hdr.w);
+        const uint32_t q[4] = {raw.qs.x, raw.qs.y, raw.qs.z, raw.qs.w};
+        const uint32_t qh[4] = {raw.qh.x, raw.qh.y, raw.qh.z, raw.qh.w};
         uint32_t lo[4], hi[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            lo[i] = qs[i] & 0x0F0F0F0Fu;
-            hi[i] = (qs[i] >> 4) & 0x0F0F0F0Fu;
+            lo[i] = q[i] & 0x0F0F0F0Fu;
+            hi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
             if constexpr (F::Q5) {
-                const uint32_t qh[4] = {raw.qh.x, raw.qh.y, raw.qh.z, raw.qh.w};
-                lo[i] |= ((qh[i] >> (2 * j)) & 0x01010101u) << 4;
-                hi[i] |= ((qh[i] >> (2 * j + 1)) & 0x01010101u) << 4;
+                lo[i] |= ((qh[i] >> j0) & 0x01010101u) << 4;
+                hi[i] |= ((qh[i] >> (j0 + 1)) & 0x01010101u) << 4;
             }
         }
-        const int off = ar * XROW + 64 * (q4 >> 1) + 16 * (q4 & 1);
+        char * pl0 = base + ar * XR + 32 * j0 + 16 * hf;
 #pragma unroll
         for (int p = 0; p < NP; p++) {
-            const uint32_t f0 = F::factor(sc0, p), f1 = F::factor(sc1, p);
-            char * pl = base + p * kPlane + off;
-            *(uint4 *) pl = make_uint4(mulb(lo[0], f0), mulb(lo[1], f0), mulb(lo[2], f0), mulb(lo[3], f0));
-            *(uint4 *) (pl + 32) = make_uint4(mulb(hi[0], f1), mulb(hi[1], f1), mulb(hi[2], f1), mulb(hi[3], f1));
+            const uint32_t f0 = F::factor((int) sc0, p), f1 = F::factor((int) sc1, p);
+            *(uint4 *) (pl0 + p * kPlane) = make_uint4(mulb(lo[0], f0), mulb(lo[1], f0), mulb(lo[2], f0), mulb(lo[3], f0));
+            *(uint4 *) (pl0 + p * kPlane + 32) = make_uint4(mulb(hi[0], f1), mulb(hi[1], f1), mulb(hi[2], f1), mulb(hi[3], f1));
         }
-        if (hs) return;
-        // (first stage of a superblock) U operand of the row: halves [m_j, 64 m_j] for
-        // j = 2 q4, 2 q4 + 1; and d_w / dmin_w
-        int mA, mB, scA, scB;
-        mi_scale_min_k4(2 * q4, raw.hdr.y, raw.hdr.z, raw.hdr.w, scA, mA);
-        mi_scale_min_k4(2 * q4 + 1, raw.hdr.y, raw.hdr.z, raw.hdr.w, scB, mB);
-        (void) scA;
-        (void) scB;
-        uint2 au;
-        au.x = (uint32_t) mi_f2h((float) mA) | ((uint32_t) mi_f2h((float) (64 * mA)) << 16);
-        au.y = (uint32_t) mi_f2h((float) mB) | ((uint32_t) mi_f2h((float) (64 * mB)) << 16);
-        *(uint2 *) (base + NP * kPlane + ar * 32 + 8 * q4) = au;
-        if (q4 < 2) {
-            float * dwm = (float *) (base + NP * kPlane + kAu);
-            dwm[q4 * XBM + ar] = mi_h2f((uint16_t) (q4 == 0 ? (raw.hdr.x & 0xFFFF) : (raw.hdr.x >> 16)));
-        }
+        // row operands: U halves [m_c, 64 m_c] at slot c; d_w (c = 0), dmin_w (c = 1)
+        char * ro = base + NP * kPlane;
+        const uint32_t mc = kmin(kc, raw.hdr.z, raw.hdr.w);
+        *(uint32_t *) (ro + ar * 32 + 4 * c8) = (uint32_t) mi_f2h((float) mc) | ((uint32_t) mi_f2h((float) (64 * mc)) << 16);
+        if (c8 < 2) ((float *) (ro + XBM * 32))[c8 * XBM + ar] = mi_h2f((uint16_t) (c8 == 0 ? (raw.hdr.x & 0xFFFF) : (raw.hdr.x >> 16)));
     };
 
-    i32x16 acc[2][NP];
-    f32x16 y[2], y1[2];  // y: this group's chain half (SK = 1: half 0), y1: half 1 (SK = 1 only)
-#pragma unroll
-    for (int t = 0; t < 2; t++) y[t] = y1[t] = f32x16{};
-    XRaw<TYPE> raw[PF];
-    i32x4 xb[PF][4];
-    half8 bu[PF];
-    float da[PF];
-#pragma unroll
-    for (int u = 0; u < PF; u++) {
-        load_raw(raw[u], u + 1);
-        load_x(xb[u], bu[u], da[u], u);
-    }
-    {
-        XRaw<TYPE> r0;
-        load_raw(r0, 0);
-        store_stage(0, r0, 0);
-    }
+    f32x16 y = {};
+    // one stage of lead for everything: the raw weights of superblock sb + 1 are staged at the end
+    // of stage sb and then reloaded with sb + 2; the activation fragment of step kk of sb + 1 is
+    // loaded into the register that step kk of sb has just consumed
+    Raw raw;
+    Xs xs;
+    load_raw(raw, 0);
+    store_stage(0, raw);
+    load_x(xs, 0);
+    load_raw(raw, 1);
     mi_lds_barrier();
 
-    const int nst_max = 2 * n_sb_max;
-    for (int s0 = 0; s0 < nst_max; s0 += PF) {
+    // one stage = superblock sb; LDS buffer sb & 1 (one loop body: the activation registers are
+    // loop-carried, so each fragment of the next superblock lands in the register just consumed)
+    for (int sb = 0; sb < S; sb++) {
+        const int cur = sb & 1;
+        const char * base = lds + cur * kBuf;
+        const char * arow_p = base + (32 * rw + r) * XR + 16 * h;
+        const int nx = sb + 1 < S ? sb + 1 : S - 1;
+        const uint32_t kbn = (uint32_t) nx * 4;
+        i32x16 acc[NP];
+        // weight fragments two 32-deep steps ahead (explicit ring; the sched_barrier per step
+        // keeps the compiler from hoisting every step's LDS reads: registers)
+        i32x4 an[2][NP];
 #pragma unroll
-        for (int u = 0; u < PF; u++) {
-            const int st = s0 + u;
-            if (st >= nst_max) break;  // uniform across the workgroup
-            const int cur = st & 1;
-            const bool active = st < nst;  // group-uniform
-            const char * base = lds_g + cur * kBuf;
-            const int sb = sb_first + (st >> 1);
-            if (active) {
-                const int hs = st & 1;
+        for (int p = 0; p < NP; p++) {
+            an[0][p] = *(const i32x4 *) (arow_p + p * kPlane);
+            an[1][p] = *(const i32x4 *) (arow_p + p * kPlane + 32);
+        }
 #pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-                    i32x4 a[2][NP];
+        for (int kk = 0; kk < 8; kk++) {
+            i32x4 a[NP];
 #pragma unroll
-                    for (int t = 0; t < 2; t++)
+            for (int p = 0; p < NP; p++) a[p] = an[kk & 1][p];
+            if (kk < 6) {
 #pragma unroll
-                        for (int p = 0; p < NP; p++)
-                            a[t][p] = *(const i32x4 *) (base + p * kPlane + (32 * t + r) * XROW + 32 * kk + 16 * h);
+                for (int p = 0; p < NP; p++) an[kk & 1][p] = *(const i32x4 *) (arow_p + p * kPlane + 32 * (kk + 2));
+            }
 #pragma unroll
-                    for (int t = 0; t < 2; t++)
-#pragma unroll
-                        for (int p = 0; p < NP; p++)
-                            acc[t][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[t][p], xb[u][kk], (hs == 0 && kk == 0) ? i32x16{} : acc[t][p], 0, 0, 0);
-                }
-                if (hs == 1) {
-                    // end of superblock: U on the f16 MFMA, then the canonical combine; the
-                    // row operands were staged with the superblock's first stage (other buffer)
-                    const char * base0 = lds_g + (cur ^ 1) * kBuf;
-                    const float * dwv = (const float *) (base0 + NP * kPlane + kAu);
-                    const bool second = SK == 1 && sb >= half;
-#pragma unroll
-                    for (int t = 0; t < 2; t++) {
-                        const half8 au = *(const half8 *) (base0 + NP * kPlane + (32 * t + r) * 32 + 16 * h);
-                        const f32x16 U = __builtin_amdgcn_mfma_f32_32x32x16_f16(au, bu[u], f32x16{}, 0, 0, 0);
-#pragma unroll
-                        for (int g = 0; g < 4; g++) {
-                            const float4 dw4 = *(const float4 *) (dwv + 32 * t + 8 * g + 4 * h);
-                            const float4 dm4 = *(const float4 *) (dwv + XBM + 32 * t + 8 * g + 4 * h);
-                            const float dw[4] = {dw4.x, dw4.y, dw4.z, dw4.w};
-                            const float dm[4] = {dm4.x, dm4.y, dm4.z, dm4.w};
-#pragma unroll
-                            for (int e = 0; e < 4; e++) {
-                                const int i = 4 * g + e;
-                                int T = acc[t][NP - 1][i];
-#pragma unroll
-                                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[t][p][i];
-                                if (second) y1[t][i] = mmqx_term(y1[t][i], T, U[i], dw[e], dm[e], da[u]);
-                                else y[t][i] = mmqx_term(y[t][i], T, U[i], dw[e], dm[e], da[u]);
-                            }
-                        }
-                    }
+            for (int p = 0; p < NP; p++) {
+                if constexpr ((ABL & 4) != 0) {  // timing ablation: no MFMAs
+                    acc[p][kk] = (kk == 0 ? 0 : acc[p][kk]) + a[p][0] * xs.q[kk][0];
+                } else {
+                    acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], xs.q[kk], kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
                 }
             }
-            if (st + 1 < nst) store_stage(cur ^ 1, raw[u], st + 1);
-            // slot u is consumed: refill it (weights for stage st + 1 + PF, activations st + PF)
-            load_raw(raw[u], st + 1 + PF);
-            load_x(xb[u], bu[u], da[u], st + PF);
-            mi_lds_barrier();
+            // step kk of the next superblock into the register just consumed
+            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kbn + (kk >> 1)) * xstep + 32 * (kk & 1), 0, 0));
+            __builtin_amdgcn_sched_barrier(0);
         }
+        // nothing below may be hoisted above this stage's MFMAs: in particular not the unpacking of
+        // the next superblock's weights, whose loads must keep their stage of lead (vmcnt is
+        // in-order, so an early use would wait for every load issued before it)
+        __builtin_amdgcn_sched_barrier(0);
+        // U on the f16 MFMA, then the canonical combine
+        if constexpr ((ABL & 2) != 0) {  // timing ablation: no combine
+#pragma unroll
+            for (int i = 0; i < 16; i++) y[i] += (float) acc[0][i];
+        } else {
+        const char * ro = base + NP * kPlane;
+        const float * dwv = (const float *) (ro + XBM * 32);
+        const half8 au = *(const half8 *) (ro + (32 * rw + r) * 32 + 16 * h);
+        const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(au, xs.bu, f32x16{}, 0, 0, 0);
+        const float da = xs.da;
+        {
+            const uint32_t sc = (uint32_t) nx * (uint32_t) ncols + bcol;
+            xs.bu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, sc * 32 + 16 * h, 0, 0));
+            xs.da = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, sc * 4, 0, 0));
+        }
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const float4 dw4 = *(const float4 *) (dwv + 32 * rw + 8 * g + 4 * h);
+            const float4 dm4 = *(const float4 *) (dwv + XBM + 32 * rw + 8 * g + 4 * h);
+            const float dw[4] = {dw4.x, dw4.y, dw4.z, dw4.w};
+            const float dm[4] = {dm4.x, dm4.y, dm4.z, dm4.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int i = 4 * g + e;
+                int T = acc[NP - 1][i];
+#pragma unroll
+                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][i];
+                y[i] = mmqx_term(y[i], T, Uv[i], dw[e], dm[e], da);
+            }
+        }
+        }
+        // superblock sb + 1 into the other buffer, then the weights of sb + 2
+        __builtin_amdgcn_sched_barrier(0);
+        store_stage(cur ^ 1, raw);
+        load_raw(raw, sb + 2);
+        mi_lds_barrier();
     }
 
-    if constexpr (SK == 2) {
-        // group 1 hands its partial tile (chain half 1) to group 0 through LDS
-        float * red = (float *) lds;
-        __syncthreads();
-        if (grp == 1) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                red[(i * 2 + 0) * 256 + tid] = y[0][i];
-                red[(i * 2 + 1) * 256 + tid] = y[1][i];
-            }
-        }
-        __syncthreads();
-        if (grp == 1) return;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            y1[0][i] = red[(i * 2 + 0) * 256 + tid];
-            y1[1][i] = red[(i * 2 + 1) * 256 + tid];
-        }
-    }
-    // y = half 0 + half 1
-#pragma unroll
-    for (int t = 0; t < 2; t++)
-#pragma unroll
-        for (int i = 0; i < 16; i++) y[t][i] += y1[t][i];
     // D[n][b]: column b = lane & 31 of this wave's 32, rows n = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
-    const int64_t b = b0 + 32 * wave + r;
+    const int64_t b = b0 + 32 * cw + r;
     if (b >= ncols) return;
     float * out = (float *) ((char *) dst + b * ycol);
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
+    for (int g = 0; g < 4; g++) {
+        const int64_t n = n0 + 32 * rw + 8 * g + 4 * h;
+        if (n + 3 < N) {
+            *(float4 *) (out + n) = make_float4(y[4 * g], y[4 * g + 1], y[4 * g + 2], y[4 * g + 3]);
+        } else {
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const int64_t n = n0 + 32 * t + 8 * g + 4 * h;
-            if (n + 3 < N) {
-                *(float4 *) (out + n) = make_float4(y[t][4 * g], y[t][4 * g + 1], y[t][4 * g + 2], y[t][4 * g + 3]);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[t][4 * g + e];
-            }
+            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[4 * g + e];
         }
     }
 }
 
 } // namespace
 
-bool mi_mmqx_supported(int type, int64_t K, size_t ycol) {
-    return (type == 12 || type == 13) && K % 256 == 0 && K >= 256 && ycol % 16 == 0;
+bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t nb01) {
+    // buffer descriptors address < 2 GiB: activations K * ncols bytes, a 64-row weight block
+    return (type == 12 || type == 13) && K % 256 == 0 && K >= 256 && ycol % 16 == 0 && K * ncols < ((int64_t) 1 << 31) &&
+           (int64_t) nb01 * XBM < ((int64_t) 1 << 31);
 }
 
 void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_mmx & act, float * dst,
                      size_t ycol, hipStream_t s) {
     const int64_t nrt = (N + XBM - 1) / XBM, nct = (act.ncols + XBN - 1) / XBN;
     const int64_t T = nrt * nct;
-    // variant bits (GGML_MI355X_MMQ_VARIANT): 64 = XCD-contiguous tile order, 128 = two 4-wave
-    // groups splitting the chain halves (2 waves per SIMD) instead of one group with both halves
-    const int var = g_mi_tuning.mmq_variant;
-    const bool xcd = (var & 64) != 0;
-    const bool sk2 = (var & 128) != 0;
+    // variant bit 64 (GGML_MI355X_MMQ_VARIANT): XCD-contiguous tile order
+    const bool xcd = (g_mi_tuning.mmq_variant & 64) != 0;
     const dim3 grid((unsigned) (xcd ? (T + 7) / 8 * 8 : T));
     const uint8_t * w = (const uint8_t *) W;
-#define MI_MMQX(TY, SKV, PF)                                                                                              \
-    if (xcd) hipLaunchKernelGGL((k_mmqx<TY, SKV, PF, true>), grid, dim3(256 * SKV), 0, s, w, nb01, K, N, act, dst, ycol);  \
-    else hipLaunchKernelGGL((k_mmqx<TY, SKV, PF, false>), grid, dim3(256 * SKV), 0, s, w, nb01, K, N, act, dst, ycol);
+    // bits 256..2048: timing ablations (results invalid): 1 no dequantization, 2 no combine, 4 no MFMAs
+    const int abl = (g_mi_tuning.mmq_variant >> 8) & 7;
+#define MI_MMQX_A(TY, A) hipLaunchKernelGGL((k_mmqx<TY, false, A>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol)
+#define MI_MMQX(TY)                                                                                                      \
+    if (abl == 1) MI_MMQX_A(TY, 1);                                                                                      \
+    else if (abl == 2) MI_MMQX_A(TY, 2);                                                                                 \
+    else if (abl == 3) MI_MMQX_A(TY, 3);                                                                                 \
+    else if (abl == 4) MI_MMQX_A(TY, 4);                                                                                 \
+    else if (abl == 7) MI_MMQX_A(TY, 7);                                                                                 \
+    else if (xcd) hipLaunchKernelGGL((k_mmqx<TY, true>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);          \
+    else hipLaunchKernelGGL((k_mmqx<TY, false>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);
     if (type == 12) {
-        if (sk2) { MI_MMQX(12, 2, 2) } else { MI_MMQX(12, 1, 4) }
+        MI_MMQX(12)
     } else {
-        if (sk2) { MI_MMQX(13, 2, 2) } else { MI_MMQX(13, 1, 3) }
+        MI_MMQX(13)
     }
 #undef MI_MMQX
+#undef MI_MMQX_A
 }
