@@ -427,6 +427,11 @@ struct mi_backend_ctx {
     int last_launches = 0;
     uint16_t * tables = nullptr;  // device: exp, gelu, silu fp16 tables (3 x 65536)
     hipEvent_t split_ready = nullptr;  // src1 of a split mul_mat is ready on `stream`
+    // hipGraph plans (mi_graph_plan_create): captured launches of a whole ggml graph
+    bool graphs = true;
+    std::vector<hipGraphExec_t> exec_pool;  // executable graphs of freed plans, for in-place update
+    int graph_fail_streak = 0;         // consecutive re-instantiations (update refused)
+    int64_t graph_stats[4] = {};       // captures, instantiations, updates, direct computes
 };
 
 static ggml_guid_t mi_guid() {
@@ -444,6 +449,9 @@ static void * scratch_take(mi_backend_ctx * ctx, size_t bytes) {
 
 static void scratch_reserve(mi_backend_ctx * ctx, size_t bytes) {
     if (bytes <= ctx->scratch_size) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    MI_CHECK(hipStreamIsCapturing(ctx->stream, &cs));
+    MI_ASSERT(cs == hipStreamCaptureStatusNone && "scratch must be reserved before a graph capture");
     MI_CHECK(hipStreamSynchronize(ctx->stream));
     if (ctx->scratch) MI_CHECK(hipFree(ctx->scratch));
     const size_t want = std::max(bytes + bytes / 2, (size_t) 16 << 20);
@@ -1521,9 +1529,116 @@ static int try_fuse_copies(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
     return last;
 }
 
+static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph * cgraph);
+
+// graph_compute: every kernel launched directly (the device starts on the first one while the
+// host still launches the rest)
 static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * cgraph) {
     auto * ctx = (mi_backend_ctx *) backend->context;
     mi_device_guard g(ctx->device);
+    ctx->graph_stats[3]++;
+    return mi_graph_launch_nodes(ctx, cgraph);
+}
+
+// Graph plans (ggml_backend_graph_plan_create / _compute, ggml-backend.h): a plan is the graph's
+// launches captured into a hipGraph, so computing it is one hipGraphLaunch instead of one host
+// launch per kernel (~3 us each). A caller that knows its next graph early -- a decode loop,
+// whose next graph depends on positions only -- creates the plan while the device still runs the
+// current one. Executable graphs are pooled per backend: a new plan updates a pooled one in place
+// (hipGraphExecUpdate) when only kernel arguments changed (KV length, cache offsets), and
+// instantiates otherwise. ggml-cuda.cu:2456-2713 is the reference's CUDA-graph analogue (there
+// captured inside graph_compute).
+struct mi_graph_plan {
+    ggml_cgraph graph;              // the caller's graph (node arrays stay the caller's)
+    hipGraphExec_t exec = nullptr;  // null: launched directly at compute time
+};
+
+// consecutive refused updates after which a backend stops capturing (as ggml-cuda.cu's
+// disable_due_to_too_many_updates)
+static constexpr int kGraphMaxFailStreak = 4;
+
+static ggml_backend_graph_plan_t mi_graph_plan_create(ggml_backend_t backend, const ggml_cgraph * cgraph) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    mi_device_guard g(ctx->device);
+    auto * plan = new mi_graph_plan();
+    plan->graph = *cgraph;
+    static const bool env_no_graphs = getenv("GGML_MI355X_DISABLE_GRAPHS") != nullptr;
+    bool capture = ctx->graphs && !env_no_graphs;
+    for (int i = 0; capture && i < cgraph->n_nodes; i++) {
+        const ggml_tensor * n = cgraph->nodes[i];
+        if (n->op == GGML_OP_MUL_MAT && is_split_tensor(n->src[0])) capture = false;  // multi-stream, events
+    }
+    if (!capture) return plan;
+    // everything that allocates or copies synchronously happens before the capture: the node
+    // pass below then only enqueues kernels on ctx->stream. Scratch: the pass's own estimate plus
+    // room for the attention planner's Q copies (at most every CONT node's bytes)
+    op_tables(ctx);
+    size_t cont_bytes = 0;
+    for (int i = 0; i < cgraph->n_nodes; i++) {
+        if (cgraph->nodes[i]->op == GGML_OP_CONT) cont_bytes += (ggml_nbytes(cgraph->nodes[i]) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+    }
+    scratch_reserve(ctx, graph_scratch_bytes(cgraph) + cont_bytes);
+    // the stream may still be running earlier work: the capture records only what follows
+    MI_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    const ggml_status st = mi_graph_launch_nodes(ctx, &plan->graph);
+    hipGraph_t graph = nullptr;
+    const hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    if (st != GGML_STATUS_SUCCESS || ec != hipSuccess || !graph) {
+        // something in the pass could not be captured: this backend launches directly from now on
+        (void) hipGetLastError();
+        if (graph) (void) hipGraphDestroy(graph);
+        ctx->graphs = false;
+        return plan;
+    }
+    ctx->graph_stats[0]++;
+    while (!ctx->exec_pool.empty() && !plan->exec) {
+        hipGraphExec_t ex = ctx->exec_pool.back();
+        ctx->exec_pool.pop_back();
+        hipGraphNode_t err_node = nullptr;
+        hipGraphExecUpdateResult res;
+        if (hipGraphExecUpdate(ex, graph, &err_node, &res) == hipSuccess && res == hipGraphExecUpdateSuccess) {
+            plan->exec = ex;
+        } else {
+            (void) hipGetLastError();
+            MI_CHECK(hipGraphExecDestroy(ex));
+        }
+    }
+    if (plan->exec) {
+        ctx->graph_stats[2]++;
+        ctx->graph_fail_streak = 0;
+    } else {
+        MI_CHECK(hipGraphInstantiate(&plan->exec, graph, nullptr, nullptr, 0));
+        ctx->graph_stats[1]++;
+        if (ctx->graph_stats[1] > 2 && ++ctx->graph_fail_streak >= kGraphMaxFailStreak) ctx->graphs = false;
+    }
+    MI_CHECK(hipGraphDestroy(graph));
+    return plan;
+}
+
+static void mi_graph_plan_free(ggml_backend_t backend, ggml_backend_graph_plan_t p) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    auto * plan = (mi_graph_plan *) p;
+    if (plan->exec) {
+        // kept for the next plan to update in place (at most a few per backend)
+        if (ctx->exec_pool.size() < 4) ctx->exec_pool.push_back(plan->exec);
+        else MI_CHECK(hipGraphExecDestroy(plan->exec));
+    }
+    delete plan;
+}
+
+static enum ggml_status mi_graph_plan_compute(ggml_backend_t backend, ggml_backend_graph_plan_t p) {
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    auto * plan = (mi_graph_plan *) p;
+    mi_device_guard g(ctx->device);
+    if (!plan->exec) {
+        ctx->graph_stats[3]++;
+        return mi_graph_launch_nodes(ctx, &plan->graph);
+    }
+    MI_CHECK(hipGraphLaunch(plan->exec, ctx->stream));
+    return GGML_STATUS_SUCCESS;
+}
+
+static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
     scratch_reserve(ctx, graph_scratch_bytes(cgraph));
     ctx->scratch_used = 0;
     ctx->act_cache.clear();
@@ -1635,6 +1750,7 @@ static void mi_backend_free(ggml_backend_t backend) {
     {
         mi_device_guard g(ctx->device);
         MI_CHECK(hipStreamSynchronize(ctx->stream));
+        for (hipGraphExec_t ex : ctx->exec_pool) MI_CHECK(hipGraphExecDestroy(ex));
         if (ctx->scratch) MI_CHECK(hipFree(ctx->scratch));
         if (ctx->tables) MI_CHECK(hipFree(ctx->tables));
         MI_CHECK(hipStreamDestroy(ctx->stream));
@@ -1735,9 +1851,9 @@ static const ggml_backend_i k_mi_backend_i = {
     /* get_tensor_async        */ mi_backend_get_tensor_async,
     /* cpy_tensor_async        */ mi_backend_cpy_tensor_async,
     /* synchronize             */ mi_backend_synchronize,
-    /* graph_plan_create       */ nullptr,
-    /* graph_plan_free         */ nullptr,
-    /* graph_plan_compute      */ nullptr,
+    /* graph_plan_create       */ mi_graph_plan_create,
+    /* graph_plan_free         */ mi_graph_plan_free,
+    /* graph_plan_compute      */ mi_graph_plan_compute,
     /* graph_compute           */ mi_graph_compute,
     /* supports_op             */ mi_supports_op,
     /* offload_op              */ mi_offload_op,
@@ -1866,6 +1982,19 @@ int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend) {
     return ((mi_backend_ctx *) backend->context)->last_launches;
 }
 
+void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable) {
+    MI_ASSERT(ggml_backend_is_mi355x(backend));
+    auto * ctx = (mi_backend_ctx *) backend->context;
+    ctx->graphs = enable;
+    ctx->graph_fail_streak = 0;
+}
+
+void ggml_backend_mi355x_graph_stats(ggml_backend_t backend, int64_t * stats4) {
+    MI_ASSERT(ggml_backend_is_mi355x(backend));
+    const auto * ctx = (const mi_backend_ctx *) backend->context;
+    for (int i = 0; i < 4; i++) stats4[i] = ctx->graph_stats[i];
+}
+
 bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     if (strcmp(name, "mmv_blocks") == 0 && value >= 0) {
         g_mi_tuning.mmv_blocks = value;
@@ -1885,6 +2014,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "mmv_order") == 0 && (value == 0 || value == 1)) {
         g_mi_tuning.mmv_order = value;
+        return true;
+    }
+    if (strcmp(name, "f16_waves") == 0 && value >= 0) {
+        g_mi_tuning.f16_waves = value;
         return true;
     }
     if (strcmp(name, "f16_threads") == 0 && (value == 0 || value == 64 || value == 128 || value == 256)) {

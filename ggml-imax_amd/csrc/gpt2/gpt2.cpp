@@ -57,9 +57,17 @@ struct gpt2_model {
     std::map<std::string, ggml_tensor *> tensors;
     vocab_t vocab;
     size_t weight_bytes = 0;
-    std::vector<uint8_t> graph_buf;
+    // two graph arenas: the next decode token's graph is built (and allocated) in one while the
+    // device still runs the graph of the other
+    std::vector<uint8_t> graph_buf[2];
+    int graph_slot = 0;                   // arena of the graph last computed
+    ggml_cgraph * next_gf = nullptr;      // prebuilt + allocated graph of (next_n_past, 1 token)
+    int next_n_past = -1;
+    ggml_backend_graph_plan_t next_plan = nullptr;  // next_gf as a backend graph plan (if supported)
     int last_nodes = 0;
     int64_t us_build = 0, us_alloc = 0, us_inputs = 0, us_compute = 0;
+    // within us_compute: enqueue of the graph, next-graph build, wait for the device, logits copy
+    int64_t us_launch = 0, us_prebuild = 0, us_wait = 0, us_readback = 0;
     std::vector<int32_t> tok, pos;  // input staging, alive until the next eval
     // scheduler mode (examples/gpt-2/main-sched.cpp): layers split over backends
     std::vector<ggml_backend_t> backends;       // [gpu, ..., cpu]
@@ -289,13 +297,14 @@ bool load_file(gpt2_model & m, const char * fname, int n_ctx_override) {
 }
 
 // gpt2_graph, main-backend.cpp:442-717
-ggml_cgraph * build_graph(gpt2_model & m, int n_past, int N) {
+ggml_cgraph * build_graph(gpt2_model & m, int n_past, int N, int slot = 0) {
     const auto & hp = m.hp;
     const int n_embd = hp.n_embd, n_layer = hp.n_layer, n_ctx = hp.n_ctx, n_head = hp.n_head;
 
     const size_t buf_size = ggml_tensor_overhead() * kMaxNodes + ggml_graph_overhead_custom(kMaxNodes, false);
-    if (m.graph_buf.size() != buf_size) m.graph_buf.resize(buf_size);
-    ggml_init_params ip = {buf_size, m.graph_buf.data(), true};
+    std::vector<uint8_t> & arena = m.graph_buf[slot];
+    if (arena.size() != buf_size) arena.resize(buf_size);
+    ggml_init_params ip = {buf_size, arena.data(), true};
     ggml_context * ctx = ggml_init(ip);
     ggml_cgraph * gf = ggml_new_graph_custom(ctx, kMaxNodes, false);
 
@@ -486,6 +495,10 @@ int gpt2_sched_n_splits(const gpt2_model * m) {
 
 void gpt2_model_free(gpt2_model * m) {
     if (!m) return;
+    if (m->next_plan) {
+        ggml_backend_synchronize(m->backend);
+        ggml_backend_graph_plan_free(m->backend, m->next_plan);
+    }
 #ifdef GPT2_WITH_SCHED
     if (m->sched) ggml_backend_sched_free((ggml_backend_sched_t) m->sched);
 #endif
@@ -545,13 +558,29 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
     }
 #endif
     const int64_t t0 = now_us();
-    ggml_cgraph * gf = build_graph(*m, n_past, N);
-    const int64_t t1 = now_us();
-    if (!ggml_gallocr_alloc_graph(m->allocr, gf)) {
-        fprintf(stderr, "gpt2_eval: graph allocation failed\n");
-        return 1;
+    ggml_cgraph * gf;
+    int64_t t1, t1b;
+    ggml_backend_graph_plan_t plan = nullptr;
+    if (m->next_gf && m->next_n_past == n_past && N == 1) {
+        // built and allocated while the device ran the previous token (graph_slot ^ 1)
+        gf = m->next_gf;
+        plan = m->next_plan;
+        m->graph_slot ^= 1;
+        t1 = t1b = t0;
+    } else {
+        if (m->next_plan) ggml_backend_graph_plan_free(m->backend, m->next_plan);
+        m->graph_slot ^= 1;
+        gf = build_graph(*m, n_past, N, m->graph_slot);
+        t1 = now_us();
+        if (!ggml_gallocr_alloc_graph(m->allocr, gf)) {
+            m->next_gf = nullptr;
+    m->next_plan = nullptr;
+            fprintf(stderr, "gpt2_eval: graph allocation failed\n");
+            return 1;
+        }
+        t1b = now_us();
     }
-    const int64_t t1b = now_us();
+    m->next_gf = nullptr;
     // inputs go in on the backend's queue, ordered before the graph (ggml_backend_tensor_set_async,
     // ggml-backend.h): no host round trip per input
     ggml_tensor * embd = ggml_graph_get_tensor(gf, "embd");
@@ -562,15 +591,40 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
     ggml_backend_tensor_set_async(m->backend, embd, m->tok.data(), 0, (size_t) N * ggml_element_size(embd));
     ggml_backend_tensor_set_async(m->backend, position, m->pos.data(), 0, (size_t) N * sizeof(int32_t));
     const int64_t t2 = now_us();
-    if (ggml_backend_graph_compute(m->backend, gf) != GGML_STATUS_SUCCESS) {
+    const ggml_status st = plan ? ggml_backend_graph_plan_compute(m->backend, plan) : ggml_backend_graph_compute_async(m->backend, gf);
+    if (st != GGML_STATUS_SUCCESS) {
         fprintf(stderr, "gpt2_eval: graph compute failed\n");
         return 1;
     }
+    const int64_t t2b = now_us();
     ggml_tensor * out = ggml_graph_get_tensor(gf, "logits");
+    // While the device runs this graph, build and allocate the next decode step's (one token at
+    // n_past + N) in the other arena: the graph depends on positions only, not on the token the
+    // caller will pick from these logits. The allocator only assigns addresses in the compute
+    // buffer; the next graph's kernels are queued after this one's on the same stream.
+    const int np1 = n_past + N;
+    if (np1 + 1 <= m->hp.n_ctx && np1 + 1 <= m->wpe->ne[1]) {
+        ggml_cgraph * nx = build_graph(*m, np1, 1, m->graph_slot ^ 1);
+        if (ggml_gallocr_alloc_graph(m->allocr, nx)) {
+            m->next_gf = nx;
+            m->next_n_past = np1;
+            // and, where the backend has graph plans (MI355X: a captured hipGraph), prepared
+            // for a single launch
+            if (m->backend->iface.graph_plan_create) m->next_plan = ggml_backend_graph_plan_create(m->backend, nx);
+        }
+    }
+    const int64_t t2c = now_us();
+    ggml_backend_synchronize(m->backend);
+    const int64_t t2d = now_us();
     const size_t nv = (size_t) m->hp.n_vocab;
     if (all_logits) ggml_backend_tensor_get(out, logits, 0, sizeof(float) * nv * N);
     else ggml_backend_tensor_get(out, logits, sizeof(float) * nv * (N - 1), sizeof(float) * nv);
     const int64_t t3 = now_us();
+    if (plan) ggml_backend_graph_plan_free(m->backend, plan);  // its graph has run
+    m->us_launch = t2b - t2;
+    m->us_prebuild = t2c - t2b;
+    m->us_wait = t2d - t2c;
+    m->us_readback = t3 - t2d;
     m->last_nodes = gf->n_nodes;
     m->us_build = t1 - t0;
     m->us_alloc = t1b - t1;
@@ -606,6 +660,13 @@ int gpt2_tokenize(const gpt2_model * m, const char * text, int32_t * out, int ma
         }
     }
     return n;
+}
+
+void gpt2_last_eval_timing(const gpt2_model * m, int64_t * us4) {
+    us4[0] = m->us_launch;
+    us4[1] = m->us_prebuild;
+    us4[2] = m->us_wait;
+    us4[3] = m->us_readback;
 }
 
 void gpt2_last_eval_stats(const gpt2_model * m, int * n_nodes, int64_t * us_build, int64_t * us_alloc, int64_t * us_inputs,

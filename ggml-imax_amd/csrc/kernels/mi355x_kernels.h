@@ -114,7 +114,8 @@ struct mi_tuning {
     int mmq_variant;  // prefill GEMM: 0 = k_mmq3 (activations in registers), 1 = k_mmq2 (activations via LDS)
     int attn_variant; // attention block: 0 = k_attn_fast where it fits, 1 = k_attn_ordered
     int attn_abl;     // timing ablations of k_attn_fast (0 = none; results invalid otherwise)
-    int mmv_order;    // quantized decode GEMV: 1 = the reference CPU's summation order (bit-identical, slower), 0 = tree sums
+    int mmv_order;    // decode GEMVs (quantized and F16): 1 = the reference CPU's summation order (bit-identical, slower), 0 = tree sums
+    int f16_waves;    // fast F16 decode GEMV: target waves on the chip (0 = automatic)
 };
 extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);
@@ -204,6 +205,12 @@ bool mi_mul_mat_f16_fused_supported(int64_t K, int64_t ncols);
 void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh,
                           int64_t ncols, float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro,
                           hipStream_t s);
+
+// the same in tree order (mmv_f16.hip; the fast F16 decode mode, mmv_order 0): 1..8 columns,
+// K % 8 == 0, 16-byte aligned activation columns (or xh), norm prologue for K <= 3072
+bool mi_mul_mat_f16_fast_supported(int64_t K, int64_t ncols, const mi_src_cols & x, const uint16_t * xh, const mi_norm_prologue & pro);
+void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
+                         float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s);
 
 // attention of the GPT-2 graph (KQ, scale, causal mask, soft_max, KQV, merge) in one launch,
 // bit-identical to the separate nodes. Strides in bytes; element (i0, i1, i2) at base + sum i*nb.

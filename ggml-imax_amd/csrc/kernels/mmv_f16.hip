@@ -1,0 +1,380 @@
+// mmv_f16.hip -- decode-regime F16 mul_mat (GEMV, up to 8 columns) in tree order: the fast mode of
+// the F16 decode path (mmv_order 0; mmv_ordered.hip's kernels replay the reference CPU's exact
+// summation order, mmv_order 1).
+//
+// Same contract as mi_mul_mat_f16_fused (mi355x_kernels.h): the activations are rounded to f16 as
+// the reference's vec_dot_type conversion does (ggml_fp32_to_fp16_row, src/ggml.c:610-612,
+// RNE), optionally produced by the graph's norm -> mul(g) -> add(b) chain computed in the kernel
+// (ggml_compute_forward_norm_f32 / rms_norm, src/ggml.c:10950-11050), and the graph's following
+// bias / residual / GELU nodes and K/V row copies are applied in the store. What differs from the
+// reference is only the order of the f32 sums (products of two halves are exact in f32; lane
+// partial sums + a 16-lane tree instead of ggml_vec_dot_f16's 32 AVX partial sums + the
+// GGML_F32x8_REDUCE tree, src/ggml.c:1680-1720), and the norm's sums (f32 tree instead of a
+// sequential double), ~1e-7 relative per dot.
+//
+// Geometry (wave64): 16 lanes per weight row, four rows per wave, one to four waves per
+// workgroup. Lane m of a row reads the row's 16-byte chunks m, m + 16, ... (a wave-instruction
+// covers 4 rows x 256 contiguous bytes), every chunk of the row requested before the first
+// v_dot2_f32_f16 when the row fits the register batch (K <= 3072), else a two-deep ring of
+// 8-chunk batches. Activations: f16 columns staged once per workgroup in LDS (read back as
+// 16-byte broadcast reads shared by the wave's four rows). Roofline: HBM (2*K bytes per row);
+// GPT-2's matrices are 1.2-4.7 MB, so a launch is latency- not bandwidth-bound, and the lever is
+// having every row of the matrix in flight at once (>= N/4 waves).
+
+#include <algorithm>
+
+#include "mi355x_common.h"
+#include "mi355x_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kLpr = 16;          // lanes per weight row
+constexpr int kChunk = 8;         // f16 per lane per chunk (16 bytes)
+constexpr int kKStep = kLpr * kChunk;  // K covered by one chunk step of a row (128)
+
+__device__ __forceinline__ float dot8(const uint4 & w, const uint4 & x, float acc) {
+    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w.x), __builtin_bit_cast(f16x2, x.x), acc, false);
+    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w.y), __builtin_bit_cast(f16x2, x.y), acc, false);
+    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w.z), __builtin_bit_cast(f16x2, x.z), acc, false);
+    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w.w), __builtin_bit_cast(f16x2, x.w), acc, false);
+    return acc;
+}
+
+// sum over each aligned 16-lane row; every lane of the row gets it
+__device__ __forceinline__ float row16_sum(float v) {
+    auto f = [](int x) { return __int_as_float(x); };
+    auto i = [](float x) { return __float_as_int(x); };
+    v += f(mi_dpp<MI_DPP_QP_1032>(0, i(v)));
+    v += f(mi_dpp<MI_DPP_QP_2301>(0, i(v)));
+    v += f(mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, i(v)));
+    v += f(mi_dpp<MI_DPP_ROW_MIRROR>(0, i(v)));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
+    return (uint32_t) mi_f2h(a) | ((uint32_t) mi_f2h(b) << 16);
+}
+
+// The graph's norm|rms_norm -> mul(g) -> add(b) of one column, by one wave, into f16 LDS (xs,
+// padded with zeros to kp): lane l holds elements 256 j + 4 l .. + 3 (j < JM) in registers, and
+// (GB) the g / b values of the same elements.
+template <int JM, bool GB>
+__device__ __forceinline__ void norm_load(const float * __restrict__ xc, int64_t K, int lane, const mi_norm_prologue & pro,
+                                          float4 (&v)[JM], float4 (&g)[GB ? JM : 1], float4 (&bb)[GB ? JM : 1]) {
+#pragma unroll
+    for (int j = 0; j < JM; j++) {
+        // unconditional loads at clamped addresses + selects: a load under a lane branch makes
+        // the compiler wait for it at the branch's join (vmcnt(0)), serialising every load
+        const int64_t k = (int64_t) j * 256 + lane * 4;
+        const bool in = k < K;
+        const int64_t kc = in ? k : K - 4;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 vv = *(const float4 *) (xc + kc);
+        v[j] = in ? vv : z;
+        if constexpr (GB) {
+            // absent g / b: the load reads x instead (valid address, no branch), the value is
+            // not used (norm_store checks pro.g / pro.b)
+            g[j] = *(const float4 *) ((pro.g ? pro.g : xc) + kc);
+            bb[j] = *(const float4 *) ((pro.b ? pro.b : xc) + kc);
+        }
+    }
+}
+
+template <int JM, bool GB>
+__device__ __forceinline__ void norm_store(float4 (&v)[JM], const float4 (&g)[GB ? JM : 1], const float4 (&bb)[GB ? JM : 1], int64_t K,
+                                           int64_t kp, const mi_norm_prologue & pro, uint16_t * xs, int lane) {
+    const float fk = (float) K;
+    float scale;
+    if (pro.mode == 2) {
+        float s2 = 0.0f;
+#pragma unroll
+        for (int j = 0; j < JM; j++) s2 += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+        scale = 1.0f / sqrtf(mi_wave_sum_u(s2) / fk + pro.eps);
+    } else {
+        float s = 0.0f;
+#pragma unroll
+        for (int j = 0; j < JM; j++) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+        const float mean = mi_wave_sum_u(s) / fk;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int j = 0; j < JM; j++) {
+            const int64_t k = (int64_t) j * 256 + lane * 4;
+            if (k < K) {
+                v[j].x -= mean; v[j].y -= mean; v[j].z -= mean; v[j].w -= mean;
+                s2 += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+            }
+        }
+        scale = 1.0f / sqrtf(mi_wave_sum_u(s2) / fk + pro.eps);
+    }
+#pragma unroll
+    for (int j = 0; j < JM; j++) {
+        const int64_t k = (int64_t) j * 256 + lane * 4;
+        if (k < kp) {
+            uint2 h = make_uint2(0u, 0u);
+            if (k < K) {
+                float y[4] = {v[j].x * scale, v[j].y * scale, v[j].z * scale, v[j].w * scale};
+                float4 gg, bv;
+                if constexpr (GB) {
+                    gg = g[j];
+                    bv = bb[j];
+                } else {
+                    gg = pro.g ? *(const float4 *) (pro.g + k) : make_float4(1.f, 1.f, 1.f, 1.f);
+                    bv = pro.b ? *(const float4 *) (pro.b + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                if (pro.g) { y[0] *= gg.x; y[1] *= gg.y; y[2] *= gg.z; y[3] *= gg.w; }
+                if (pro.b) { y[0] += bv.x; y[1] += bv.y; y[2] += bv.z; y[3] += bv.w; }
+                h = make_uint2(pack_h2(y[0], y[1]), pack_h2(y[2], y[3]));
+            }
+            *(uint2 *) (xs + k) = h;
+        }
+    }
+}
+
+// f32 activation column -> f16 LDS (zero-padded to kp), JX float4 per thread per round, all of a
+// round's loads in flight together
+template <int JX>
+struct ColStager {
+    float4 v[JX];
+    __device__ __forceinline__ void load(const float * __restrict__ xc, int64_t K, int64_t base) {
+#pragma unroll
+        for (int j = 0; j < JX; j++) {
+            const int64_t i = base + (int64_t) j * blockDim.x + threadIdx.x;  // float4 index
+            const bool in = i * 4 < K;
+            const float4 vv = *(const float4 *) (xc + (in ? i * 4 : K - 4));  // branch-free (see norm_load)
+            v[j] = in ? vv : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    __device__ __forceinline__ void store(uint16_t * xd, int64_t kp, int64_t base) {
+#pragma unroll
+        for (int j = 0; j < JX; j++) {
+            const int64_t i = base + (int64_t) j * blockDim.x + threadIdx.x;
+            if (i * 4 < kp) *(uint2 *) (xd + i * 4) = make_uint2(pack_h2(v[j].x, v[j].y), pack_h2(v[j].z, v[j].w));
+        }
+    }
+    __device__ __forceinline__ void column(const float * __restrict__ xc, int64_t K, int64_t kp, uint16_t * xd, int64_t from) {
+        for (int64_t base = from; base < kp / 4; base += (int64_t) JX * blockDim.x) {
+            load(xc, K, base);
+            store(xd, kp, base);
+        }
+    }
+};
+
+// One workgroup = KS waves (runtime, blockDim.x / 64) on 4 weight rows (16 lanes each); the
+// waves split the rows' 128-wide K steps: wave w takes steps w, w + KS, ... -- at most U of them
+// in registers when ONE, else a two-deep ring of U-step batches -- and the KS partial sums of a
+// (row, column) are added in wave order through LDS. JM: register depth of the norm prologue
+// (K <= 256 JM), 0 = no prologue. Many small waves rather than few long ones: a decode matrix is
+// 1-5 MB, so what bounds a launch is how many rows' bytes are in flight at once.
+template <int NC, int EPI, int U, bool ONE, int JM>
+__global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                  mi_src_cols x, const uint16_t * __restrict__ xh, int64_t ncols,
+                                                  float * __restrict__ dst, size_t ycol, mi_f16_epilogue e, mi_norm_prologue pro,
+                                                  int64_t kp) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][kp] f16 (zero beyond K), then [KS][4][NC] f32
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int m = lane & (kLpr - 1), rg = lane >> 4;
+    const int64_t row = (int64_t) blockIdx.x * 4 + rg;
+    const bool live = row < N;
+    const int64_t c0 = (int64_t) blockIdx.y * NC;
+    const int nc = (int) std::min<int64_t>(NC, ncols - c0);
+    const int nit = (int) ((K + kKStep - 1) / kKStep);   // K steps of a row (host: nw <= nit)
+    const int nj = (nit - wave + nw - 1) / nw;            // this wave's steps
+    const int64_t k8 = K / kChunk;  // whole 16-byte chunks of the row (K % 8 == 0)
+
+    const uint8_t * wrow = W + (live ? row : 0) * nb01;
+    // this wave's j-th step; branch-free (see norm_load): clamped address, then zero past the row
+    auto ld = [&](int j) -> uint4 {
+        const int it = wave + (j < nj ? j : nj - 1) * nw;
+        const int64_t c = (int64_t) it * kLpr + m;
+        const uint4 v = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);
+        return c < k8 ? v : make_uint4(0u, 0u, 0u, 0u);
+    };
+
+    // Everything that does not depend on the weights is requested before them (vmcnt retires in
+    // order, so its consumers then do not wait for the weight stream): the first activation
+    // column (or the norm prologue's column, g and b) and the epilogue's bias / residual. Loads
+    // are unconditional (clamped indices): a load under a branch is waited for at its join.
+    constexpr bool GB = JM > 0 && JM <= 4;
+    constexpr int JX = ONE ? 4 : 8;
+    float4 pv[JM > 0 ? JM : 1], pg[GB ? JM : 1], pb[GB ? JM : 1];
+    ColStager<JX> st;
+    if constexpr (JM > 0) {
+        norm_load<JM, GB>((const float *) (x.base + (c0 + (wave < nc ? wave : 0)) * x.nb1), K, lane, pro, pv, pg, pb);
+    } else {
+        if (!xh) st.load((const float *) (x.base + c0 * x.nb1), K, 0);
+    }
+    float e_bias = 0.0f, e_res = 0.0f;
+    {
+        const int64_t rc = live ? row : 0, cc = c0 + (m < nc ? m : nc - 1);
+        if (EPI >= 1) e_bias = e.bias[rc];
+        if (EPI == 2) e_res = *(const float *) (e.resid + cc * e.resid_nb1 + rc * sizeof(float));
+    }
+    uint4 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) cur[u] = ld(u);
+
+    // stage the f16 activation columns (zero-padded to kp). One column with the norm prologue:
+    // every wave normalizes it into its own LDS copy (PRIV), so no wave waits for another's.
+    constexpr bool PRIV = JM > 0 && NC == 1;
+    uint16_t * xw = PRIV ? xs + (size_t) wave * kp : xs;
+    if constexpr (PRIV) {
+        norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xw, lane);
+    } else if constexpr (JM > 0) {
+        for (int c = wave; c < nc; c += nw) {
+            if (c != wave) norm_load<JM, GB>((const float *) (x.base + (c0 + c) * x.nb1), K, lane, pro, pv, pg, pb);
+            norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) c * kp, lane);
+        }
+    } else if (xh) {
+        for (int c = 0; c < nc; c++) {
+            const uint4 * src = (const uint4 *) (xh + (c0 + c) * K);
+            uint4 * xd = (uint4 *) (xs + (size_t) c * kp);
+            for (int64_t k = threadIdx.x; k < kp / 8; k += blockDim.x) xd[k] = k < k8 ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+        }
+    } else {
+        st.store(xs, kp, 0);
+        st.column((const float *) (x.base + c0 * x.nb1), K, kp, xs, (int64_t) JX * blockDim.x);
+        for (int c = 1; c < nc; c++) st.column((const float *) (x.base + (c0 + c) * x.nb1), K, kp, xs + (size_t) c * kp, 0);
+    }
+    if constexpr (!PRIV) mi_lds_barrier();
+
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) acc[c] = 0.0f;
+    auto step = [&](const uint4 & w, int j) {
+        const int64_t k = ((int64_t) (wave + j * nw) * kLpr + m) * kChunk;
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+            if (c < nc) acc[c] = dot8(w, *(const uint4 *) (xw + (size_t) c * kp + k), acc[c]);
+    };
+    if constexpr (ONE) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (u < nj) step(cur[u], u);
+    } else {
+        uint4 nxt[U];
+        for (int s0 = 0; s0 < nj; s0 += U) {
+            const int s1 = s0 + U;
+            if (s1 < nj) {
+#pragma unroll
+                for (int u = 0; u < U; u++) nxt[u] = ld(s1 + u);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (s0 + u < nj) step(cur[u], s0 + u);
+#pragma unroll
+            for (int u = 0; u < U; u++) cur[u] = nxt[u];
+        }
+    }
+
+    // this wave's row totals in every lane of the row; lane m < nc holds column m
+    float mine = 0.0f;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const float t = row16_sum(acc[c]);
+        if (m == c) mine = t;
+    }
+    if (nw > 1) {
+        // the waves' partial sums of each (row, column), added in wave order by wave 0
+        float * red = (float *) (xs + (size_t) (PRIV ? nw : NC) * kp);
+        if (m < nc) red[(wave * 4 + rg) * NC + m] = mine;
+        mi_lds_barrier();
+        if (wave != 0) return;
+        if (m < nc) {
+            mine = red[rg * NC + m];
+            for (int w = 1; w < nw; w++) mine += red[(w * 4 + rg) * NC + m];
+        }
+    }
+    if (live && m < nc) {
+        const int64_t col = c0 + m;
+        float v = mine;
+        if (EPI >= 1) v = v + e_bias;
+        if (EPI == 2) v = v + e_res;
+        if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
+        *(float *) ((char *) dst + col * ycol + row * sizeof(float)) = v;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (e.copy[k].ptr && row >= e.copy[k].row0 && row < e.copy[k].row1)
+                *(float *) (e.copy[k].ptr + col * e.copy[k].col_stride + (row - e.copy[k].row0) * sizeof(float)) = v;
+        }
+    }
+}
+
+template <int NC, int U, bool ONE, int JM>
+void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols, float * dst,
+               size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int ks) {
+    const int64_t kp = (K + kKStep - 1) / kKStep * kKStep;
+    const dim3 grid((unsigned) ((N + 3) / 4), (unsigned) ((ncols + NC - 1) / NC));
+    const size_t lds = (size_t) (JM > 0 && NC == 1 ? ks : NC) * kp * sizeof(uint16_t) + (size_t) ks * 4 * NC * sizeof(float);
+    const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
+    const uint8_t * w = (const uint8_t *) W;
+#define MI_GEMV_F16(EP) hipLaunchKernelGGL((k_gemv_f16<NC, EP, U, ONE, JM>), grid, dim3(64 * ks), lds, s, w, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, kp)
+    switch (epi) {
+        case 0: MI_GEMV_F16(0); break;
+        case 1: MI_GEMV_F16(1); break;
+        case 2: MI_GEMV_F16(2); break;
+        default: MI_GEMV_F16(3); break;
+    }
+#undef MI_GEMV_F16
+}
+
+template <int U, bool ONE, int JM>
+void launch_u(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols, float * dst,
+              size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int nc, int ks) {
+    switch (nc) {
+        case 1: launch_nc<1, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks); break;
+        case 2: launch_nc<2, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks); break;
+        case 4: launch_nc<4, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks); break;
+        default: launch_nc<8, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks); break;
+    }
+}
+
+// one register pass of `per` steps per wave: U = per rounded up to 1/2/4/8 (no wasted loads)
+template <int JM>
+void launch_one(int per, const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
+                float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int nc, int ks) {
+    if (per <= 1) launch_u<1, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+    else if (per <= 2) launch_u<2, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+    else if (per <= 4) launch_u<4, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+    else launch_u<8, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+}
+
+} // namespace
+
+bool mi_mul_mat_f16_fast_supported(int64_t K, int64_t ncols, const mi_src_cols & x, const uint16_t * xh, const mi_norm_prologue & pro) {
+    if (ncols < 1 || ncols > 8 || K < 8 || K % 8 != 0 || K > 16384) return false;
+    if (!xh && (x.nb1 % 16 != 0 || (uintptr_t) x.base % 16 != 0)) return false;
+    // norm prologue: column in registers (K <= 3072), one register pass per wave (K <= 1024 or >= 3 waves)
+    if (pro.mode && (K > 3072 || xh || ((uintptr_t) pro.g | (uintptr_t) pro.b) % 16 != 0)) return false;
+    return true;
+}
+
+void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
+                         float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s) {
+    // columns per workgroup: ncols rounded up to 1/2/4/8, within 64 KB of f16 columns in LDS
+    const int64_t kp = (K + kKStep - 1) / kKStep * kKStep;
+    int nc = ncols >= 8 ? 8 : ncols >= 3 ? 4 : (int) ncols;
+    while (nc > 1 && (int64_t) nc * kp * 2 > 60000) nc /= 2;
+    // waves per workgroup (K split): about kWaves waves on the chip (~8 per CU), at most 8 per
+    // workgroup and no more than the row's K steps, then as few as give the same steps per wave
+    const int nit = (int) (kp / kKStep);
+    const int64_t groups = (N + 3) / 4 * ((ncols + nc - 1) / nc);
+    const int64_t want = g_mi_tuning.f16_waves > 0 ? g_mi_tuning.f16_waves : 2048;
+    int ks = (int) std::max<int64_t>(1, std::min<int64_t>(8, want / std::max<int64_t>(groups, 1)));
+    ks = std::min(ks, nit);
+    if (pro.mode) ks = std::max(ks, (nit + 7) / 8);  // the prologue path runs one register pass
+    const int per = (nit + ks - 1) / ks;  // steps per wave
+    ks = (nit + per - 1) / per;
+    const bool one = per <= 8;
+    if (pro.mode) {  // supported() guarantees one pass (K <= 3072)
+        if (K <= 1024) launch_one<4>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+        else launch_one<12>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+    } else if (one) {
+        launch_one<0>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+    } else {
+        launch_u<8, false, 0>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+    }
+}

@@ -849,7 +849,11 @@ bool mi_mul_mat_f16_fused_supported(int64_t K, int64_t ncols) { return ncols >= 
 void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh,
                           int64_t ncols, float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro,
                           hipStream_t s) {
-    // columns per workgroup: up to 4, with the f16 activations (+ one f32 column) within 64 KB of LDS
+    if (g_mi_tuning.mmv_order == 0 && mi_mul_mat_f16_fast_supported(K, ncols, x, xh, pro)) {
+        mi_mul_mat_f16_fast(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s);
+        return;
+    }
+    // reference CPU order: columns per workgroup: up to 4, with the f16 activations (+ one f32 column) within 64 KB of LDS
     const int64_t cap = (32768 - (pro.mode ? 2 * K : 0)) / K;
     const int nc = (int) std::min<int64_t>(std::min<int64_t>(ncols, 4), std::max<int64_t>(cap, 1));
     switch (nc) {

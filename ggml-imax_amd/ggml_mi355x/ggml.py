@@ -202,6 +202,9 @@ _SIGS = {
     "ggml_backend_graph_compute": ([c_void_p, POINTER(ggml_cgraph)], c_int),
     "ggml_backend_graph_compute_async": ([c_void_p, POINTER(ggml_cgraph)], c_int),
     "ggml_backend_synchronize": ([c_void_p], None),
+    "ggml_backend_graph_plan_create": ([c_void_p, POINTER(ggml_cgraph)], c_void_p),
+    "ggml_backend_graph_plan_free": ([c_void_p, c_void_p], None),
+    "ggml_backend_graph_plan_compute": ([c_void_p, c_void_p], c_int),
     "ggml_backend_supports_op": ([c_void_p, T], c_bool),
     "ggml_backend_reg_get_count": ([], c_size_t),
     "ggml_backend_reg_get_name": ([c_size_t], c_char_p),
@@ -230,6 +233,8 @@ _SIGS = {
     "ggml_backend_mi355x_get_stream": ([c_void_p], c_void_p),
     "ggml_backend_mi355x_last_launch_count": ([c_void_p], c_int),
     "ggml_backend_mi355x_set_tuning": ([c_char_p, c_int], c_bool),
+    "ggml_backend_mi355x_set_graph_capture": ([c_void_p, c_bool], None),
+    "ggml_backend_mi355x_graph_stats": ([c_void_p, c_void_p], None),
     "ggml_backend_mi355x_quantize_activations": ([c_void_p, c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p], c_bool),
     # GPT-2 driver (include/gpt2-mi355x.h)
     "gpt2_model_load": ([c_char_p, c_void_p, c_int, c_int], c_void_p),
@@ -244,6 +249,7 @@ _SIGS = {
     "gpt2_token_text": ([c_void_p, c_int32], c_char_p),
     "gpt2_tokenize": ([c_void_p, c_char_p, c_void_p, c_int], c_int),
     "gpt2_last_eval_stats": ([c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], None),
+    "gpt2_last_eval_timing": ([c_void_p, c_void_p], None),
 }
 
 BACKEND_EXPORTS = [k for k in _SIGS if k.startswith("ggml_backend_mi355x") or k == "ggml_backend_is_mi355x"]

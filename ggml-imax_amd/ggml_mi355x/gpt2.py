@@ -218,7 +218,12 @@ class Model:
         n = ctypes.c_int()
         b, a, i, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         self.lib.gpt2_last_eval_stats(self.m, ctypes.byref(n), ctypes.byref(b), ctypes.byref(a), ctypes.byref(i), ctypes.byref(c))
-        return {"nodes": n.value, "us_build": b.value, "us_alloc": a.value, "us_inputs": i.value, "us_compute": c.value}
+        r = {"nodes": n.value, "us_build": b.value, "us_alloc": a.value, "us_inputs": i.value, "us_compute": c.value}
+        if hasattr(self.lib, "gpt2_last_eval_timing"):
+            t = (ctypes.c_int64 * 4)()
+            self.lib.gpt2_last_eval_timing(self.m, t)
+            r.update(us_launch=t[0], us_prebuild=t[1], us_wait=t[2], us_readback=t[3])
+        return r
 
     def tokenize(self, text: str) -> list[int]:
         buf = np.empty(4096, dtype=np.int32)

@@ -54,6 +54,16 @@ GGML_API void * ggml_backend_mi355x_get_stream(ggml_backend_t backend);
 // Number of kernels launched by the last graph_compute (for tests / profiling).
 GGML_API int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend);
 
+// Graph plans (ggml_backend_graph_plan_create / _compute) are hipGraphs: the plan's launches
+// are captured at creation (updating a pooled executable graph in place when only kernel
+// arguments changed) and computing it is one hipGraphLaunch. graph_compute launches directly.
+// GGML_MI355X_DISABLE_GRAPHS=1 (process-wide, as GGML_CUDA_DISABLE_GRAPHS, ggml-cuda.cu:2462) or
+// set_graph_capture(false) makes plans launch directly too.
+GGML_API void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable);
+// counters since init: [0] captured plans, [1] graph instantiations, [2] in-place updates,
+// [3] direct (uncaptured) computes
+GGML_API void ggml_backend_mi355x_graph_stats(ggml_backend_t backend, int64_t * stats4);
+
 // Launch-shape knobs of the streaming kernels, for A/B tuning inside one process:
 // "mmv_blocks" (resident workgroups of the fused GEMV), "mmv_variant" (see mi355x_kernels.h).
 // Returns false for an unknown name.

@@ -69,6 +69,11 @@ GGML_API int gpt2_tokenize(const struct gpt2_model * model, const char * text, i
 GGML_API void gpt2_last_eval_stats(const struct gpt2_model * model, int * n_nodes, int64_t * us_build, int64_t * us_alloc,
                                    int64_t * us_inputs, int64_t * us_compute);
 
+// the parts of us_compute of the last direct-backend eval, microseconds: us4[0] host time to
+// enqueue the graph (ggml_backend_graph_compute_async), [1] to build + allocate the next decode
+// step's graph while the device runs this one, [2] waiting for the device, [3] the logits copy
+GGML_API void gpt2_last_eval_timing(const struct gpt2_model * model, int64_t * us4);
+
 #ifdef __cplusplus
 }
 #endif
