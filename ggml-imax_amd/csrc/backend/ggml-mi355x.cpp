@@ -1502,6 +1502,32 @@ static bool is_copy(const ggml_tensor * t) {
            ggml_nelements(t) == ggml_nelements(t->src[0]);
 }
 
+// GET_ROWS(a, ia), GET_ROWS(b, ib), ADD of the two (GPT-2's token + position embedding,
+// main-backend.cpp:475-478) as one launch; the two row sets must be private intermediates
+static int try_fuse_embedding(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u) {
+    ggml_tensor * g1 = g->nodes[i];
+    const int j = next_node(g, i);
+    if (j < 0) return -1;
+    ggml_tensor * g2 = g->nodes[j];
+    const int k = next_node(g, j);
+    if (k < 0 || g2->op != GGML_OP_GET_ROWS) return -1;
+    ggml_tensor * add = g->nodes[k];
+    if (add->op != GGML_OP_ADD || !((add->src[0] == g1 && add->src[1] == g2) || (add->src[0] == g2 && add->src[1] == g1))) return -1;
+    if (!private_intermediate(g1, u) || !private_intermediate(g2, u)) return -1;
+    for (const ggml_tensor * t : {(const ggml_tensor *) g1, (const ggml_tensor *) g2}) {
+        if (t->type != GGML_TYPE_F32 || t->ne[2] != 1 || t->ne[3] != 1 || t->src[1]->ne[1] != 1 || t->src[1]->ne[2] != 1) return -1;
+        if (t->src[0]->ne[2] != 1 || t->src[0]->ne[3] != 1) return -1;
+    }
+    if (!ggml_are_same_shape(g1, g2) || !ggml_are_same_shape(add, g1) || add->type != GGML_TYPE_F32 || add->nb[0] != sizeof(float)) return -1;
+    // the output is written while the row tables and indices are read
+    for (const ggml_tensor * t : {g1->src[0], g1->src[1], g2->src[0], g2->src[1]}) {
+        if (overlaps(add, t)) return -1;
+    }
+    mi_op_get_rows_add(desc(add), desc(g1->src[0]), desc(g1->src[1]), desc(g2->src[0]), desc(g2->src[1]), ctx->stream);
+    ctx->last_launches++;
+    return k;
+}
+
 // consecutive independent copies (GPT-2: K -> cache, V -> cache, cont(Q)) as one launch
 static int try_fuse_copies(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
     std::vector<ggml_tensor *> grp = {g->nodes[i]};
@@ -1645,7 +1671,7 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
     ctx->last_launches = 0;
     static const bool no_fuse = getenv("GGML_MI355X_NO_FUSED_MMV") != nullptr;
     static const bool no_node_fusion = getenv("GGML_MI355X_NO_NODE_FUSION") != nullptr;
-    // bit mask of enabled node fusions (debug/A-B): 1 norm, 2 softmax, 4 f16 GEMV, 8 copies, 16 attention
+    // bit mask of enabled node fusions (debug/A-B): 1 norm, 2 softmax, 4 f16 GEMV, 8 copies, 16 attention, 64 embedding
     static const int fuse_mask = getenv("GGML_MI355X_FUSE_MASK") ? atoi(getenv("GGML_MI355X_FUSE_MASK")) : 0xff;
     mi_uses uses;
     std::vector<uint8_t> absorbed_nodes;
@@ -1709,6 +1735,7 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
                 case GGML_OP_CPY:
                 case GGML_OP_DUP:
                 case GGML_OP_CONT: last = (fuse_mask & 8) ? try_fuse_copies(ctx, cgraph, i) : -1; break;
+                case GGML_OP_GET_ROWS: last = (fuse_mask & 64) ? try_fuse_embedding(ctx, cgraph, i, uses) : -1; break;
                 default: break;
             }
         }
@@ -2018,6 +2045,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "f16_waves") == 0 && value >= 0) {
         g_mi_tuning.f16_waves = value;
+        return true;
+    }
+    if (strcmp(name, "f16_rgs") == 0 && value >= 0 && value <= 8) {
+        g_mi_tuning.f16_rgs = value;
         return true;
     }
     if (strcmp(name, "f16_threads") == 0 && (value == 0 || value == 64 || value == 128 || value == 256)) {

@@ -116,6 +116,7 @@ struct mi_tuning {
     int attn_abl;     // timing ablations of k_attn_fast (0 = none; results invalid otherwise)
     int mmv_order;    // decode GEMVs (quantized and F16): 1 = the reference CPU's summation order (bit-identical, slower), 0 = tree sums
     int f16_waves;    // fast F16 decode GEMV: target waves on the chip (0 = automatic)
+    int f16_rgs;      // fast F16 decode GEMV: row groups (4 rows) per workgroup (0 = automatic)
 };
 extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);
@@ -166,6 +167,10 @@ void mi_op_cpy(const mi_tensor_desc & d, const mi_tensor_desc & a, hipStream_t s
 constexpr int kMiMaxCopies = 4;
 void mi_op_cpy_multi(const mi_tensor_desc * d, const mi_tensor_desc * a, int count, hipStream_t s);
 void mi_op_get_rows(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & idx, hipStream_t s);
+// d = get_rows(a, ia) + get_rows(b, ib) (1-D index vectors, f32 dst): the graph's two GET_ROWS and
+// their ADD in one launch, each value as the separate nodes compute it
+void mi_op_get_rows_add(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & ia, const mi_tensor_desc & b,
+                        const mi_tensor_desc & ib, hipStream_t s);
 void mi_op_diag_mask(const mi_tensor_desc & d, const mi_tensor_desc & a, int n_past, float value, hipStream_t s);
 // norm / rms_norm; g, b (optional, 1-D over ne0): the graph's following mul(., g) and add(., b)
 void mi_op_norm(const mi_tensor_desc & d, const mi_tensor_desc & a, float eps, bool rms, const float * g, const float * b,

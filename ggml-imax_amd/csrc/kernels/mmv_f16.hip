@@ -163,21 +163,25 @@ struct ColStager {
     }
 };
 
-// One workgroup = KS waves (runtime, blockDim.x / 64) on 4 weight rows (16 lanes each); the
-// waves split the rows' 128-wide K steps: wave w takes steps w, w + KS, ... -- at most U of them
-// in registers when ONE, else a two-deep ring of U-step batches -- and the KS partial sums of a
-// (row, column) are added in wave order through LDS. JM: register depth of the norm prologue
-// (K <= 256 JM), 0 = no prologue. Many small waves rather than few long ones: a decode matrix is
-// 1-5 MB, so what bounds a launch is how many rows' bytes are in flight at once.
+// One workgroup = RGS row groups of 4 weight rows (16 lanes per row) x KS waves per group
+// (runtime: KS = blockDim.x / 64 / RGS); a group's waves split the rows' 128-wide K steps: wave
+// s of the group takes steps s, s + KS, ... -- at most U of them in registers when ONE, else a
+// two-deep ring of U-step batches -- and the KS partial sums of a (row, column) are added in wave
+// order through LDS. JM: register depth of the norm prologue (K <= 256 JM), 0 = no prologue.
+// Many small waves rather than few long ones: a decode matrix is 1-5 MB, so what bounds a launch
+// is how many rows' bytes are in flight at once; several row groups per workgroup only for very
+// tall matrices (lm_head), where the per-workgroup staging of the activations would otherwise
+// cost more L2 traffic than the weights.
 template <int NC, int EPI, int U, bool ONE, int JM>
 __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                                   mi_src_cols x, const uint16_t * __restrict__ xh, int64_t ncols,
                                                   float * __restrict__ dst, size_t ycol, mi_f16_epilogue e, mi_norm_prologue pro,
-                                                  int64_t kp) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][kp] f16 (zero beyond K), then [KS][4][NC] f32
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+                                                  int64_t kp, int rgs) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][kp] f16 (zero beyond K), then [waves][4][NC] f32
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x >> 6) / rgs;
+    const int grp = wid / nw, wave = wid % nw;  // row group, K slice
     const int m = lane & (kLpr - 1), rg = lane >> 4;
-    const int64_t row = (int64_t) blockIdx.x * 4 + rg;
+    const int64_t row = ((int64_t) blockIdx.x * rgs + grp) * 4 + rg;
     const bool live = row < N;
     const int64_t c0 = (int64_t) blockIdx.y * NC;
     const int nc = (int) std::min<int64_t>(NC, ncols - c0);
@@ -203,7 +207,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
     float4 pv[JM > 0 ? JM : 1], pg[GB ? JM : 1], pb[GB ? JM : 1];
     ColStager<JX> st;
     if constexpr (JM > 0) {
-        norm_load<JM, GB>((const float *) (x.base + (c0 + (wave < nc ? wave : 0)) * x.nb1), K, lane, pro, pv, pg, pb);
+        norm_load<JM, GB>((const float *) (x.base + (c0 + (wid < nc ? wid : 0)) * x.nb1), K, lane, pro, pv, pg, pb);
     } else {
         if (!xh) st.load((const float *) (x.base + c0 * x.nb1), K, 0);
     }
@@ -219,14 +223,17 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
 
     // stage the f16 activation columns (zero-padded to kp). One column with the norm prologue:
     // every wave normalizes it into its own LDS copy (PRIV), so no wave waits for another's.
-    constexpr bool PRIV = JM > 0 && NC == 1;
-    uint16_t * xw = PRIV ? xs + (size_t) wave * kp : xs;
-    if constexpr (PRIV) {
-        norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xw, lane);
-    } else if constexpr (JM > 0) {
-        for (int c = wave; c < nc; c += nw) {
-            if (c != wave) norm_load<JM, GB>((const float *) (x.base + (c0 + c) * x.nb1), K, lane, pro, pv, pg, pb);
-            norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) c * kp, lane);
+    const bool priv = JM > 0 && NC == 1 && rgs == 1;
+    uint16_t * xw = priv ? xs + (size_t) wave * kp : xs;
+    if constexpr (JM > 0) {
+        if (priv) {
+            norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xw, lane);
+        } else {
+            const int nwt = blockDim.x >> 6;
+            for (int c = wid; c < nc; c += nwt) {
+                if (c != wid) norm_load<JM, GB>((const float *) (x.base + (c0 + c) * x.nb1), K, lane, pro, pv, pg, pb);
+                norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) c * kp, lane);
+            }
         }
     } else if (xh) {
         for (int c = 0; c < nc; c++) {
@@ -239,7 +246,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
         st.column((const float *) (x.base + c0 * x.nb1), K, kp, xs, (int64_t) JX * blockDim.x);
         for (int c = 1; c < nc; c++) st.column((const float *) (x.base + (c0 + c) * x.nb1), K, kp, xs + (size_t) c * kp, 0);
     }
-    if constexpr (!PRIV) mi_lds_barrier();
+    if (!priv) mi_lds_barrier();
 
     float acc[NC];
 #pragma unroll
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
     }
     if (nw > 1) {
         // the waves' partial sums of each (row, column), added in wave order by wave 0
-        float * red = (float *) (xs + (size_t) (PRIV ? nw : NC) * kp);
+        float * red = (float *) (xs + (size_t) (priv ? nw : NC) * kp) + (size_t) grp * nw * 4 * NC;
         if (m < nc) red[(wave * 4 + rg) * NC + m] = mine;
         mi_lds_barrier();
         if (wave != 0) return;
@@ -303,15 +310,84 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
     }
 }
 
+// Tall matrices (lm_head, N = 50257): one column, rows in one register pass (K <= 128 U). A
+// fixed grid of 4-wave workgroups (~8 waves per CU) stages / normalizes the column once per
+// workgroup, then every wave walks its row groups (4 rows) grid-stride, the next group's weights
+// requested before the current group is reduced: the weight stream keeps two row groups per wave
+// in flight instead of paying one launch-wide latency round per row group.
+template <int EPI, int U, int JM>
+__global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                       mi_src_cols x, float * __restrict__ dst, mi_f16_epilogue e,
+                                                       mi_norm_prologue pro, int64_t kp) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [kp] f16
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int m = lane & (kLpr - 1), rg = lane >> 4;
+    const int64_t ngroups = (N + 3) / 4, stride = (int64_t) gridDim.x * 4;
+    const int nit = (int) ((K + kKStep - 1) / kKStep);
+    const int64_t k8 = K / kChunk;
+    int64_t grp = (int64_t) blockIdx.x * 4 + wid;
+    auto row_of = [&](int64_t gi) { const int64_t r = gi * 4 + rg; return r < N ? r : N - 1; };
+    auto load_group = [&](uint4 (&w)[U], float & eb, int64_t gi) {
+        const int64_t r = row_of(gi < ngroups ? gi : ngroups - 1);
+        const uint8_t * wrow = W + r * nb01;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int it = u < nit ? u : nit - 1;
+            const int64_t c = (int64_t) it * kLpr + m;
+            const uint4 v = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);
+            w[u] = c < k8 ? v : make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (EPI >= 1) eb = e.bias[r];
+    };
+
+    constexpr bool GB = JM > 0 && JM <= 4;
+    float4 pv[JM > 0 ? JM : 1], pg[GB ? JM : 1], pb[GB ? JM : 1];
+    ColStager<4> st;
+    if constexpr (JM > 0) norm_load<JM, GB>((const float *) x.base, K, lane, pro, pv, pg, pb);
+    else st.load((const float *) x.base, K, 0);
+    uint4 cur[U];
+    float eb = 0.0f;
+    load_group(cur, eb, grp);
+    if constexpr (JM > 0) {
+        if (wid == 0) norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs, lane);
+    } else {
+        st.store(xs, kp, 0);
+        st.column((const float *) x.base, K, kp, xs, (int64_t) 4 * blockDim.x);
+    }
+    mi_lds_barrier();
+
+    for (; grp < ngroups; grp += stride) {
+        uint4 nxt[U];
+        float ebn = 0.0f;
+        load_group(nxt, ebn, grp + stride);
+        float acc = 0.0f;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (u < nit) acc = dot8(cur[u], *(const uint4 *) (xs + ((int64_t) u * kLpr + m) * kChunk), acc);
+        acc = row16_sum(acc);
+        const int64_t row = grp * 4 + rg;
+        if (m == 0 && row < N) {
+            float v = acc;
+            if (EPI >= 1) v = v + eb;
+            if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
+            dst[row] = v;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) cur[u] = nxt[u];
+        eb = ebn;
+    }
+}
+
 template <int NC, int U, bool ONE, int JM>
 void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols, float * dst,
-               size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int ks) {
+               size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int ks, int rgs) {
     const int64_t kp = (K + kKStep - 1) / kKStep * kKStep;
-    const dim3 grid((unsigned) ((N + 3) / 4), (unsigned) ((ncols + NC - 1) / NC));
-    const size_t lds = (size_t) (JM > 0 && NC == 1 ? ks : NC) * kp * sizeof(uint16_t) + (size_t) ks * 4 * NC * sizeof(float);
+    const dim3 grid((unsigned) ((N + 4 * rgs - 1) / (4 * rgs)), (unsigned) ((ncols + NC - 1) / NC));
+    const bool priv = JM > 0 && NC == 1 && rgs == 1;
+    const size_t lds = (size_t) (priv ? ks : NC) * kp * sizeof(uint16_t) + (size_t) ks * rgs * 4 * NC * sizeof(float);
     const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
     const uint8_t * w = (const uint8_t *) W;
-#define MI_GEMV_F16(EP) hipLaunchKernelGGL((k_gemv_f16<NC, EP, U, ONE, JM>), grid, dim3(64 * ks), lds, s, w, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, kp)
+#define MI_GEMV_F16(EP) hipLaunchKernelGGL((k_gemv_f16<NC, EP, U, ONE, JM>), grid, dim3(64 * ks * rgs), lds, s, w, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, kp, rgs)
     switch (epi) {
         case 0: MI_GEMV_F16(0); break;
         case 1: MI_GEMV_F16(1); break;
@@ -323,23 +399,23 @@ void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_c
 
 template <int U, bool ONE, int JM>
 void launch_u(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols, float * dst,
-              size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int nc, int ks) {
+              size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int nc, int ks, int rgs) {
     switch (nc) {
-        case 1: launch_nc<1, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks); break;
-        case 2: launch_nc<2, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks); break;
-        case 4: launch_nc<4, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks); break;
-        default: launch_nc<8, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks); break;
+        case 1: launch_nc<1, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks, rgs); break;
+        case 2: launch_nc<2, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks, rgs); break;
+        case 4: launch_nc<4, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks, rgs); break;
+        default: launch_nc<8, U, ONE, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, ks, rgs); break;
     }
 }
 
 // one register pass of `per` steps per wave: U = per rounded up to 1/2/4/8 (no wasted loads)
 template <int JM>
 void launch_one(int per, const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols,
-                float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int nc, int ks) {
-    if (per <= 1) launch_u<1, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
-    else if (per <= 2) launch_u<2, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
-    else if (per <= 4) launch_u<4, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
-    else launch_u<8, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+                float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int nc, int ks, int rgs) {
+    if (per <= 1) launch_u<1, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
+    else if (per <= 2) launch_u<2, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
+    else if (per <= 4) launch_u<4, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
+    else launch_u<8, true, JM>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
 }
 
 } // namespace
@@ -362,19 +438,38 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
     // workgroup and no more than the row's K steps, then as few as give the same steps per wave
     const int nit = (int) (kp / kKStep);
     const int64_t groups = (N + 3) / 4 * ((ncols + nc - 1) / nc);
-    const int64_t want = g_mi_tuning.f16_waves > 0 ? g_mi_tuning.f16_waves : 2048;
+    // target waves: ~8 per CU; with the norm prologue every wave reads the whole column, g and b
+    // (12 K bytes, the same lines for every wave of the chip), so fewer (~3 per CU)
+    const int64_t want = g_mi_tuning.f16_waves > 0 ? g_mi_tuning.f16_waves : (pro.mode ? 768 : 2048);
     int ks = (int) std::max<int64_t>(1, std::min<int64_t>(8, want / std::max<int64_t>(groups, 1)));
+    // very tall matrices (lm_head): row groups share one staging of the activations per workgroup
     ks = std::min(ks, nit);
     if (pro.mode) ks = std::max(ks, (nit + 7) / 8);  // the prologue path runs one register pass
     const int per = (nit + ks - 1) / ks;  // steps per wave
     ks = (nit + per - 1) / per;
     const bool one = per <= 8;
+    const int rgs = g_mi_tuning.f16_rgs > 0 ? std::max(1, std::min(g_mi_tuning.f16_rgs, 8 / ks)) : 1;
+    if (ncols == 1 && groups >= 4096 && K <= 1024 && !xh && !e.resid && !e.copy[0].ptr && g_mi_tuning.f16_rgs == 0) {
+        // tall matrix: grid-stride row groups (k_gemv_f16_tall)
+        const dim3 grid((unsigned) std::min<int64_t>((groups + 3) / 4, 512));
+        const size_t lds = (size_t) kp * sizeof(uint16_t);
+        const int epi = e.gelu_table ? 3 : (e.bias ? 1 : 0);
+        const uint8_t * w = (const uint8_t *) W;
+#define MI_GEMV_TALL(EP, JMV) hipLaunchKernelGGL((k_gemv_f16_tall<EP, 8, JMV>), grid, dim3(256), lds, s, w, nb01, K, N, x, dst, e, pro, kp)
+        if (pro.mode) {
+            if (epi == 0) MI_GEMV_TALL(0, 4); else if (epi == 1) MI_GEMV_TALL(1, 4); else MI_GEMV_TALL(3, 4);
+        } else {
+            if (epi == 0) MI_GEMV_TALL(0, 0); else if (epi == 1) MI_GEMV_TALL(1, 0); else MI_GEMV_TALL(3, 0);
+        }
+#undef MI_GEMV_TALL
+        return;
+    }
     if (pro.mode) {  // supported() guarantees one pass (K <= 3072)
-        if (K <= 1024) launch_one<4>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
-        else launch_one<12>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+        if (K <= 1024) launch_one<4>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
+        else launch_one<12>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
     } else if (one) {
-        launch_one<0>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+        launch_one<0>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
     } else {
-        launch_u<8, false, 0>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks);
+        launch_u<8, false, 0>(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
     }
 }

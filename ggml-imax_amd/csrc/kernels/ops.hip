@@ -190,6 +190,27 @@ __global__ __launch_bounds__(256) void k_get_rows_q(mi_tensor_desc d, mi_tensor_
     }
 }
 
+// get_rows(a, ia) + get_rows(b, ib) in one pass (the GPT-2 token + position embedding,
+// main-backend.cpp:475-478): each element is read exactly as k_get_rows / k_get_rows_q read it
+// and the two f32 values are added once, as the ADD node does. 1-D index vectors, f32 dst rows.
+template <int T>  // 0: f32 / f16 (ld_f), else the quantized type
+__device__ __forceinline__ float emb_elem(const mi_tensor_desc & a, int32_t r, int64_t c) {
+    if constexpr (T == 0) return ld_f(a.data + c * a.nb[0] + (size_t) r * a.nb[1], a.type);
+    else return dequant_elem<T>((const uint8_t *) a.data + (size_t) r * a.nb[1], c);
+}
+
+template <int TA, int TB>
+__global__ __launch_bounds__(256) void k_get_rows_add(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc ia, mi_tensor_desc b,
+                                                      mi_tensor_desc ib, int64_t n) {
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        const int64_t c = i % d.ne[0], r = i / d.ne[0];
+        const int32_t ra = *(const int32_t *) (ia.data + r * ia.nb[0]);
+        const int32_t rb = *(const int32_t *) (ib.data + r * ib.nb[0]);
+        const float va = emb_elem<TA>(a, ra, c), vb = emb_elem<TB>(b, rb, c);
+        *(float *) (d.data + c * d.nb[0] + r * d.nb[1]) = va + vb;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_diag_mask(mi_tensor_desc d, mi_tensor_desc a, int n_past, float value, int64_t n) {
     for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
         int64_t i0, i1, i2, i3;
@@ -406,6 +427,31 @@ void mi_op_get_rows(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi
         case 12: hipLaunchKernelGGL(k_get_rows_q<12>, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n); break;
         case 13: hipLaunchKernelGGL(k_get_rows_q<13>, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n); break;
         default: hipLaunchKernelGGL(k_get_rows, dim3(grid_for(n)), dim3(256), 0, s, d, a, idx, n); break;
+    }
+}
+
+template <int TA>
+static void launch_get_rows_add(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & ia, const mi_tensor_desc & b,
+                                const mi_tensor_desc & ib, int64_t n, hipStream_t s) {
+    const dim3 g(grid_for(n));
+    switch (b.type) {
+        case 2: hipLaunchKernelGGL((k_get_rows_add<TA, 2>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
+        case 8: hipLaunchKernelGGL((k_get_rows_add<TA, 8>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
+        case 12: hipLaunchKernelGGL((k_get_rows_add<TA, 12>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
+        case 13: hipLaunchKernelGGL((k_get_rows_add<TA, 13>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
+        default: hipLaunchKernelGGL((k_get_rows_add<TA, 0>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
+    }
+}
+
+void mi_op_get_rows_add(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & ia, const mi_tensor_desc & b,
+                        const mi_tensor_desc & ib, hipStream_t s) {
+    const int64_t n = d.ne[0] * d.ne[1];
+    switch (a.type) {
+        case 2: launch_get_rows_add<2>(d, a, ia, b, ib, n, s); break;
+        case 8: launch_get_rows_add<8>(d, a, ia, b, ib, n, s); break;
+        case 12: launch_get_rows_add<12>(d, a, ia, b, ib, n, s); break;
+        case 13: launch_get_rows_add<13>(d, a, ia, b, ib, n, s); break;
+        default: launch_get_rows_add<0>(d, a, ia, b, ib, n, s); break;
     }
 }
 

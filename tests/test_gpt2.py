@@ -250,9 +250,10 @@ def test_quantized_gpt2_logits_bit_identical_to_reference_cpu(quantized_paths, q
 @pytest.mark.gpu
 @pytest.mark.parametrize("qtype", ["f16", "q4_k", "q8_0"])
 def test_gpt2_decode_launches_per_token(model_path, quantized_paths, qtype):
-    """Node fusion keeps a decode token at 64 kernel launches for f16 and quantized models alike:
+    """Node fusion keeps a decode token at 62 kernel launches for f16 and quantized models alike:
     per layer the norm chain rides in the GEMV prologue, bias / residual / GELU and the K/V-cache
-    copies in its epilogue, the attention block is one kernel."""
+    copies in its epilogue, the attention block is one kernel; the token + position embedding
+    (two GET_ROWS and their ADD) is one kernel."""
     lib = G.runtime()
     be = G.mi355x_backend(lib)
     m = gpt2.Model(lib, model_path if qtype == "f16" else quantized_paths[qtype], be, n_ctx=1024, n_batch=8)
@@ -260,7 +261,7 @@ def test_gpt2_decode_launches_per_token(model_path, quantized_paths, qtype):
         toks = m.tokenize(PROMPT)
         m.eval(0, toks[:8])
         m.eval(8, [toks[8]])
-        assert lib.ggml_backend_mi355x_last_launch_count(be) == 64
+        assert lib.ggml_backend_mi355x_last_launch_count(be) == 62
     finally:
         m.free()
         lib.ggml_backend_free(be)

@@ -26,7 +26,8 @@ def build(rt, kind, L):
     b = rt.ggml_new_tensor_1d(c, F32, E)
     bE = rt.ggml_new_tensor_1d(c, F32, E)
     bF = rt.ggml_new_tensor_1d(c, F32, F)
-    ws = []
+    b3 = rt.ggml_new_tensor_1d(c, F32, 3 * E)
+    ws, extra = [], []
     cur = x
     for i in range(L):
         if kind == "add":
@@ -46,21 +47,38 @@ def build(rt, kind, L):
             h = rt.ggml_add(c, rt.ggml_mul(c, rt.ggml_norm(c, cur, 1e-5), g), b)
             h = rt.ggml_gelu(c, rt.ggml_add(c, rt.ggml_mul_mat(c, w1, h), bF))
             cur = rt.ggml_add(c, rt.ggml_add(c, rt.ggml_mul_mat(c, w2, h), bE), cur)
+        elif kind == "lm_head":  # ln_f + lm_head (768 x 50257), chained through the first 768 logits
+            w = rt.ggml_new_tensor_2d(c, F16, E, 50257); ws.append(w)
+            h = rt.ggml_add(c, rt.ggml_mul(c, rt.ggml_norm(c, cur, 1e-5), g), b)
+            cur = rt.ggml_view_1d(c, rt.ggml_mul_mat(c, w, h), E, 0)
+        elif kind == "c_attn":  # ln_1 + c_attn (768 x 2304) + bias + K/V cache row copies, chained through Q
+            w = rt.ggml_new_tensor_2d(c, F16, E, 3 * E); ws.append(w)
+            kc = rt.ggml_new_tensor_1d(c, F32, E); vc = rt.ggml_new_tensor_1d(c, F32, E)
+            h = rt.ggml_add(c, rt.ggml_mul(c, rt.ggml_norm(c, cur, 1e-5), g), b)
+            y = rt.ggml_add(c, rt.ggml_mul_mat(c, w, h), b3)
+            extra += [rt.ggml_cpy(c, rt.ggml_view_1d(c, y, E, 4 * E), kc), rt.ggml_cpy(c, rt.ggml_view_1d(c, y, E, 8 * E), vc)]
+            cur = rt.ggml_view_1d(c, y, E, 0)
         elif kind == "fc_gelu":
             w1 = rt.ggml_new_tensor_2d(c, F16, E, F); w2 = rt.ggml_new_tensor_2d(c, F16, F, E); ws += [w1, w2]
             h = rt.ggml_gelu(c, rt.ggml_add(c, rt.ggml_mul_mat(c, w1, cur), bF))
             cur = rt.ggml_mul_mat(c, w2, h)
     gr = rt.ggml_new_graph_custom(c, 16 * L + 64, False)
+    for t in extra:
+        rt.ggml_build_forward_expand(gr, t)
     rt.ggml_build_forward_expand(gr, cur)
-    return ctx, gr, (x, g, b, bE, bF), ws
+    return ctx, gr, (x, g, b, bE, bF, b3), ws
 
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     rt = G.runtime()
     be = G.mi355x_backend(rt)
-    L = 24
-    for kind in ("add", "mm768", "mm768_bias_resid", "ln_mm768", "fc_gelu", "mlp"):
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+    tunings = [t.split("=") for t in sys.argv[3].split(",")] if len(sys.argv) > 3 else [("f16_rgs", "0")]
+    for kind, L, (tn, tv) in [(k, 4 if k == "lm_head" else 24, t)
+                               for k in ("add", "mm768", "mm768_bias_resid", "ln_mm768", "c_attn", "fc_gelu", "mlp", "lm_head")
+                               for t in tunings if not only or k in only]:
+        rt.ggml_backend_mi355x_set_tuning(tn.encode(), int(tv))
         ctx, gr, vecs, ws = build(rt, kind, L)
         buf = rt.ggml_backend_alloc_ctx_tensors(ctx.ctx, be)
         for i, v in enumerate(vecs):
@@ -84,7 +102,7 @@ def main():
             rt.ggml_backend_graph_plan_free(be, plan)
             res[mode] = dt / reps
         launches = rt.ggml_backend_mi355x_last_launch_count(be)
-        print(f"{kind:18s} L={L}: {launches:3d} launches  plan {res['plan'] * 1e6 / launches:6.2f} us/launch "
+        print(f"{kind:18s} {tn}={tv} L={L}: {launches:3d} launches  plan {res['plan'] * 1e6 / launches:6.2f} us/launch "
               f"({res['plan'] * 1e6:7.1f} us/graph)   eager {res['eager'] * 1e6 / launches:6.2f} us/launch", flush=True)
         rt.ggml_backend_buffer_free(buf)
         ctx.free()
