@@ -1,0 +1,158 @@
+// attn_fast.hip -- the attention block of the GPT-2 graph (KQ, scale, causal mask, soft_max, KQV,
+// head merge; examples/gpt-2/main-backend.cpp:552-608) in tree order: the fast decode mode
+// (mmv_order 0). mmv_ordered.hip's k_attn_fast / k_attn_ordered replay the reference CPU's exact
+// summation order (mmv_order 1).
+//
+// What is kept from the reference: the scores are (q . k) * pre_scale (ggml_scale) masked to -inf
+// past n_past + t (diag_mask_inf) times the soft_max scale; the soft_max weights are the
+// reference's fp16 values exp(f16(s - max)) rounded to fp16 (ggml_compute_forward_soft_max_f32
+// reads them from ggml_table_exp_f16, src/ggml.c:12196-12260: here computed with expf and rounded
+// the same way, equal to the table entry except where expf and the host's expf straddle an fp16
+// rounding boundary). What differs: every sum is an f32 tree (dots, the soft_max denominator and
+// the KQV sums) and the KQV weights are applied unnormalized, the 1 / sum scaling once at the end.
+//
+// One workgroup (8 waves) per (head, query token). A key is handled by D / 8 lanes (8 head-dim
+// elements each, 2 x 16-byte loads per row), 64 keys per pass of the workgroup; the K and V rows
+// of the first 64 * KPG keys are all requested before any arithmetic. Pass 1: scores (kept in
+// LDS) and the workgroup max (one barrier); pass 2: p = exp weights, unnormalized sum p * v per
+// lane, then the waves' partial (sum p, sum p v) are added through LDS (one barrier).
+
+#include "mi355x_common.h"
+#include "mi355x_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+template <int LPK>
+__device__ __forceinline__ float group_sum(float v) {  // sum over each aligned group of LPK lanes
+#pragma unroll
+    for (int off = 1; off < LPK; off <<= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// D: head dim (64 or 128); KPG: keys per lane group held in registers per pass
+template <int D, int KPG>
+__global__ __launch_bounds__(512) void k_attn_tree(mi_attn_desc a) {
+    constexpr int LPK = D / 8;          // lanes per key
+    constexpr int GPW = 64 / LPK;       // key groups per wave
+    constexpr int G = 8 * GPW;          // key groups per workgroup
+    constexpr int CH = G * KPG;         // keys per pass
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // s[n_kv] | red[8][D + 8]
+    __shared__ float shm[8];
+    const int h = blockIdx.x, t = blockIdx.y;
+    const int hk = h / a.r2;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int j = lane % LPK;                       // 8-element slice of the head dim
+    const int grp = wave * GPW + lane / LPK;        // key group of the workgroup
+    const int n_kv = a.n_kv;
+    float * s = sm;
+
+    // q slice (8 floats), and the first pass's K and V rows, all requested up front
+    const char * qrow = a.q + (size_t) t * a.q_nb[1] + (size_t) h * a.q_nb[2] + (size_t) j * 32;
+    const float4 q0 = *(const float4 *) qrow, q1 = *(const float4 *) (qrow + 16);
+    const char * kb = a.k + (size_t) hk * a.k_nb[2] + (size_t) j * 32;
+    const char * vb = a.v + (size_t) hk * a.v_nb[2] + (size_t) j * 32;
+    float4 kr[KPG][2], vr[KPG][2];
+    auto load_rows = [&](const char * base, size_t nb, int c0, float4 (&r)[KPG][2]) {
+#pragma unroll
+        for (int kk = 0; kk < KPG; kk++) {
+            const int key = min(c0 + kk * G + grp, n_kv - 1);  // clamped: unconditional loads
+            const char * p = base + (size_t) key * nb;
+            r[kk][0] = *(const float4 *) p;
+            r[kk][1] = *(const float4 *) (p + 16);
+        }
+    };
+    load_rows(kb, a.k_nb[1], 0, kr);
+    load_rows(vb, a.v_nb[0], 0, vr);
+
+    // ---- pass 1: scores and their max
+    const int lim = a.n_past + t;  // keys k > lim are masked (diag_mask_inf)
+    float mx = -INFINITY;
+    for (int c0 = 0; c0 < n_kv; c0 += CH) {
+        if (c0) load_rows(kb, a.k_nb[1], c0, kr);
+#pragma unroll
+        for (int kk = 0; kk < KPG; kk++) {
+            float d = kr[kk][0].x * q0.x + kr[kk][0].y * q0.y + kr[kk][0].z * q0.z + kr[kk][0].w * q0.w +
+                      (kr[kk][1].x * q1.x + kr[kk][1].y * q1.y + kr[kk][1].z * q1.z + kr[kk][1].w * q1.w);
+            d = group_sum<LPK>(d);
+            const int key = c0 + kk * G + grp;
+            float w = d * a.pre_scale;
+            if (key >= a.n_past && key > lim) w = -INFINITY;
+            w = w * a.sm_scale;
+            if (key < n_kv) {
+                mx = fmaxf(mx, w);
+                if (j == 0) s[key] = w;
+            }
+        }
+    }
+    mx = mi_wave_max(mx);
+    if (lane == 0) shm[wave] = mx;
+    __syncthreads();  // s[] and shm[] complete
+    mx = shm[0];
+#pragma unroll
+    for (int w = 1; w < 8; w++) mx = fmaxf(mx, shm[w]);
+
+    // ---- pass 2: p = fp16 exp(fp16(s - max)), unnormalized sums of p and p * v
+    float l = 0.0f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < n_kv; c0 += CH) {
+        if (c0) load_rows(vb, a.v_nb[0], c0, vr);
+#pragma unroll
+        for (int kk = 0; kk < KPG; kk++) {
+            const int key = c0 + kk * G + grp;
+            if (key < n_kv) {
+                const float w = s[key];
+                const float p = w == -INFINITY ? 0.0f : mi_h2f(mi_f2h(expf(mi_h2f(mi_f2h(w - mx)))));
+                if (j == 0) l += p;
+                o[0] += p * vr[kk][0].x; o[1] += p * vr[kk][0].y; o[2] += p * vr[kk][0].z; o[3] += p * vr[kk][0].w;
+                o[4] += p * vr[kk][1].x; o[5] += p * vr[kk][1].y; o[6] += p * vr[kk][1].z; o[7] += p * vr[kk][1].w;
+            }
+        }
+    }
+    // the wave's groups: lanes of equal j hold the same head-dim slice
+#pragma unroll
+    for (int off = LPK; off < 64; off <<= 1) {
+        l += __shfl_xor(l, off, 64);
+#pragma unroll
+        for (int e = 0; e < 8; e++) o[e] += __shfl_xor(o[e], off, 64);
+    }
+    l = group_sum<LPK>(l);  // only lane j == 0 of each group accumulated l
+    float * red = sm + n_kv;  // [8 waves][D + 8]: o slices, then l at [D]
+    if (lane < LPK) {
+        float * r = red + wave * (D + 8) + lane * 8;
+#pragma unroll
+        for (int e = 0; e < 8; e++) r[e] = o[e];
+        if (lane == 0) red[wave * (D + 8) + D] = l;
+    }
+    __syncthreads();
+    if (threadIdx.x < D) {
+        const int d = threadIdx.x;
+        float num = red[d], den = red[D];
+#pragma unroll
+        for (int w = 1; w < 8; w++) {
+            num += red[w * (D + 8) + d];
+            den += red[w * (D + 8) + D];
+        }
+        *(float *) (a.out + (size_t) d * a.o_nb[0] + (size_t) t * a.o_nb[1] + (size_t) h * a.o_nb[2]) = num / den;
+    }
+}
+
+} // namespace
+
+bool mi_attn_tree_supported(const mi_attn_desc & a) {
+    return (a.D == 64 || a.D == 128) && a.n_kv >= 1 && a.q_nb[0] == 4 && a.k_nb[0] == 4 && a.v_nb[1] == 4 &&
+           ((uintptr_t) a.q | (uintptr_t) a.k | (uintptr_t) a.v | a.q_nb[1] | a.q_nb[2] | a.k_nb[1] | a.k_nb[2] | a.v_nb[0] |
+            a.v_nb[2]) % 16 == 0 &&
+           (size_t) (a.n_kv + 8 * (a.D + 8)) * 4 <= 64 * 1024;
+}
+
+void mi_attn_tree(const mi_attn_desc & a, hipStream_t s) {
+    const dim3 grid((unsigned) a.H, (unsigned) a.N);
+    const size_t lds = (size_t) (a.n_kv + 8 * (a.D + 8)) * sizeof(float);
+    if (a.D == 64) {
+        if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_tree<64, 4>), grid, dim3(512), lds, s, a);
+        else hipLaunchKernelGGL((k_attn_tree<64, 8>), grid, dim3(512), lds, s, a);
+    } else {
+        hipLaunchKernelGGL((k_attn_tree<128, 4>), grid, dim3(512), lds, s, a);
+    }
+}

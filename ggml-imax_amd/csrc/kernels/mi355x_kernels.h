@@ -234,7 +234,11 @@ struct mi_attn_desc {
     float sm_scale;         // soft_max scale (op_params[0])
 };
 bool mi_attn_supported(int D, int n_kv);
+// mmv_order 1 (or attn_variant 1): the reference's summation order, bit-identical; otherwise the
+// tree-order kernel of attn_fast.hip where it applies (mi_attn_tree_supported)
 void mi_attn_ordered(const mi_attn_desc & a, const uint16_t * exp_table, hipStream_t s);
+bool mi_attn_tree_supported(const mi_attn_desc & a);
+void mi_attn_tree(const mi_attn_desc & a, hipStream_t s);
 
 // f16 weights x f16-rounded activations
 void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s);

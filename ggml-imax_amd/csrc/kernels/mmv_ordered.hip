@@ -867,6 +867,10 @@ void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, con
 bool mi_attn_supported(int D, int n_kv) { return D >= 1 && D <= 256 && n_kv >= 1 && (size_t) (D + n_kv) * 4 <= 60 * 1024; }
 
 void mi_attn_ordered(const mi_attn_desc & a, const uint16_t * exp_table, hipStream_t s) {
+    if (g_mi_tuning.mmv_order == 0 && g_mi_tuning.attn_variant == 0 && mi_attn_tree_supported(a)) {
+        mi_attn_tree(a, s);  // attn_fast.hip: tree order (the default decode mode)
+        return;
+    }
     static const bool lds_ok = [] {  // the V slab needs more than the default 64 KB of dynamic LDS
         bool ok = true;
         for (const void * f : {(const void *) k_attn_fast<64, 128>, (const void *) k_attn_fast<64, 256>, (const void *) k_attn_fast<64, 512>,
