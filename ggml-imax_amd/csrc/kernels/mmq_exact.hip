@@ -16,9 +16,10 @@
 //   * U: one v_mfma_f32_32x32x16_f16 per superblock with exact small integers: A = [m_j, 64 m_j]
 //     (<= 4032), B = [S_j & 63, S_j >> 6] where S_j = sum of 32 q8 (the activation quantizer
 //     writes these), so every product and partial sum is an integer < 2^24: exact.
-// The float combine per superblock and the order of the superblock chain are fixed (mmqx_term
-// and one chain in superblock order) and shared by every kernel of this file, so column shards of a
-// prompt (prompt-sharded multi-GPU) give the same bits as the whole prompt. Against the
+// The float combine per superblock and the combine order are fixed (mmqx_term, chains over groups
+// of 4 superblocks, left-folded) and shared by every kernel of this file, so column shards of a
+// prompt (prompt-sharded multi-GPU) give the same bits as the whole prompt, whichever kernel runs
+// them. Against the
 // reference CPU the only difference is the f32 combine order (reference: 8-lane partial chains
 // + hsum): ~1e-7 relative.
 //
@@ -45,6 +46,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));  // 32x32 f32 accumul
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
+constexpr int kGS = 4;             // superblocks per K group (the canonical fold unit)
+constexpr int kMaxGroups = 16;     // k_mmqd: per-group partial sums of a tile in LDS
 constexpr int XBM = 64;            // weight rows per workgroup
 constexpr int XBN = 128;           // activation columns per workgroup (4 waves x 32)
 constexpr int XSK = 128;           // K per LDS stage (half a superblock)
@@ -177,8 +180,9 @@ namespace {
 // the other LDS plane buffer, plus the row operands of the combine. Activations and weights arrive a stage ahead (vmcnt is in-order: every load is
 // consumed in the order it was issued, each with one stage of lead). Two waves per SIMD: while
 // one issues its MFMAs the other runs its dequantization / combine VALU.
-// Canonical combine order (shared by every kernel of this file): one f32 chain over the
-// superblocks in increasing order, y = mmqx_term(y, ...) from y = +0.
+// Canonical combine order (shared by every kernel of this file): per group of kGS superblocks one
+// f32 chain over the group's superblocks in increasing order, y_g = mmqx_term(y_g, ...) from
+// y_g = +0, then the left fold y = y_0; y = y + y_1; y = y + y_2; ...
 template <int TYPE, bool XCD, int ABL = 0>
 __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                               mi_act_mmx act, float * __restrict__ dst, size_t ycol) {
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
         if (c8 < 2) ((float *) (ro + XBM * 32))[c8 * XBM + ar] = mi_h2f((uint16_t) (c8 == 0 ? (raw.hdr.x & 0xFFFF) : (raw.hdr.x >> 16)));
     };
 
-    f32x16 y = {};
+    f32x16 y = {}, ytot = {};
     // one stage of lead for everything: the raw weights of superblock sb + 1 are staged at the end
     // of stage sb and then reloaded with sb + 2; the activation fragment of step kk of sb + 1 is
     // loaded into the register that step kk of sb has just consumed
@@ -386,6 +390,12 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
             }
         }
         }
+        // group end (kGS superblocks, or the last): left fold of the group chains
+        if ((sb + 1) % kGS == 0 || sb == S - 1) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) ytot[i] = sb < kGS ? y[i] : ytot[i] + y[i];
+            y = f32x16{};
+        }
         // superblock sb + 1 into the other buffer, then the weights of sb + 2
         __builtin_amdgcn_sched_barrier(0);
         store_stage(cur ^ 1, raw);
@@ -401,46 +411,218 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
     for (int g = 0; g < 4; g++) {
         const int64_t n = n0 + 32 * rw + 8 * g + 4 * h;
         if (n + 3 < N) {
-            *(float4 *) (out + n) = make_float4(y[4 * g], y[4 * g + 1], y[4 * g + 2], y[4 * g + 3]);
+            *(float4 *) (out + n) = make_float4(ytot[4 * g], ytot[4 * g + 1], ytot[4 * g + 2], ytot[4 * g + 3]);
         } else {
 #pragma unroll
-            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[4 * g + e];
+            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = ytot[4 * g + e];
         }
+    }
+}
+
+
+// ---- short prompts: one wave per 32 x 32 tile and K group, weights dequantized in registers ---
+// One wave = one 32 x 32 output tile (32 prompt columns x 32 weight rows) over the K groups
+// w, w + KW, ... of kGS superblocks; a workgroup = the KW waves of one tile, whose per-group
+// partial sums meet in LDS for the canonical left fold. Orientation: the activations are the MFMA
+// A operand (accumulator row = prompt column), the weights the B operand (accumulator column =
+// weight row = the lane's own row), so every lane dequantizes its own weight row straight from the
+// 16-byte loads it issued (no LDS staging, no barrier in the K loop) and applies its own row's
+// d / dmin. Every register is reloaded with the next superblock's data as soon as it is consumed.
+// C4: ncols % 4 == 0 (the four da of an accumulator row group are one aligned 16-byte load).
+template <int TYPE, bool C4>
+__global__ __launch_bounds__(256) void k_mmqd(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
+                                              float * __restrict__ dst, size_t ycol) {
+    using F = XFmt<TYPE>;
+    constexpr int NP = F::NP;
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [group][element][lane] partial sums
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, kw = blockDim.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t ncols = act.ncols;
+    const int S = (int) (K / 256), ng = (S + kGS - 1) / kGS;
+    const int64_t nrt = (N + 31) / 32;
+    const int64_t n0 = (blockIdx.x % nrt) * 32, c0 = (blockIdx.x / nrt) * 32;
+
+    // this wave's superblocks, flattened: groups w, w + kw, ...; position i -> superblock
+    const int my_groups = (ng - w + kw - 1) / kw;
+    auto sb_of = [&](int i) -> int {
+        const int g = w + (i / kGS) * kw, sb = g * kGS + i % kGS;
+        return sb < S ? sb : S - 1;
+    };
+    int count = 0;
+    for (int gi = 0; gi < my_groups; gi++) count += min(kGS, S - (w + gi * kw) * kGS);
+
+    const int nrows = (int) std::min<int64_t>(32, N - n0);
+    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
+    const uint32_t wrow = (uint32_t) (min(r, nrows - 1) * nb01);
+    const uint32_t acol = (uint32_t) std::min<int64_t>(c0 + r, ncols - 1);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
+    const uint32_t xstep = (uint32_t) ncols * 64;
+    const uint32_t xcol = acol * 64 + 16 * h;
+    constexpr uint32_t kQs = F::Q5 ? 48 : 16;
+
+    auto ld_x = [&](int sb, int kk) -> i32x4 {
+        return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + ((uint32_t) sb * 4 + (kk >> 1)) * xstep + 32 * (kk & 1), 0, 0));
+    };
+    auto ld_w = [&](int sb, uint32_t off) -> uint4 {
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wrow + (uint32_t) sb * F::BS + off, 0, 0));
+    };
+    auto ld_u = [&](int sb) -> half8 {
+        return __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, ((uint32_t) sb * (uint32_t) ncols + acol) * 32 + 16 * h, 0, 0));
+    };
+    // da of accumulator elements 4g .. 4g + 3: prompt columns c0 + 8 g + 4 h + 0..3 (columns past
+    // ncols read another superblock's scales or, past the buffer, zeros: never stored)
+    auto ld_da = [&](int sb, int g) -> float4 {
+        const uint32_t off = (uint32_t) ((int64_t) sb * ncols + c0 + 8 * g + 4 * h) * 4;
+        if constexpr (C4) {
+            return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dres, off, 0, 0));
+        } else {
+            return make_float4(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off, 0, 0)),
+                               __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 4, 0, 0)),
+                               __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 8, 0, 0)),
+                               __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 12, 0, 0)));
+        }
+    };
+
+    int sb = sb_of(0);
+    i32x4 xa[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) xa[kk] = ld_x(sb, kk);
+    uint4 hdr = ld_w(sb, 0);
+    uint4 q4[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) q4[p] = ld_w(sb, kQs + 32 * p + 16 * h);
+    uint4 qh = F::Q5 ? ld_w(sb, 16 + 16 * h) : uint4{};
+    half8 xu = ld_u(sb);
+    float4 da[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) da[g] = ld_da(sb, g);
+
+    f32x16 y = {};
+    int gi = 0, in_group = 0;
+    int gsz = min(kGS, S - w * kGS);
+    for (int i = 0; i < count; i++) {
+        const int sn = sb_of(i + 1 < count ? i + 1 : i);
+        // header -> plane factors (splat u16x2), U operand, d, dmin (get_scale_min_k4, ggml-quants.c)
+        const uint32_t w0 = hdr.y, w1 = hdr.z, w2 = hdr.w;
+        const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
+        uint32_t fac[8][NP];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int jj = j & 3;
+            const uint32_t sc = j < 4 ? ((w0 >> (8 * jj)) & 63) : (((w2 >> (8 * jj)) & 0xF) | (((w0 >> (8 * jj + 6)) & 3) << 4));
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                const uint32_t f = F::factor((int) sc, p);
+                fac[j][p] = f | (f << 16);
+            }
+        }
+        half8 mu;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int j = 4 * h + t;  // this lane's k-halves of the U MFMA: sub-blocks 4h .. 4h + 3
+            const int jj = j & 3;
+            const uint32_t m = j < 4 ? ((w1 >> (8 * jj)) & 63) : (((w2 >> (8 * jj + 4)) & 0xF) | (((w1 >> (8 * jj + 6)) & 3) << 4));
+            mu[2 * t] = (_Float16) (float) m;
+            mu[2 * t + 1] = (_Float16) (float) (64 * m);
+        }
+        hdr = ld_w(sn, 0);
+        i32x16 acc[NP];
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const uint4 q = q4[kk >> 1];
+            uint32_t v[4] = {q.x, q.y, q.z, q.w};
+            const uint32_t hb[4] = {qh.x, qh.y, qh.z, qh.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                v[e] = (kk & 1) ? (v[e] >> 4) & 0x0F0F0F0Fu : v[e] & 0x0F0F0F0Fu;
+                if constexpr (F::Q5) v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
+            }
+            if (kk & 1) q4[kk >> 1] = ld_w(sn, kQs + 32 * (kk >> 1) + 16 * h);
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                const uint32_t f = fac[kk][p];
+                const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+                acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[kk], b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
+            }
+            xa[kk] = ld_x(sn, kk);
+        }
+        if constexpr (F::Q5) qh = ld_w(sn, 16 + 16 * h);
+        const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
+        xu = ld_u(sn);
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const float dav[4] = {da[g].x, da[g].y, da[g].z, da[g].w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int el = 4 * g + e;
+                int T = acc[NP - 1][el];
+#pragma unroll
+                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
+                y[el] = mmqx_term(y[el], T, Uv[el], dw, dm, dav[e]);
+            }
+            da[g] = ld_da(sn, g);
+        }
+        // group end: park y_g in LDS (slot = group index), the next group starts from +0
+        if (++in_group == gsz) {
+            const int g = w + gi * kw;
+#pragma unroll
+            for (int el = 0; el < 16; el++) red[(g * 16 + el) * 64 + lane] = y[el];
+            y = f32x16{};
+            in_group = 0;
+            gi++;
+            gsz = min(kGS, S - (w + gi * kw) * kGS);
+        }
+    }
+    __syncthreads();
+    if (w != 0) return;
+    // left fold over the groups in order, then the store: element el = prompt column
+    // c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
+    const int64_t n = n0 + r;
+    if (n >= N) return;
+#pragma unroll
+    for (int el = 0; el < 16; el++) {
+        float v = red[el * 64 + lane];
+        for (int g = 1; g < ng; g++) v = v + red[(g * 16 + el) * 64 + lane];
+        const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * h;
+        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = v;
     }
 }
 
 } // namespace
 
 bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t nb01) {
-    // buffer descriptors address < 2 GiB: activations K * ncols bytes, a 64-row weight block
+    // buffer descriptors address < 2 GiB: activations K * ncols bytes, a 64-row weight block;
+    // k_mmqd keeps the per-group partial sums of a tile in LDS (<= 16 groups)
     return (type == 12 || type == 13) && K % 256 == 0 && K >= 256 && ycol % 16 == 0 && K * ncols < ((int64_t) 1 << 31) &&
-           (int64_t) nb01 * XBM < ((int64_t) 1 << 31);
+           (int64_t) nb01 * XBM < ((int64_t) 1 << 31) && K / 256 <= kGS * kMaxGroups;
 }
 
 void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_mmx & act, float * dst,
                      size_t ycol, hipStream_t s) {
-    const int64_t nrt = (N + XBM - 1) / XBM, nct = (act.ncols + XBN - 1) / XBN;
-    const int64_t T = nrt * nct;
-    // variant bit 64 (GGML_MI355X_MMQ_VARIANT): XCD-contiguous tile order
-    const bool xcd = (g_mi_tuning.mmq_variant & 64) != 0;
-    const dim3 grid((unsigned) (xcd ? (T + 7) / 8 * 8 : T));
     const uint8_t * w = (const uint8_t *) W;
-    // bits 256..2048: timing ablations (results invalid): 1 no dequantization, 2 no combine, 4 no MFMAs
-    const int abl = (g_mi_tuning.mmq_variant >> 8) & 7;
-#define MI_MMQX_A(TY, A) hipLaunchKernelGGL((k_mmqx<TY, false, A>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol)
-#define MI_MMQX(TY)                                                                                                      \
-    if (abl == 1) MI_MMQX_A(TY, 1);                                                                                      \
-    else if (abl == 2) MI_MMQX_A(TY, 2);                                                                                 \
-    else if (abl == 3) MI_MMQX_A(TY, 3);                                                                                 \
-    else if (abl == 4) MI_MMQX_A(TY, 4);                                                                                 \
-    else if (abl == 7) MI_MMQX_A(TY, 7);                                                                                 \
-    else if (xcd) hipLaunchKernelGGL((k_mmqx<TY, true>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);          \
-    else hipLaunchKernelGGL((k_mmqx<TY, false>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);
-    if (type == 12) {
-        MI_MMQX(12)
-    } else {
-        MI_MMQX(13)
+    // short prompts (<= 128 columns): one wave per 32 x 32 tile and K group (k_mmqd); long ones:
+    // 64 x 128 tiles with the weights dequantized once per workgroup into LDS (k_mmqx). Both
+    // follow the same canonical combine order, so a prompt's column shards give the whole
+    // prompt's bits whichever kernel runs them (variant bit 128 forces k_mmqx, 16 k_mmqd).
+    const int var = g_mi_tuning.mmq_variant;
+    const bool direct = (var & 16) || (act.ncols <= 128 && !(var & 128));
+    if (direct) {
+        const int64_t nrt = (N + 31) / 32, nct = (act.ncols + 31) / 32;
+        const int ng = (int) ((K / 256 + kGS - 1) / kGS);
+        const int kw = std::min(ng, 4);
+        const dim3 grid((unsigned) (nrt * nct));
+        const size_t lds = (size_t) ng * 16 * 64 * sizeof(float);
+        const bool c4 = act.ncols % 4 == 0;
+#define MI_MMQD(TY, C) hipLaunchKernelGGL((k_mmqd<TY, C>), grid, dim3(64 * kw), lds, s, w, nb01, K, N, act, dst, ycol)
+        if (type == 12) { if (c4) MI_MMQD(12, true); else MI_MMQD(12, false); }
+        else { if (c4) MI_MMQD(13, true); else MI_MMQD(13, false); }
+#undef MI_MMQD
+        return;
     }
-#undef MI_MMQX
-#undef MI_MMQX_A
+    const int64_t nrt = (N + XBM - 1) / XBM, nct = (act.ncols + XBN - 1) / XBN;
+    const dim3 grid((unsigned) (nrt * nct));
+    if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);
+    else hipLaunchKernelGGL((k_mmqx<13, false>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);
 }
