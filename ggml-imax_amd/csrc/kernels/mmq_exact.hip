@@ -16,8 +16,8 @@
 //   * U: one v_mfma_f32_32x32x16_f16 per superblock with exact small integers: A = [m_j, 64 m_j]
 //     (<= 4032), B = [S_j & 63, S_j >> 6] where S_j = sum of 32 q8 (the activation quantizer
 //     writes these), so every product and partial sum is an integer < 2^24: exact.
-// The float combine per superblock and the combine order are fixed (mmqx_term, chains over groups
-// of 4 superblocks, left-folded) and shared by every kernel of this file, so column shards of a
+// The float combine per superblock and the combine order are fixed (mmqx_term, its terms
+// left-folded in superblock order) and shared by every kernel of this file, so column shards of a
 // prompt (prompt-sharded multi-GPU) give the same bits as the whole prompt, whichever kernel runs
 // them. Against the
 // reference CPU the only difference is the f32 combine order (reference: 8-lane partial chains
@@ -46,8 +46,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));  // 32x32 f32 accumul
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kGS = 4;             // superblocks per K group (the canonical fold unit)
-constexpr int kMaxGroups = 16;     // k_mmqd: per-group partial sums of a tile in LDS
 constexpr int XBM = 64;            // weight rows per workgroup
 constexpr int XBN = 128;           // activation columns per workgroup (4 waves x 32)
 constexpr int XSK = 128;           // K per LDS stage (half a superblock)
@@ -60,10 +58,11 @@ __device__ __forceinline__ uint32_t mulb(uint32_t x, uint32_t m) {
     return __builtin_bit_cast(uint32_t, a * b);
 }
 
-// the canonical per-superblock combine (every kernel of the family uses exactly this)
-__device__ __forceinline__ float mmqx_term(float y, int T, float U, float dw, float dm, float da) {
+// the canonical per-superblock term (every kernel of the family uses exactly this); the terms of
+// an output are then left-folded in superblock order: y = term_0; y = y + term_1; ...
+__device__ __forceinline__ float mmqx_term(int T, float U, float dw, float dm, float da) {
     const float t = __builtin_fmaf(-dm, U, dw * (float) T);
-    return __builtin_fmaf(da, t, y);
+    return __builtin_fmaf(da, t, 0.0f);
 }
 
 template <int TYPE>
@@ -101,43 +100,16 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K_mmx(mi_src_cols x, int64_
     const float * col = (const float *) (x.base + i1 * x.nb1 + i2 * x.nb2 + i3 * x.nb3);
     const float4 v4 = *(const float4 *) (col + b * 256 + lane * 4);
     const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-    // quantize_row_q8_K_reference: first max-|x| element (sign kept), iscale = -127/max,
-    // q = min(127, nearest_int(iscale*x)) -- as quantize.hip's k_quantize_q8_K, bit for bit
-    float amax = 0.0f, vmax = 0.0f;
-    int idx = 0x7fffffff;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const float ax = fabsf(v[i]);
-        if (ax > amax) { amax = ax; vmax = v[i]; idx = lane * 4 + i; }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float oa = __shfl_xor(amax, off, 64);
-        const float ov = __shfl_xor(vmax, off, 64);
-        const int oi = __shfl_xor(idx, off, 64);
-        if (oa > amax || (oa == amax && oi < idx)) { amax = oa; vmax = ov; idx = oi; }
-    }
-    uint32_t packed = 0;
-    int sum = 0;
-    float d = 0.0f;
-    if (amax != 0.0f) {
-        const float iscale = -127.f / vmax;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int bits = __float_as_int(__builtin_fmaf(iscale, v[i], 12582912.f));
-            int q = (bits & 0x007fffff) - 0x00400000;
-            q = q < 127 ? q : 127;
-            sum += q;
-            packed |= ((uint32_t) (q & 0xFF)) << (8 * i);
-        }
-        d = 1.0f / iscale;
-    }
+    // quantize_row_q8_K_reference as the reference's -mfma build computes it (mi355x_common.h:
+    // first max-|x| element keeps its sign, iscale = -127/max, fma rounding trick); DPP
+    // reductions, sums of 32 per 8-lane group
+    uint32_t packed;
+    int sum;
+    float d;
+    mi_q8K_superblock(v, lane, packed, sum, d);
     const int64_t ncols = act.ncols;
     // element k = lane*4 .. +3 of the superblock: 64-block lane/16, offset (lane%16)*4
     *(uint32_t *) (act.xq + ((b * 4 + (lane >> 4)) * ncols + c) * 64 + (lane & 15) * 4) = packed;
-    sum += __shfl_xor(sum, 1, 64);
-    sum += __shfl_xor(sum, 2, 64);
-    sum += __shfl_xor(sum, 4, 64);  // lanes 8j..8j+7: S_j (sub-block j of 32)
     if ((lane & 7) == 0) {
         const int j = lane >> 3;
         const uint32_t lo = mi_f2h((float) (sum & 63)), hi = mi_f2h((float) (sum >> 6));
@@ -180,9 +152,8 @@ namespace {
 // the other LDS plane buffer, plus the row operands of the combine. Activations and weights arrive a stage ahead (vmcnt is in-order: every load is
 // consumed in the order it was issued, each with one stage of lead). Two waves per SIMD: while
 // one issues its MFMAs the other runs its dequantization / combine VALU.
-// Canonical combine order (shared by every kernel of this file): per group of kGS superblocks one
-// f32 chain over the group's superblocks in increasing order, y_g = mmqx_term(y_g, ...) from
-// y_g = +0, then the left fold y = y_0; y = y + y_1; y = y + y_2; ...
+// Canonical combine order (shared by every kernel of this file): the superblock terms
+// (mmqx_term) left-folded in superblock order, y = term_0; y = y + term_1; ...
 template <int TYPE, bool XCD, int ABL = 0>
 __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                               mi_act_mmx act, float * __restrict__ dst, size_t ycol) {
@@ -305,7 +276,7 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
         if (c8 < 2) ((float *) (ro + XBM * 32))[c8 * XBM + ar] = mi_h2f((uint16_t) (c8 == 0 ? (raw.hdr.x & 0xFFFF) : (raw.hdr.x >> 16)));
     };
 
-    f32x16 y = {}, ytot = {};
+    f32x16 y = {};
     // one stage of lead for everything: the raw weights of superblock sb + 1 are staged at the end
     // of stage sb and then reloaded with sb + 2; the activation fragment of step kk of sb + 1 is
     // loaded into the register that step kk of sb has just consumed
@@ -386,15 +357,10 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
                 int T = acc[NP - 1][i];
 #pragma unroll
                 for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][i];
-                y[i] = mmqx_term(y[i], T, Uv[i], dw[e], dm[e], da);
+                const float term = mmqx_term(T, Uv[i], dw[e], dm[e], da);
+                y[i] = sb == 0 ? term : y[i] + term;
             }
         }
-        }
-        // group end (kGS superblocks, or the last): left fold of the group chains
-        if ((sb + 1) % kGS == 0 || sb == S - 1) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) ytot[i] = sb < kGS ? y[i] : ytot[i] + y[i];
-            y = f32x16{};
         }
         // superblock sb + 1 into the other buffer, then the weights of sb + 2
         __builtin_amdgcn_sched_barrier(0);
@@ -411,45 +377,37 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
     for (int g = 0; g < 4; g++) {
         const int64_t n = n0 + 32 * rw + 8 * g + 4 * h;
         if (n + 3 < N) {
-            *(float4 *) (out + n) = make_float4(ytot[4 * g], ytot[4 * g + 1], ytot[4 * g + 2], ytot[4 * g + 3]);
+            *(float4 *) (out + n) = make_float4(y[4 * g], y[4 * g + 1], y[4 * g + 2], y[4 * g + 3]);
         } else {
 #pragma unroll
-            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = ytot[4 * g + e];
+            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[4 * g + e];
         }
     }
 }
 
 
-// ---- short prompts: one wave per 32 x 32 tile and K group, weights dequantized in registers ---
-// One wave = one 32 x 32 output tile (32 prompt columns x 32 weight rows) over the K groups
-// w, w + KW, ... of kGS superblocks; a workgroup = the KW waves of one tile, whose per-group
-// partial sums meet in LDS for the canonical left fold. Orientation: the activations are the MFMA
-// A operand (accumulator row = prompt column), the weights the B operand (accumulator column =
-// weight row = the lane's own row), so every lane dequantizes its own weight row straight from the
-// 16-byte loads it issued (no LDS staging, no barrier in the K loop) and applies its own row's
-// d / dmin. Every register is reloaded with the next superblock's data as soon as it is consumed.
+// ---- short prompts: a workgroup of NWV waves per 32 x 32 tile, superblocks dealt round-robin ---
+// Wave w of the tile computes the terms of superblocks w, w + NWV, ... (one per round) for the
+// tile's 32 prompt columns x 32 weight rows; after each round wave 0 left-folds the round's terms
+// from LDS in superblock order. Orientation: the activations are the MFMA A operand (accumulator
+// row = prompt column), the weights the B operand (accumulator column = weight row = the lane's
+// own row), so every lane dequantizes its own weight row straight from the 16-byte loads it
+// issued and applies its own row's d / dmin. Each wave's registers are reloaded with its next
+// round's superblock as soon as they are consumed (one round of lead).
 // C4: ncols % 4 == 0 (the four da of an accumulator row group are one aligned 16-byte load).
 template <int TYPE, bool C4>
-__global__ __launch_bounds__(256) void k_mmqd(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
+__global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
                                               float * __restrict__ dst, size_t ycol) {
     using F = XFmt<TYPE>;
     constexpr int NP = F::NP;
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [group][element][lane] partial sums
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, kw = blockDim.x >> 6;
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [wave][lane][16] terms of a round
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int64_t ncols = act.ncols;
-    const int S = (int) (K / 256), ng = (S + kGS - 1) / kGS;
+    const int S = (int) (K / 256);
+    const int rounds = (S + nw - 1) / nw;
     const int64_t nrt = (N + 31) / 32;
     const int64_t n0 = (blockIdx.x % nrt) * 32, c0 = (blockIdx.x / nrt) * 32;
-
-    // this wave's superblocks, flattened: groups w, w + kw, ...; position i -> superblock
-    const int my_groups = (ng - w + kw - 1) / kw;
-    auto sb_of = [&](int i) -> int {
-        const int g = w + (i / kGS) * kw, sb = g * kGS + i % kGS;
-        return sb < S ? sb : S - 1;
-    };
-    int count = 0;
-    for (int gi = 0; gi < my_groups; gi++) count += min(kGS, S - (w + gi * kw) * kGS);
 
     const int nrows = (int) std::min<int64_t>(32, N - n0);
     const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
@@ -485,7 +443,7 @@ __global__ __launch_bounds__(256) void k_mmqd(const uint8_t * __restrict__ W, si
         }
     };
 
-    int sb = sb_of(0);
+    int sb = w < S ? w : S - 1;
     i32x4 xa[8];
 #pragma unroll
     for (int kk = 0; kk < 8; kk++) xa[kk] = ld_x(sb, kk);
@@ -499,11 +457,12 @@ __global__ __launch_bounds__(256) void k_mmqd(const uint8_t * __restrict__ W, si
 #pragma unroll
     for (int g = 0; g < 4; g++) da[g] = ld_da(sb, g);
 
-    f32x16 y = {};
-    int gi = 0, in_group = 0;
-    int gsz = min(kGS, S - w * kGS);
-    for (int i = 0; i < count; i++) {
-        const int sn = sb_of(i + 1 < count ? i + 1 : i);
+    f32x16 y = {};  // the fold (wave 0)
+    float * mine = red + ((size_t) w * 64 + lane) * 16;
+    for (int rd = 0; rd < rounds; rd++) {
+        const int cur = rd * nw + w;
+        int sn = cur + nw;
+        sn = sn < S ? sn : S - 1;
         // header -> plane factors (splat u16x2), U operand, d, dmin (get_scale_min_k4, ggml-quants.c)
         const uint32_t w0 = hdr.y, w1 = hdr.z, w2 = hdr.w;
         const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
@@ -551,6 +510,7 @@ __global__ __launch_bounds__(256) void k_mmqd(const uint8_t * __restrict__ W, si
         if constexpr (F::Q5) qh = ld_w(sn, 16 + 16 * h);
         const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
         xu = ld_u(sn);
+        float term[16];
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const float dav[4] = {da[g].x, da[g].y, da[g].z, da[g].w};
@@ -560,33 +520,37 @@ __global__ __launch_bounds__(256) void k_mmqd(const uint8_t * __restrict__ W, si
                 int T = acc[NP - 1][el];
 #pragma unroll
                 for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
-                y[el] = mmqx_term(y[el], T, Uv[el], dw, dm, dav[e]);
+                term[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
             }
             da[g] = ld_da(sn, g);
         }
-        // group end: park y_g in LDS (slot = group index), the next group starts from +0
-        if (++in_group == gsz) {
-            const int g = w + gi * kw;
+        // the round's terms meet in LDS; wave 0 folds them in superblock order
 #pragma unroll
-            for (int el = 0; el < 16; el++) red[(g * 16 + el) * 64 + lane] = y[el];
-            y = f32x16{};
-            in_group = 0;
-            gi++;
-            gsz = min(kGS, S - (w + gi * kw) * kGS);
+        for (int q = 0; q < 4; q++) *(float4 *) (mine + 4 * q) = make_float4(term[4 * q], term[4 * q + 1], term[4 * q + 2], term[4 * q + 3]);
+        mi_lds_barrier();
+        if (w == 0) {
+            const int nv = min(nw, S - rd * nw);
+            for (int v = 0; v < nv; v++) {
+                const float * src = red + ((size_t) v * 64 + lane) * 16;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 t4 = *(const float4 *) (src + 4 * q);
+                    const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) y[4 * q + e] = (rd == 0 && v == 0) ? tv[e] : y[4 * q + e] + tv[e];
+                }
+            }
         }
+        mi_lds_barrier();
     }
-    __syncthreads();
     if (w != 0) return;
-    // left fold over the groups in order, then the store: element el = prompt column
-    // c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
+    // store: element el = prompt column c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
     const int64_t n = n0 + r;
     if (n >= N) return;
 #pragma unroll
     for (int el = 0; el < 16; el++) {
-        float v = red[el * 64 + lane];
-        for (int g = 1; g < ng; g++) v = v + red[(g * 16 + el) * 64 + lane];
         const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * h;
-        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = v;
+        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y[el];
     }
 }
 
@@ -594,15 +558,14 @@ __global__ __launch_bounds__(256) void k_mmqd(const uint8_t * __restrict__ W, si
 
 bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t nb01) {
     // buffer descriptors address < 2 GiB: activations K * ncols bytes, a 64-row weight block;
-    // k_mmqd keeps the per-group partial sums of a tile in LDS (<= 16 groups)
     return (type == 12 || type == 13) && K % 256 == 0 && K >= 256 && ycol % 16 == 0 && K * ncols < ((int64_t) 1 << 31) &&
-           (int64_t) nb01 * XBM < ((int64_t) 1 << 31) && K / 256 <= kGS * kMaxGroups;
+           (int64_t) nb01 * XBM < ((int64_t) 1 << 31);
 }
 
 void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_mmx & act, float * dst,
                      size_t ycol, hipStream_t s) {
     const uint8_t * w = (const uint8_t *) W;
-    // short prompts (<= 128 columns): one wave per 32 x 32 tile and K group (k_mmqd); long ones:
+    // short prompts (<= 128 columns): 8 waves per 32 x 32 tile, superblocks round-robin (k_mmqd); long ones:
     // 64 x 128 tiles with the weights dequantized once per workgroup into LDS (k_mmqx). Both
     // follow the same canonical combine order, so a prompt's column shards give the whole
     // prompt's bits whichever kernel runs them (variant bit 128 forces k_mmqx, 16 k_mmqd).
@@ -610,12 +573,12 @@ void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N
     const bool direct = (var & 16) || (act.ncols <= 128 && !(var & 128));
     if (direct) {
         const int64_t nrt = (N + 31) / 32, nct = (act.ncols + 31) / 32;
-        const int ng = (int) ((K / 256 + kGS - 1) / kGS);
-        const int kw = std::min(ng, 4);
+        const int S = (int) (K / 256);
+        const int nwv = std::min(S, 8);  // waves per tile (superblocks dealt round-robin)
         const dim3 grid((unsigned) (nrt * nct));
-        const size_t lds = (size_t) ng * 16 * 64 * sizeof(float);
+        const size_t lds = (size_t) nwv * 64 * 16 * sizeof(float);
         const bool c4 = act.ncols % 4 == 0;
-#define MI_MMQD(TY, C) hipLaunchKernelGGL((k_mmqd<TY, C>), grid, dim3(64 * kw), lds, s, w, nb01, K, N, act, dst, ycol)
+#define MI_MMQD(TY, C) hipLaunchKernelGGL((k_mmqd<TY, C>), grid, dim3(64 * nwv), lds, s, w, nb01, K, N, act, dst, ycol)
         if (type == 12) { if (c4) MI_MMQD(12, true); else MI_MMQD(12, false); }
         else { if (c4) MI_MMQD(13, true); else MI_MMQD(13, false); }
 #undef MI_MMQD
