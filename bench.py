@@ -286,7 +286,7 @@ def torch_view(torch, lib, t, device):
     return torch.as_tensor(_DevArray(G.tensor_data_ptr(lib, t), n), device=device)
 
 
-def rowsplit_prefill(lib, backend, dist, world, rank, device, torch, steps=5, K=4096, N=4096, B=512):
+def rowsplit_prefill(lib, backend, dist, world, rank, device, torch, steps=5, K=4096, N=4096, B=512, return_y=False):
     """Optional tensor-split row path over RCCL (north_star "RCCL only for
     the optional tensor-split row path"): rank r holds rows row_shard(N) of one Q4_K weight; per
     step rank 0's prompt activations X (f32 [K, B]) are broadcast to every rank (RCCL over xGMI),
@@ -339,11 +339,28 @@ def rowsplit_prefill(lib, backend, dist, world, rank, device, torch, steps=5, K=
     y_full = reassemble_rows(y_all.cpu().numpy(), N, world, B)
     res = {"workload": f"Q4_K {K}x{N} x B={B}, rows split over {world} ranks: RCCL broadcast of X, local GEMM, RCCL all-gather of Y",
            "rows_per_rank": rows, "TFLOP/s": round(2.0 * K * N * B * steps / dt / 1e12, 2),
-           "us_per_step": round(dt / steps * 1e6, 2),
-           "y_checksum": float(np.abs(y_full).sum())}
+           "us_per_step": round(dt / steps * 1e6, 2)}
+    res.update(rowsplit_parity(y_full, K, N, B))
     lib.ggml_backend_buffer_free(buf)
     ctx.free()
-    return res
+    return (res, y_full) if return_y else res
+
+
+def rowsplit_parity(y_full, K, N, B):
+    """Element-wise check of the reassembled Y [B, N] against the reference's own output for this
+    exact workload (tests/golden: BASELINE config 5, weights splitmix64 seed 42 quantized to Q4_K,
+    X seed 43; every 16th column from the reference CPU build, plus the SHA-256 of its whole Y)."""
+    gold = os.path.join(REPO, "tests", "golden")
+    try:
+        man = {c["name"]: c for c in json.load(open(os.path.join(gold, "manifest.json")))["cases"]}
+        c = man[f"P_q4_K_{K}x{N}_b{B}"]
+        ys = np.fromfile(os.path.join(gold, c["name"] + ".ys.f32"), dtype=np.float32).reshape(-1, N)
+    except (OSError, KeyError, ValueError):
+        return {"parity": "no golden fixture for this shape"}
+    got = y_full[::c["y_col_step"]]
+    err = float(np.max(np.abs(got.astype(np.float64) - ys)) / np.max(np.abs(ys)))
+    return {"max_rel_err_vs_reference": err, "parity_ok": err <= 1e-5,
+            "parity": f"every {c['y_col_step']}th column ({got.shape[0]} x {N}) element-wise vs the reference CPU output (<= 1e-5)"}
 
 
 def timed_region(run, sync, dist=None, device=None):

@@ -621,6 +621,27 @@ static void invalidate_activations(mi_backend_ctx * ctx, const ggml_tensor * wri
             c.end());
 }
 
+// the batched (prompt) GEMM applies: more than 8 columns of plain 2-D operands
+static bool mm_batched(const mi_mm_desc & m, const ggml_tensor * src1) {
+    static const bool no_mmq = getenv("GGML_MI355X_NO_MMQ") != nullptr;
+    return !no_mmq && act_kind((ggml_type) m.type) >= 0 && src1->ne[1] > 8 && m.ne02 == 1 && m.ne03 == 1 && m.ne12 == 1 &&
+           m.ne13 == 1 && mi_mmq_supported(m.type, m.K, m.nb01, m.nb1) && ((uintptr_t) m.W % 16) == 0;
+}
+
+// The activation format mul_mat_run converts src1 to for this mul_mat (act_bytes kinds), or -1
+// (F32 weights: src1 is read as it lies). Q4_K / Q5_K prompts: the exact-integer int8 GEMM's
+// layouts (8); other batched types: f16 operands (2 / 3 / 4, K-blocked + 3); decode: q8 SoA
+// (0 / 1) or f16 (2).
+static int mm_act_kind(const mi_mm_desc & m, const ggml_tensor * src1) {
+    const int kind = act_kind((ggml_type) m.type);
+    if (kind < 0) return -1;
+    if (!mm_batched(m, src1)) return kind;
+    const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
+    // GGML_MI355X_MMQ_VARIANT bit 32 selects the f16 GEMM for K-quants too (A/B timing)
+    if (kind == 1 && (g_mi_tuning.mmq_variant & 32) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01)) return 8;
+    return (kind == 2 ? 2 : kind + 3) + (mi_mmq_wants_blocked() ? 3 : 0);
+}
+
 // The mul_mat of (src0, src1) with src0's rows taken from (W, N) and the output written at out
 // (column strides nb1..nb3): op_mul_mat runs the whole node through it, the split-buffer path
 // (op_mul_mat_split) each device's row slice.
@@ -650,33 +671,24 @@ static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const vo
     m.nb2 = nb2;
     m.nb3 = nb3;
 
-    const int kind = act_kind(src0->type);
-    if (kind < 0) {
+    const int xkind = mm_act_kind(m, src1);
+    if (xkind < 0) {
         MI_ASSERT(src0->type == GGML_TYPE_F32);
         mi_mul_mat_f32(m, src_cols(src1), ctx->stream);
     } else {
         const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
-        static const bool no_mmq = getenv("GGML_MI355X_NO_MMQ") != nullptr;
-        const bool batched = !no_mmq && src1->ne[1] > 8 && m.ne02 == 1 && m.ne03 == 1 && m.ne12 == 1 && m.ne13 == 1 &&
-                             mi_mmq_supported(m.type, m.K, m.nb01, m.nb1) && ((uintptr_t) m.W % 16) == 0;
-        // Q4_K / Q5_K: the exact-integer int8 MFMA GEMM (mmq_exact.hip); GGML_MI355X_MMQ_VARIANT
-        // bit 32 selects the f16 GEMM below instead (A/B timing)
-        const bool exact = batched && kind == 1 && (g_mi_tuning.mmq_variant & 32) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01);
-        if (exact) {
-            const int64_t nc = ncols;
-            mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, mi_act_mmx_carve(get_activations(ctx, src1, 8, m.K), m.K, nc), m.dst,
-                            m.nb1, ctx->stream);
-        } else if (batched) {
+        void * xa = get_activations(ctx, src1, xkind, m.K);
+        if (xkind == 8) {
+            // Q4_K / Q5_K: the exact-integer int8 MFMA GEMM (mmq_exact.hip)
+            mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, mi_act_mmx_carve(xa, m.K, ncols), m.dst, m.nb1, ctx->stream);
+        } else if (xkind >= 3 || (xkind == 2 && mm_batched(m, src1))) {
             // the GEMM's activation operand: f16 for F16 weights, else f16(d * q) of the q8 quants
-            // written by the quantizer itself (kinds 3/4)
-            const bool blk = mi_mmq_wants_blocked();
-            const int xkind = (kind == 2 ? 2 : kind + 3) + (blk ? 3 : 0);
-            const uint16_t * xh = (const uint16_t *) get_activations(ctx, src1, xkind, m.K);
-            mi_mul_mat_mmq(m.type, m.W, m.nb01, m.K, m.N, mi_act_q8{}, xh, ncols, m.dst, m.nb1, nullptr, ctx->stream);
-        } else if (kind == 2) {
-            mi_mul_mat_f16(m, (const uint16_t *) get_activations(ctx, src1, kind, m.K), ctx->stream);
+            // written by the quantizer itself (kinds 3/4, K-blocked 5..7)
+            mi_mul_mat_mmq(m.type, m.W, m.nb01, m.K, m.N, mi_act_q8{}, (const uint16_t *) xa, ncols, m.dst, m.nb1, nullptr, ctx->stream);
+        } else if (xkind == 2) {
+            mi_mul_mat_f16(m, (const uint16_t *) xa, ctx->stream);
         } else {
-            mi_mul_mat_q(m, mi_act_q8_carve(get_activations(ctx, src1, kind, m.K), m.K, ncols, kind == 1), ctx->stream);
+            mi_mul_mat_q(m, mi_act_q8_carve(xa, m.K, ncols, xkind == 1), ctx->stream);
         }
     }
     ctx->last_launches++;
@@ -720,9 +732,13 @@ static mi_split_aux * split_aux(int slot, int main_device) {
 }
 
 // GGML_OP_MUL_MAT with a weight in the split buffer type (ggml-cuda.cu:1360-1647 analogue): the
-// slot on the backend's own device computes its rows in place into dst; every other slot gets
-// src1 copied to its device (peer copy over xGMI), computes its rows on its own stream into local
-// scratch, and copies them back into dst's row range (a pitched copy), ordered by events.
+// slot on the backend's own device computes its rows in place into dst; every other slot gets the
+// activations copied to its device (peer copy over xGMI), computes its rows on its own stream into
+// local scratch, and copies them back into dst's row range (a pitched copy), ordered by events.
+// As the reference quantizes src1 once and ships the q8_1 blocks (ggml-cuda.cu:1551-1565), the
+// activations are converted ONCE on the main device, in the format the slots' kernels read (q8_K
+// / q8_0 blocks, or f16), and those bytes travel -- for Q4_K at K = 4096 4.4 KB per column
+// instead of the f32 column's 16 KB; only F32 weights ship f32.
 static void op_mul_mat_split(mi_backend_ctx * ctx, ggml_tensor * dst) {
     const ggml_tensor * src0 = dst->src[0];
     const ggml_tensor * src1 = dst->src[1];
@@ -731,51 +747,84 @@ static void op_mul_mat_split(mi_backend_ctx * ctx, ggml_tensor * dst) {
     MI_ASSERT(src1->type == GGML_TYPE_F32 && ggml_is_contiguous(src1) && dst->nb[0] == sizeof(float));
     const auto * extra = (const mi_split_extra *) src0->extra;
     const int64_t K = src0->ne[0], ncols = src1->ne[1];
-    bool ready_recorded = false;
-    std::vector<mi_split_aux *> waits;
+    // the backend's own slot (the first slot placed on its device) runs in place; further slots on
+    // the same device (GGML_MI355X_SPLIT_SLOTS > device count) take the copy path
+    auto is_local = [&](const mi_split_slice & sl) { return sl.device == ctx->device && sl.slot == ctx->device % split_slots(); };
+    // the activation format of each remote slot's mul_mat, converted on the main stream first
+    struct remote {
+        const mi_split_slice * sl;
+        int64_t ld;
+        int xkind;        // act_bytes kind shipped, -1: the f32 columns
+        const void * xa;  // converted activations on the main device
+    };
+    std::vector<remote> rem;
     for (const auto & sl : extra->slices) {
+        if (is_local(sl)) continue;
+        const int64_t rows = sl.row_high - sl.row_low;
+        remote rm{&sl, (rows + 3) & ~(int64_t) 3, -1, src1->data};
+        mi_mm_desc m{};
+        m.W = sl.ptr;
+        m.type = src0->type;
+        m.K = K;
+        m.N = rows;
+        m.ne02 = m.ne03 = m.ne12 = m.ne13 = 1;
+        m.nb01 = src0->nb[1];
+        m.ne11 = ncols;
+        m.nb1 = (size_t) rm.ld * sizeof(float);
+        rm.xkind = mm_act_kind(m, src1);
+        if (rm.xkind >= 0) rm.xa = get_activations(ctx, src1, rm.xkind, K);
+        rem.push_back(rm);
+    }
+    if (!rem.empty()) {
+        mi_device_guard g(ctx->device);
+        if (!ctx->split_ready) MI_CHECK(hipEventCreateWithFlags(&ctx->split_ready, hipEventDisableTiming));
+        MI_CHECK(hipEventRecord(ctx->split_ready, ctx->stream));  // src1 and its conversions are ready
+    }
+    for (const auto & sl : extra->slices) {
+        if (!is_local(sl)) continue;
+        mul_mat_run(ctx, src0, sl.ptr, sl.row_high - sl.row_low, src1, (float *) ((char *) dst->data + sl.row_low * sizeof(float)),
+                    dst->nb[1], dst->nb[2], dst->nb[3]);
+    }
+    std::vector<mi_split_aux *> waits;
+    for (const remote & rm : rem) {
+        const mi_split_slice & sl = *rm.sl;
         const int64_t rows = sl.row_high - sl.row_low;
         float * out = (float *) ((char *) dst->data + sl.row_low * sizeof(float));
-        // the backend's own slot (the first slot placed on its device) runs in place; further
-        // slots on the same device (GGML_MI355X_SPLIT_SLOTS > device count) take the copy path
-        if (sl.device == ctx->device && sl.slot == ctx->device % split_slots()) {
-            mul_mat_run(ctx, src0, sl.ptr, rows, src1, out, dst->nb[1], dst->nb[2], dst->nb[3]);
-            continue;
-        }
         mi_split_aux * a = split_aux(sl.slot, ctx->device);
-        if (!ready_recorded) {
-            mi_device_guard g(ctx->device);
-            if (!ctx->split_ready) MI_CHECK(hipEventCreateWithFlags(&ctx->split_ready, hipEventDisableTiming));
-            MI_CHECK(hipEventRecord(ctx->split_ready, ctx->stream));
-            ready_recorded = true;
-        }
         mi_device_guard g(a->ctx.device);
         MI_CHECK(hipStreamWaitEvent(a->ctx.stream, ctx->split_ready, 0));
-        const int64_t ld = (rows + 3) & ~(int64_t) 3;  // 16-byte aligned local columns
-        const size_t xbytes = (size_t) K * ncols * sizeof(float);
-        const size_t ybytes = (size_t) ld * ncols * sizeof(float);
-        const int kind = act_kind(src0->type);
-        size_t need = xbytes + ybytes + 4 * kBufferAlign;
-        if (kind >= 0) need += act_bytes(kind, K, ncols) + act_bytes(kind == 2 ? 5 : kind + 6, K, ncols) + 2 * kBufferAlign;
-        scratch_reserve(&a->ctx, need);  // stream-ordered reuse: earlier users of this scratch ran on the same stream
+        const size_t xbytes = rm.xkind >= 0 ? act_bytes(rm.xkind, K, ncols) : (size_t) K * ncols * sizeof(float);
+        const size_t ybytes = (size_t) rm.ld * ncols * sizeof(float);
+        scratch_reserve(&a->ctx, xbytes + ybytes + 4 * kBufferAlign);  // stream-ordered reuse: earlier users ran on the same stream
         a->ctx.scratch_used = 0;
         a->ctx.act_cache.clear();
         void * xl = scratch_take(&a->ctx, xbytes);
         float * yl = (float *) scratch_take(&a->ctx, ybytes);
         if (a->ctx.device == ctx->device) {
-            MI_CHECK(hipMemcpyAsync(xl, src1->data, xbytes, hipMemcpyDeviceToDevice, a->ctx.stream));
+            MI_CHECK(hipMemcpyAsync(xl, rm.xa, xbytes, hipMemcpyDeviceToDevice, a->ctx.stream));
         } else {
-            MI_CHECK(hipMemcpyPeerAsync(xl, a->ctx.device, src1->data, ctx->device, xbytes, a->ctx.stream));
+            MI_CHECK(hipMemcpyPeerAsync(xl, a->ctx.device, rm.xa, ctx->device, xbytes, a->ctx.stream));
         }
-        ggml_tensor x1 = *src1;  // src1 as it lies on the slot's device
+        ggml_tensor x1 = *src1;  // src1 as the slot sees it (the f32 columns or their conversion)
         x1.data = xl;
         x1.view_src = nullptr;
         x1.view_offs = 0;
+        if (rm.xkind >= 0) {
+            // the slot's mul_mat finds its activations already converted
+            mi_act_cache_entry e;
+            e.data = xl;
+            e.nbytes = ggml_nbytes(src1);
+            e.kind = rm.xkind;
+            memcpy(e.ne, x1.ne, sizeof(e.ne));
+            memcpy(e.nb, x1.nb, sizeof(e.nb));
+            e.dev = xl;
+            a->ctx.act_cache.push_back(e);
+        }
         a->ctx.last_launches = 0;
-        mul_mat_run(&a->ctx, src0, sl.ptr, rows, &x1, yl, (size_t) ld * sizeof(float), (size_t) ld * ncols * sizeof(float),
-                    (size_t) ld * ncols * sizeof(float));
+        mul_mat_run(&a->ctx, src0, sl.ptr, rows, &x1, yl, (size_t) rm.ld * sizeof(float), (size_t) rm.ld * ncols * sizeof(float),
+                    (size_t) rm.ld * ncols * sizeof(float));
         ctx->last_launches += a->ctx.last_launches;
-        MI_CHECK(hipMemcpy2DAsync(out, dst->nb[1], yl, (size_t) ld * sizeof(float), (size_t) rows * sizeof(float), (size_t) ncols,
+        MI_CHECK(hipMemcpy2DAsync(out, dst->nb[1], yl, (size_t) rm.ld * sizeof(float), (size_t) rows * sizeof(float), (size_t) ncols,
                                   hipMemcpyDeviceToDevice, a->ctx.stream));
         MI_CHECK(hipEventRecord(a->done, a->ctx.stream));
         waits.push_back(a);
