@@ -215,7 +215,7 @@ static const char * mi_host_buft_name(ggml_backend_buffer_type_t) { return "MI35
 
 static ggml_backend_buffer_t mi_host_buft_alloc(ggml_backend_buffer_type_t buft, size_t size) {
     void * ptr = nullptr;
-    if (hipHostMalloc(&ptr, std::max(size, (size_t) 1), hipHostMallocPortable) != hipSuccess) {
+    if (hipHostMalloc(&ptr, std::max(size, (size_t) 1), hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) {
         (void) hipGetLastError();
         // fall back to pageable host memory of the runtime's host buffer type
         return ggml_backend_buft_alloc_buffer(ggml_backend_cpu_buffer_type(), size);
@@ -432,6 +432,14 @@ struct mi_backend_ctx {
     std::vector<hipGraphExec_t> exec_pool;  // executable graphs of freed plans, for in-place update
     int graph_fail_streak = 0;         // consecutive re-instantiations (update refused)
     int64_t graph_stats[4] = {};       // captures, instantiations, updates, direct computes
+    // a node value still held as partial sums (try_fuse_attn_proj): `out` = sum_h parts[h], to be
+    // stored by its consumer's kernel (the next GEMV's norm prologue) or by mi_sum_parts
+    struct {
+        const ggml_tensor * out = nullptr;
+        float * parts = nullptr;
+        int nparts = 0;
+        int64_t n = 0;
+    } pend;
 };
 
 static ggml_guid_t mi_guid() {
@@ -987,6 +995,11 @@ static size_t graph_scratch_bytes(const ggml_cgraph * cgraph) {
     for (int i = 0; i < cgraph->n_nodes; i++) {
         const ggml_tensor * n = cgraph->nodes[i];
         if (n->op != GGML_OP_MUL_MAT) continue;
+        if (n->src[0]->type == GGML_TYPE_F16 && n->src[1]->op == GGML_OP_CONT && n->src[1]->ne[1] == 1) {
+            // an attention output projection: room for its per-head partial sums (try_fuse_attn_proj;
+            // head dim >= 64, so at most K / 64 heads)
+            total += ((size_t) (n->src[0]->ne[0] / 64) * n->src[0]->ne[1] * sizeof(float) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+        }
         const int kind = act_kind(n->src[0]->type);
         if (kind < 0) continue;
         const ggml_tensor * b = n->src[1];
@@ -1231,8 +1244,16 @@ static int collect_epilogue(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const 
     return last;
 }
 
+// stores a value left as partial sums (ctx->pend) before anything else reads it
+static void flush_pending(mi_backend_ctx * ctx) {
+    if (!ctx->pend.out) return;
+    mi_sum_parts((float *) ctx->pend.out->data, ctx->pend.parts, ctx->pend.nparts, ctx->pend.n, ctx->stream);
+    ctx->last_launches++;
+    ctx->pend = {};
+}
+
 // pro / pro_x: the src1 of this mul_mat is the output of a norm chain (norm -> mul g -> add b)
-// that the kernel computes itself from pro_x
+// that the kernel computes itself from pro_x (pro->parts: pro_x is the pending partial-sum value)
 static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_uses & u,
                              const mi_norm_prologue * pro = nullptr, const ggml_tensor * pro_x = nullptr) {
     ggml_tensor * mm = g->nodes[i];
@@ -1257,6 +1278,16 @@ static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const
     if (res_t && !safe_alias(out, res_t)) return -1;
     const uint16_t * xh = nullptr;
     if (pro && (overlaps(out, x) || (x->nb[1] % sizeof(float)) != 0)) return -1;
+    if (pro && pro->parts) {
+        // only the tree-order kernel sums partials
+        if (g_mi_tuning.mmv_order != 0 || !mi_mul_mat_f16_fast_supported(w->ne[0], x->ne[1], src_cols(x), nullptr, *pro)) return -1;
+        // x (stored by the first workgroup) must not be read by the others through the epilogue
+        if ((bias_t && overlaps(x, bias_t)) || (res_t && overlaps(x, res_t))) return -1;
+        mi_mul_mat_f16_fast(w->data, w->nb[1], w->ne[0], N, src_cols(x), nullptr, x->ne[1], (float *) out->data, out->nb[1], e, *pro,
+                            ctx->stream);
+        ctx->last_launches++;
+        return last;
+    }
     if (overlaps(out, x)) {
         uint16_t * tmp = (uint16_t *) scratch_take(ctx, act_bytes(2, w->ne[0], x->ne[1]));
         mi_convert_f16(src_cols(x), w->ne[0], tmp, ctx->stream);
@@ -1346,10 +1377,25 @@ static int try_fuse_norm(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_
         pro.b = bias;
         pro.eps = op_param_f(norm, 0);
         pro.mode = norm->op == GGML_OP_RMS_NORM ? 2 : 1;
+        if (ctx->pend.out && ctx->pend.out == norm->src[0] && ctx->pend.n == E) {
+            // the norm's input is still partial sums (try_fuse_attn_proj): added in the prologue,
+            // stored by the GEMV's first workgroup
+            mi_norm_prologue pp = pro;
+            pp.parts = ctx->pend.parts;
+            pp.nparts = ctx->pend.nparts;
+            pp.store = (float *) ctx->pend.out->data;
+            const int r = try_fuse_f16_gemv(ctx, g, m, u, &pp, norm->src[0]);
+            if (r >= 0) {
+                ctx->pend = {};
+                return r;
+            }
+        }
+        flush_pending(ctx);
         int r = try_fuse_f16_gemv(ctx, g, m, u, &pro, norm->src[0]);
         if (r < 0 && (fuse_mask_q() & 32)) r = try_fuse_q_gemv(ctx, g, m, u, &pro, norm->src[0]);
         if (r >= 0) return r;
     }
+    flush_pending(ctx);
     if (!safe_alias(out, norm->src[0]) || overlaps(out, mul->src[1]) || (bias && overlaps(out, g->nodes[last]->src[1]))) return -1;
     mi_op_norm(desc(out), desc(norm->src[0]), op_param_f(norm, 0), norm->op == GGML_OP_RMS_NORM,
                (const float *) mul->src[1]->data, bias, ctx->stream);
@@ -1546,6 +1592,50 @@ static void plan_attention(const ggml_cgraph * g, const mi_uses & u, std::vector
 #undef MI_ATTN_SKIP
 }
 
+// At an attention block's KQV node: the block, the F16 output projection consuming its merged
+// output (GPT-2's c_proj, main-backend.cpp:610-620) and that projection's bias and residual ADDs
+// as one k_attn_proj launch, whose result stays as per-head partial sums (ctx->pend) until its
+// consumer adds them (tree-order decode mode only). Returns the last node covered, or -1.
+static int try_fuse_attn_proj(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_attn_plan & pl, const mi_uses & u) {
+    if (g_mi_tuning.mmv_order != 0 || g_mi_tuning.attn_variant != 0 || pl.d.N != 1) return -1;
+    const int j = next_node(g, i);
+    if (j < 0) return -1;
+    ggml_tensor * mm = g->nodes[j];
+    const ggml_tensor * M = pl.merged;
+    if (mm->op != GGML_OP_MUL_MAT || mm->src[1] != M || u.of(M) != 1 || (M->flags & GGML_TENSOR_FLAG_OUTPUT)) return -1;
+    const ggml_tensor * w = mm->src[0];
+    if (is_split_tensor(w) || w->type != GGML_TYPE_F16 || w->ne[2] != 1 || w->ne[3] != 1 || w->nb[0] != 2) return -1;
+    if (M->ne[0] != w->ne[0] || M->ne[1] != 1 || M->ne[2] != 1 || M->ne[3] != 1) return -1;
+    if (!mi_attn_proj_supported(pl.d, w->ne[0], w->ne[1], w->nb[1], w->data)) return -1;
+    const int64_t N = w->ne[1];
+    const int k1 = next_node(g, j);
+    if (k1 < 0 || !private_intermediate(mm, u)) return -1;
+    ggml_tensor * a1 = g->nodes[k1];
+    const ggml_tensor * bias = add_operand(a1, mm);
+    if (!bias || !is_vec_f32(bias, N) || !ggml_are_same_shape(a1, mm) || a1->nb[0] != sizeof(float)) return -1;
+    const int k2 = next_node(g, k1);
+    if (k2 < 0 || !private_intermediate(a1, u)) return -1;
+    ggml_tensor * a2 = g->nodes[k2];
+    const ggml_tensor * res = add_operand(a2, a1);
+    if (!res || res == a1 || !is_vec_f32(res, N) || !is_vec_f32(a2, N)) return -1;
+    if ((size_t) pl.d.H * N * sizeof(float) > (size_t) (w->ne[0] / 64) * N * sizeof(float)) return -1;  // graph_scratch_bytes
+    float * parts = (float *) scratch_take(ctx, (size_t) pl.d.H * N * sizeof(float));
+    mi_attn_proj_desc p;
+    p.W = (const uint8_t *) w->data;
+    p.nb01 = w->nb[1];
+    p.N = N;
+    p.bias = (const float *) bias->data;
+    p.resid = (const float *) res->data;
+    p.parts = parts;
+    mi_attn_proj(pl.d, p, ctx->stream);
+    ctx->last_launches++;
+    ctx->pend.out = a2;
+    ctx->pend.parts = parts;
+    ctx->pend.nparts = pl.d.H;
+    ctx->pend.n = N;
+    return k2;
+}
+
 static bool is_copy(const ggml_tensor * t) {
     return (t->op == GGML_OP_CPY || t->op == GGML_OP_DUP || t->op == GGML_OP_CONT) && is_f16_or_f32(t->src[0]) && is_f16_or_f32(t) &&
            ggml_nelements(t) == ggml_nelements(t->src[0]);
@@ -1720,8 +1810,10 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
     ctx->last_launches = 0;
     static const bool no_fuse = getenv("GGML_MI355X_NO_FUSED_MMV") != nullptr;
     static const bool no_node_fusion = getenv("GGML_MI355X_NO_NODE_FUSION") != nullptr;
-    // bit mask of enabled node fusions (debug/A-B): 1 norm, 2 softmax, 4 f16 GEMV, 8 copies, 16 attention, 64 embedding
+    // bit mask of enabled node fusions (debug/A-B): 1 norm, 2 softmax, 4 f16 GEMV, 8 copies, 16 attention,
+    // 64 embedding, 128 attention + output projection
     static const int fuse_mask = getenv("GGML_MI355X_FUSE_MASK") ? atoi(getenv("GGML_MI355X_FUSE_MASK")) : 0xff;
+    ctx->pend = {};
     mi_uses uses;
     std::vector<uint8_t> absorbed_nodes;
     std::vector<mi_attn_plan> attn;
@@ -1759,10 +1851,21 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
             }
         }
         if (is_noop(node) || absorbed(i)) continue;
+        if (ctx->pend.out) {
+            // a value held as partial sums is stored before any node but its norm consumer runs
+            const bool consumer = !no_node_fusion && (fuse_mask & 1) && (node->op == GGML_OP_NORM || node->op == GGML_OP_RMS_NORM) &&
+                                  node->src[0] == ctx->pend.out;
+            if (!consumer) flush_pending(ctx);
+        }
         if (next_attn < attn.size() && attn[next_attn].kqv == i) {
-            mi_attn_ordered(attn[next_attn].d, op_tables(ctx), ctx->stream);
-            ctx->last_launches++;
+            const int lastp = (fuse_mask & 128) ? try_fuse_attn_proj(ctx, cgraph, i, attn[next_attn], uses) : -1;
+            if (lastp < 0) {
+                mi_attn_ordered(attn[next_attn].d, op_tables(ctx), ctx->stream);
+                ctx->last_launches++;
+            }
             invalidate_activations(ctx, attn[next_attn].merged);  // written here, at the KQV node
+            for (int k = i + 1; k <= lastp; k++) invalidate_activations(ctx, cgraph->nodes[k]);
+            if (lastp >= 0) i = lastp;
             next_attn++;
             continue;
         }
@@ -1793,6 +1896,7 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
             i = last;
             continue;
         }
+        flush_pending(ctx);
         switch (node->op) {
             case GGML_OP_MUL_MAT:
                 if (!no_fuse && fused_mv_eligible(node)) {
@@ -1806,6 +1910,7 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
         }
         invalidate_activations(ctx, node);
     }
+    flush_pending(ctx);
     tl_absorbed = nullptr;
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
@@ -2094,6 +2199,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "f16_waves") == 0 && value >= 0) {
         g_mi_tuning.f16_waves = value;
+        return true;
+    }
+    if (strcmp(name, "f16_ps_waves") == 0 && (value == 0 || value == 2 || value == 4 || value == 8)) {
+        g_mi_tuning.f16_ps_waves = value;
         return true;
     }
     if (strcmp(name, "f16_rgs") == 0 && value >= 0 && value <= 8) {

@@ -69,6 +69,11 @@ struct gpt2_model {
     // within us_compute: enqueue of the graph, next-graph build, wait for the device, logits copy
     int64_t us_launch = 0, us_prebuild = 0, us_wait = 0, us_readback = 0;
     std::vector<int32_t> tok, pos;  // input staging, alive until the next eval
+    // gpt2_model_load_ex with a host buffer type: the token ids and positions live in host memory
+    // the device reads in place (no upload), and the logits come back through a host staging
+    // tensor copied into right behind the graph on the backend's queue
+    bool host_io = false;
+    ggml_tensor * logits_host = nullptr;
     // scheduler mode (examples/gpt-2/main-sched.cpp): layers split over backends
     std::vector<ggml_backend_t> backends;       // [gpu, ..., cpu]
     std::vector<ggml_backend_buffer_t> buffers_w;
@@ -309,7 +314,12 @@ ggml_cgraph * build_graph(gpt2_model & m, int n_past, int N, int slot = 0) {
     ggml_cgraph * gf = ggml_new_graph_custom(ctx, kMaxNodes, false);
 
     ggml_tensor * embd, * position;
-    if (m.embd_in) {
+    if (m.host_io) {
+        // host-resident inputs: pos_in holds 0 .. n_ctx - 1 for good, so a graph's positions are a
+        // view at n_past and only the token ids change per eval
+        embd = ggml_view_1d(ctx, m.embd_in, N, 0);
+        position = ggml_view_1d(ctx, m.pos_in, N, (size_t) n_past * sizeof(int32_t));
+    } else if (m.embd_in) {
         // scheduler mode: views of persistent input tensors (main-sched.cpp:562-570)
         embd = ggml_view_1d(ctx, m.embd_in, N, 0);
         position = ggml_view_1d(ctx, m.pos_in, N, 0);
@@ -407,6 +417,11 @@ void split_words(std::string str, std::vector<std::string> & words) {
 extern "C" {
 
 gpt2_model * gpt2_model_load(const char * fname, ggml_backend_t backend, int n_ctx, int n_batch) {
+    return gpt2_model_load_ex(fname, backend, n_ctx, n_batch, nullptr);
+}
+
+gpt2_model * gpt2_model_load_ex(const char * fname, ggml_backend_t backend, int n_ctx, int n_batch,
+                                ggml_backend_buffer_type_t host_buft) {
     if (!backend) {
         fprintf(stderr, "gpt2_model_load: no backend\n");
         return nullptr;
@@ -417,8 +432,30 @@ gpt2_model * gpt2_model_load(const char * fname, ggml_backend_t backend, int n_c
         gpt2_model_free(m);
         return nullptr;
     }
-    m->allocr = ggml_gallocr_new(ggml_backend_get_default_buffer_type(backend));
     const int n_tokens = std::min(m->hp.n_ctx, n_batch > 0 ? n_batch : 8);
+    if (host_buft) {
+        ggml_init_params ip = {ggml_tensor_overhead() * 3, nullptr, true};
+        m->ctx_in = ggml_init(ip);
+        m->embd_in = ggml_new_tensor_1d(m->ctx_in, GGML_TYPE_I32, m->hp.n_ctx);
+        m->pos_in = ggml_new_tensor_1d(m->ctx_in, GGML_TYPE_I32, m->hp.n_ctx);
+        m->logits_host = ggml_new_tensor_2d(m->ctx_in, GGML_TYPE_F32, m->hp.n_vocab, n_tokens);
+        ggml_set_name(m->embd_in, "in/embd");
+        ggml_set_name(m->pos_in, "in/position");
+        ggml_set_name(m->logits_host, "out/logits");
+        m->buffer_input = ggml_backend_alloc_ctx_tensors_from_buft(m->ctx_in, host_buft);
+        // the device reads these in place: a buffer the type fell back to (e.g. pageable memory,
+        // another buffer type) will not do
+        if (!m->buffer_input || m->buffer_input->buft != host_buft || !ggml_backend_buffer_is_host(m->buffer_input)) {
+            fprintf(stderr, "gpt2_model_load: host input buffer allocation failed (or not a host buffer type)\n");
+            gpt2_model_free(m);
+            return nullptr;
+        }
+        std::vector<int32_t> pos(m->hp.n_ctx);
+        for (int i = 0; i < m->hp.n_ctx; i++) pos[i] = i;
+        ggml_backend_tensor_set(m->pos_in, pos.data(), 0, pos.size() * sizeof(int32_t));
+        m->host_io = true;
+    }
+    m->allocr = ggml_gallocr_new(ggml_backend_get_default_buffer_type(backend));
     ggml_cgraph * gf = build_graph(*m, m->hp.n_ctx - n_tokens, n_tokens);
     if (!ggml_gallocr_reserve(m->allocr, gf)) {
         fprintf(stderr, "gpt2_model_load: compute buffer reservation failed\n");
@@ -581,23 +618,33 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
         t1b = now_us();
     }
     m->next_gf = nullptr;
-    // inputs go in on the backend's queue, ordered before the graph (ggml_backend_tensor_set_async,
-    // ggml-backend.h): no host round trip per input
-    ggml_tensor * embd = ggml_graph_get_tensor(gf, "embd");
-    ggml_tensor * position = ggml_graph_get_tensor(gf, "position");
-    m->pos.resize(N);
-    m->tok.assign(tokens, tokens + N);
-    for (int i = 0; i < N; i++) m->pos[i] = n_past + i;
-    ggml_backend_tensor_set_async(m->backend, embd, m->tok.data(), 0, (size_t) N * ggml_element_size(embd));
-    ggml_backend_tensor_set_async(m->backend, position, m->pos.data(), 0, (size_t) N * sizeof(int32_t));
+    if (m->host_io) {
+        // the device reads the ids in place: the previous eval synchronized, so nothing reads them now
+        memcpy(m->embd_in->data, tokens, (size_t) N * sizeof(int32_t));
+    } else {
+        // inputs go in on the backend's queue, ordered before the graph (ggml_backend_tensor_set_async,
+        // ggml-backend.h): no host round trip per input
+        ggml_tensor * embd = ggml_graph_get_tensor(gf, "embd");
+        ggml_tensor * position = ggml_graph_get_tensor(gf, "position");
+        m->pos.resize(N);
+        m->tok.assign(tokens, tokens + N);
+        for (int i = 0; i < N; i++) m->pos[i] = n_past + i;
+        ggml_backend_tensor_set_async(m->backend, embd, m->tok.data(), 0, (size_t) N * ggml_element_size(embd));
+        ggml_backend_tensor_set_async(m->backend, position, m->pos.data(), 0, (size_t) N * sizeof(int32_t));
+    }
     const int64_t t2 = now_us();
     const ggml_status st = plan ? ggml_backend_graph_plan_compute(m->backend, plan) : ggml_backend_graph_compute_async(m->backend, gf);
     if (st != GGML_STATUS_SUCCESS) {
         fprintf(stderr, "gpt2_eval: graph compute failed\n");
         return 1;
     }
-    const int64_t t2b = now_us();
     ggml_tensor * out = ggml_graph_get_tensor(gf, "logits");
+    const size_t nv = (size_t) m->hp.n_vocab;
+    const size_t lg_off = all_logits ? 0 : sizeof(float) * nv * (N - 1), lg_size = sizeof(float) * nv * (all_logits ? N : 1);
+    // logits staged through host memory by a copy queued right behind the graph
+    const bool staged = m->host_io && lg_size <= ggml_nbytes(m->logits_host);
+    if (staged) ggml_backend_tensor_get_async(m->backend, out, m->logits_host->data, lg_off, lg_size);
+    const int64_t t2b = now_us();
     // While the device runs this graph, build and allocate the next decode step's (one token at
     // n_past + N) in the other arena: the graph depends on positions only, not on the token the
     // caller will pick from these logits. The allocator only assigns addresses in the compute
@@ -616,9 +663,15 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
     const int64_t t2c = now_us();
     ggml_backend_synchronize(m->backend);
     const int64_t t2d = now_us();
-    const size_t nv = (size_t) m->hp.n_vocab;
-    if (all_logits) ggml_backend_tensor_get(out, logits, 0, sizeof(float) * nv * N);
-    else ggml_backend_tensor_get(out, logits, sizeof(float) * nv * (N - 1), sizeof(float) * nv);
+    if (staged) {
+        if (logits) memcpy(logits, m->logits_host->data, lg_size);  // else: the caller reads gpt2_logits_host()
+    } else {
+        if (!logits) {
+            fprintf(stderr, "gpt2_eval: logits == NULL needs the host staging of gpt2_model_load_ex\n");
+            return 1;
+        }
+        ggml_backend_tensor_get(out, logits, lg_off, lg_size);
+    }
     const int64_t t3 = now_us();
     if (plan) ggml_backend_graph_plan_free(m->backend, plan);  // its graph has run
     m->us_launch = t2b - t2;
@@ -661,6 +714,8 @@ int gpt2_tokenize(const gpt2_model * m, const char * text, int32_t * out, int ma
     }
     return n;
 }
+
+const float * gpt2_logits_host(const gpt2_model * m) { return m->host_io ? (const float *) m->logits_host->data : nullptr; }
 
 void gpt2_last_eval_timing(const gpt2_model * m, int64_t * us4) {
     us4[0] = m->us_launch;

@@ -152,7 +152,13 @@ int main(int argc, char ** argv) {
     }
 
     const int64_t t_load0 = ggml_time_us();
-    gpt2_model * model = gpt2_model_load(p.model.c_str(), backend, p.n_ctx, p.n_batch);
+    // on the MI355X backend: inputs read in place from pinned host memory, logits staged through it
+    ggml_backend_buffer_type_t host_buft = nullptr;
+    typedef ggml_backend_buffer_type_t (*host_buft_fn)(void);
+    if (strcmp(ggml_backend_name(backend), "CPU") != 0) {
+        if (auto fn = (host_buft_fn) dlsym(RTLD_DEFAULT, "ggml_backend_mi355x_host_buffer_type")) host_buft = fn();
+    }
+    gpt2_model * model = gpt2_model_load_ex(p.model.c_str(), backend, p.n_ctx, p.n_batch, host_buft);
     if (!model) {
         fprintf(stderr, "%s: failed to load model from '%s'\n", __func__, p.model.c_str());
         ggml_backend_free(backend);

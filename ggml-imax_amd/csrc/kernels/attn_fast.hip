@@ -24,6 +24,8 @@
 
 namespace {
 
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
 template <int LPK>
 __device__ __forceinline__ float group_sum(float v) {  // sum over each aligned group of LPK lanes
 #pragma unroll
@@ -31,16 +33,15 @@ __device__ __forceinline__ float group_sum(float v) {  // sum over each aligned 
     return v;
 }
 
-// D: head dim (64 or 128); KPG: keys per lane group held in registers per pass
+// One (head h, query token t) of the block by the workgroup's 8 waves. D: head dim (64 or 128);
+// KPG: keys per lane group held in registers per pass. sm: LDS of n_kv + 8 (D + 8) floats.
+// Returns, in threads d < D, element d of the head's output (num / den); other threads return 0.
 template <int D, int KPG>
-__global__ __launch_bounds__(512) void k_attn_tree(mi_attn_desc a) {
+__device__ __forceinline__ float attn_head(const mi_attn_desc & a, int h, int t, float * sm, float * shm) {
     constexpr int LPK = D / 8;          // lanes per key
     constexpr int GPW = 64 / LPK;       // key groups per wave
     constexpr int G = 8 * GPW;          // key groups per workgroup
     constexpr int CH = G * KPG;         // keys per pass
-    extern __shared__ __attribute__((aligned(16))) float sm[];  // s[n_kv] | red[8][D + 8]
-    __shared__ float shm[8];
-    const int h = blockIdx.x, t = blockIdx.y;
     const int hk = h / a.r2;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int j = lane % LPK;                       // 8-element slice of the head dim
@@ -125,6 +126,7 @@ __global__ __launch_bounds__(512) void k_attn_tree(mi_attn_desc a) {
         if (lane == 0) red[wave * (D + 8) + D] = l;
     }
     __syncthreads();
+    float res = 0.0f;
     if (threadIdx.x < D) {
         const int d = threadIdx.x;
         float num = red[d], den = red[D];
@@ -133,8 +135,63 @@ __global__ __launch_bounds__(512) void k_attn_tree(mi_attn_desc a) {
             num += red[w * (D + 8) + d];
             den += red[w * (D + 8) + D];
         }
-        *(float *) (a.out + (size_t) d * a.o_nb[0] + (size_t) t * a.o_nb[1] + (size_t) h * a.o_nb[2]) = num / den;
+        res = num / den;
     }
+    return res;
+}
+
+template <int D, int KPG>
+__global__ __launch_bounds__(512) void k_attn_tree(mi_attn_desc a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // s[n_kv] | red[8][D + 8]
+    __shared__ float shm[8];
+    const int h = blockIdx.x, t = blockIdx.y;
+    const float r = attn_head<D, KPG>(a, h, t, sm, shm);
+    if (threadIdx.x < D)
+        *(float *) (a.out + (size_t) threadIdx.x * a.o_nb[0] + (size_t) t * a.o_nb[1] + (size_t) h * a.o_nb[2]) = r;
+}
+
+// Attention of one decode token fused with the output projection that consumes it (GPT-2's
+// c_proj, main-backend.cpp:610-620): workgroup (row block rb, head h) computes head h's output
+// (attn_head; rounded to f16, as the F16 GEMV rounds its activations), then the partial product
+// of rows rb * RPW .. + RPW of W over that head's D input columns: part[h][row]. Head 0 adds the
+// bias and the residual (the graph's two ADDs), so that sum_h part[h] (in head order) is the
+// projection's final output; the consumer (mi_sum_parts, or the next GEMV's norm prologue) adds
+// the H partials. Each workgroup of a head repeats that head's attention (K/V rows from L2).
+// Weights: D / 8 lanes per row, one 16-byte chunk each, requested before the attention.
+template <int D, int KPG>
+__global__ __launch_bounds__(512) void k_attn_proj(mi_attn_desc a, mi_attn_proj_desc p) {
+    constexpr int LPR = D / 8;           // lanes per weight row
+    constexpr int RPW = 512 / LPR;       // rows per workgroup
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // s[n_kv] | red[8][D + 8] | (16 B aligned) oh[D] f16
+    __shared__ float shm[8];
+    const int rb = blockIdx.x, h = blockIdx.y;
+    const int c = threadIdx.x % LPR;
+    const int64_t row = (int64_t) rb * RPW + threadIdx.x / LPR;
+    const int64_t rc = row < p.N ? row : p.N - 1;
+    const uint4 w = *(const uint4 *) (p.W + rc * p.nb01 + ((size_t) h * D + c * 8) * 2);
+    const float e_bias = p.bias[rc], e_res = p.resid[rc];  // requested before the attention too
+    const float r = attn_head<D, KPG>(a, h, 0, sm, shm);
+    uint16_t * oh = (uint16_t *) (sm + ((a.n_kv + 3) & ~3) + 8 * (D + 8));  // 16-byte aligned
+    if (threadIdx.x < D) oh[threadIdx.x] = mi_f2h(r);
+    __syncthreads();
+    const uint4 x = *(const uint4 *) (oh + c * 8);
+    float acc = 0.0f;
+    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w.x), __builtin_bit_cast(f16x2, x.x), acc, false);
+    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w.y), __builtin_bit_cast(f16x2, x.y), acc, false);
+    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w.z), __builtin_bit_cast(f16x2, x.z), acc, false);
+    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w.w), __builtin_bit_cast(f16x2, x.w), acc, false);
+    acc = group_sum<LPR>(acc);
+    // head 0: (x + bias) + resid, the order of the unfused epilogue
+    if (c == 0 && row < p.N) p.parts[(size_t) h * p.N + row] = h == 0 ? (acc + e_bias) + e_res : acc;
+}
+
+// out[i] = sum_h parts[h][i], in head order
+__global__ void k_sum_parts(float * __restrict__ out, const float * __restrict__ parts, int nparts, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float v = parts[i];
+    for (int h = 1; h < nparts; h++) v += parts[(size_t) h * n + i];
+    out[i] = v;
 }
 
 } // namespace
@@ -155,4 +212,21 @@ void mi_attn_tree(const mi_attn_desc & a, hipStream_t s) {
     } else {
         hipLaunchKernelGGL((k_attn_tree<128, 4>), grid, dim3(512), lds, s, a);
     }
+}
+
+bool mi_attn_proj_supported(const mi_attn_desc & a, int64_t K, int64_t N, size_t nb01, const void * W) {
+    return a.D == 64 && a.N == 1 && mi_attn_tree_supported(a) && K == (int64_t) a.D * a.H && N >= 1 && N <= (1 << 20) &&
+           nb01 % 16 == 0 && (uintptr_t) W % 16 == 0 && (size_t) (a.n_kv + 3 + 8 * (a.D + 8) + a.D) * 4 <= 64 * 1024;
+}
+
+void mi_attn_proj(const mi_attn_desc & a, const mi_attn_proj_desc & p, hipStream_t s) {
+    constexpr int RPW = 512 / (64 / 8);
+    const dim3 grid((unsigned) ((p.N + RPW - 1) / RPW), (unsigned) a.H);
+    const size_t lds = (size_t) (a.n_kv + 3 + 8 * (a.D + 8) + a.D) * sizeof(float);
+    if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_proj<64, 4>), grid, dim3(512), lds, s, a, p);
+    else hipLaunchKernelGGL((k_attn_proj<64, 8>), grid, dim3(512), lds, s, a, p);
+}
+
+void mi_sum_parts(float * out, const float * parts, int nparts, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_sum_parts, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, out, parts, nparts, n);
 }

@@ -117,6 +117,7 @@ struct mi_tuning {
     int mmv_order;    // decode GEMVs (quantized and F16): 1 = the reference CPU's summation order (bit-identical, slower), 0 = tree sums
     int f16_waves;    // fast F16 decode GEMV: target waves on the chip (0 = automatic)
     int f16_rgs;      // fast F16 decode GEMV: row groups (4 rows) per workgroup (0 = automatic)
+    int f16_ps_waves; // k_gemv_f16_ps (GEMV over summed partials): waves per workgroup, 2 / 4 / 8 (0 = automatic)
 };
 extern mi_tuning g_mi_tuning;
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);
@@ -204,6 +205,11 @@ struct mi_norm_prologue {
     const float * b = nullptr;  // [K] or null
     float eps = 0.0f;
     int mode = 0;               // 0 none, 1 norm, 2 rms_norm
+    // the norm's input as partial sums (mi_attn_proj's output; fast F16 path, one column only):
+    // x = sum_{p < nparts} parts[p][0 .. K), and the first workgroup stores x to `store`
+    const float * parts = nullptr;
+    int nparts = 0;
+    float * store = nullptr;
 };
 bool mi_mul_mat_f16_fused_supported(int64_t K, int64_t ncols);
 // xh: optional f16 [ncols][K] activations already converted (then x is not read)
@@ -239,6 +245,21 @@ bool mi_attn_supported(int D, int n_kv);
 void mi_attn_ordered(const mi_attn_desc & a, const uint16_t * exp_table, hipStream_t s);
 bool mi_attn_tree_supported(const mi_attn_desc & a);
 void mi_attn_tree(const mi_attn_desc & a, hipStream_t s);
+// one decode token's attention fused with the F16 output projection W [K = D H, N] that consumes
+// it, plus the projection's bias and residual ADDs: parts[h][i] = W[i, hD .. hD + D) . o_h (head 0
+// also + bias[i] + resid[i]); sum_h parts[h] (head order) is the projection's output
+struct mi_attn_proj_desc {
+    const uint8_t * W;
+    size_t nb01;
+    int64_t N;
+    const float * bias;   // [N]
+    const float * resid;  // [N]
+    float * parts;        // [H][N]
+};
+bool mi_attn_proj_supported(const mi_attn_desc & a, int64_t K, int64_t N, size_t nb01, const void * W);
+void mi_attn_proj(const mi_attn_desc & a, const mi_attn_proj_desc & p, hipStream_t s);
+// out[i] = sum_{h < nparts} parts[h][i], in h order
+void mi_sum_parts(float * out, const float * parts, int nparts, int64_t n, hipStream_t s);
 
 // f16 weights x f16-rounded activations
 void mi_mul_mat_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s);

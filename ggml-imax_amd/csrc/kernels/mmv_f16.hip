@@ -378,6 +378,105 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
     }
 }
 
+// The F16 GEMV of one column whose input is a norm chain over a value still held as partial sums
+// (mi_attn_proj's per-head parts, mi_norm_prologue::parts): workgroup = RW waves x 4 rows (RW =
+// blockDim / 64), each wave the whole K of its rows in one register pass. The workgroup adds the
+// parts once (QPT groups of 4 elements per thread, parts in order, all loads before the
+// weights') into LDS, the first workgroup also storing the sum (the graph value it stands for);
+// then every wave normalizes the column into its own f16 copy (no second barrier) and runs its
+// rows. NPM: parts capacity (registers), >= pro.nparts.
+constexpr int kPsMaxParts = 16;
+template <int EPI, int U, int JM, int NPM, int QPT>
+__global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                     float * __restrict__ dst, mi_f16_epilogue e, mi_norm_prologue pro, int64_t kp) {
+    const int rw = blockDim.x >> 6;
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [rw][kp] f16 per wave, then [kp] f32 (the sum)
+    float * xf = (float *) (xs + (size_t) rw * kp);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int m = lane & (kLpr - 1), rg = lane >> 4;
+    const int64_t row = ((int64_t) blockIdx.x * rw + wid) * 4 + rg;
+    const bool live = row < N;
+    const int nit = (int) ((K + kKStep - 1) / kKStep);
+    const int64_t k8 = K / kChunk;
+    const uint8_t * wrow = W + (live ? row : 0) * nb01;
+
+    // the parts of this thread's QPT x 4 elements (threads past K share one clamped line)
+    float4 pp[QPT][NPM];
+#pragma unroll
+    for (int r = 0; r < QPT; r++) {
+        const int64_t q4 = ((int64_t) r * blockDim.x + threadIdx.x) * 4;
+        const int64_t kq = q4 < K ? q4 : K - 4;
+#pragma unroll
+        for (int q = 0; q < NPM; q++) pp[r][q] = *(const float4 *) (pro.parts + (int64_t) (q < pro.nparts ? q : 0) * K + kq);
+    }
+    // g, b of the lane's norm elements, the epilogue's bias / residual
+    float4 pg[JM], pb[JM];
+#pragma unroll
+    for (int j = 0; j < JM; j++) {
+        const int64_t k = (int64_t) j * 256 + lane * 4;
+        const int64_t kc = k < K ? k : K - 4;
+        pg[j] = *(const float4 *) ((pro.g ? pro.g : pro.parts) + kc);
+        pb[j] = *(const float4 *) ((pro.b ? pro.b : pro.parts) + kc);
+    }
+    float e_bias = 0.0f, e_res = 0.0f;
+    {
+        const int64_t rc = live ? row : 0;
+        if (EPI >= 1) e_bias = e.bias[rc];
+        if (EPI == 2) e_res = *(const float *) (e.resid + rc * sizeof(float));
+    }
+    uint4 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int it = u < nit ? u : nit - 1;
+        const int64_t c = (int64_t) it * kLpr + m;
+        const uint4 v = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);
+        cur[u] = c < k8 && u < nit ? v : make_uint4(0u, 0u, 0u, 0u);
+    }
+
+#pragma unroll
+    for (int r = 0; r < QPT; r++) {
+        float4 sum = pp[r][0];
+#pragma unroll
+        for (int q = 1; q < NPM; q++) {
+            if (q < pro.nparts) {
+                sum.x += pp[r][q].x; sum.y += pp[r][q].y; sum.z += pp[r][q].z; sum.w += pp[r][q].w;
+            }
+        }
+        const int64_t q4 = ((int64_t) r * blockDim.x + threadIdx.x) * 4;
+        if (q4 < K) {
+            *(float4 *) (xf + q4) = sum;
+            if (blockIdx.x == 0) *(float4 *) (pro.store + q4) = sum;
+        }
+    }
+    __syncthreads();
+    float4 v[JM];
+#pragma unroll
+    for (int j = 0; j < JM; j++) {
+        const int64_t k = (int64_t) j * 256 + lane * 4;
+        v[j] = k < K ? *(const float4 *) (xf + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    uint16_t * xw = xs + (size_t) wid * kp;
+    norm_store<JM, true>(v, pg, pb, K, kp, pro, xw, lane);
+
+    float acc = 0.0f;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        if (u < nit) acc = dot8(cur[u], *(const uint4 *) (xw + ((int64_t) u * kLpr + m) * kChunk), acc);
+    acc = row16_sum(acc);
+    if (live && m == 0) {
+        float r = acc;
+        if (EPI >= 1) r = r + e_bias;
+        if (EPI == 2) r = r + e_res;
+        if (EPI == 3) r = r <= -10.0f ? 0.0f : (r >= 10.0f ? r : mi_h2f(e.gelu_table[mi_f2h(r)]));
+        dst[row] = r;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (e.copy[k].ptr && row >= e.copy[k].row0 && row < e.copy[k].row1)
+                *(float *) (e.copy[k].ptr + (row - e.copy[k].row0) * sizeof(float)) = r;
+        }
+    }
+}
+
 template <int NC, int U, bool ONE, int JM>
 void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols, float * dst,
                size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int ks, int rgs) {
@@ -425,6 +524,9 @@ bool mi_mul_mat_f16_fast_supported(int64_t K, int64_t ncols, const mi_src_cols &
     if (!xh && (x.nb1 % 16 != 0 || (uintptr_t) x.base % 16 != 0)) return false;
     // norm prologue: column in registers (K <= 3072), one register pass per wave (K <= 1024 or >= 3 waves)
     if (pro.mode && (K > 3072 || xh || ((uintptr_t) pro.g | (uintptr_t) pro.b) % 16 != 0)) return false;
+    // summed-partials prologue (k_gemv_f16_ps): one column, K <= 1024
+    if (pro.parts && (!pro.mode || ncols != 1 || K > 1024 || pro.nparts < 1 || pro.nparts > kPsMaxParts || !pro.store ||
+                      ((uintptr_t) pro.parts | (uintptr_t) pro.store) % 16 != 0 || K % 8 != 0)) return false;
     return true;
 }
 
@@ -449,7 +551,7 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
     ks = (nit + per - 1) / per;
     const bool one = per <= 8;
     const int rgs = g_mi_tuning.f16_rgs > 0 ? std::max(1, std::min(g_mi_tuning.f16_rgs, 8 / ks)) : 1;
-    if (ncols == 1 && groups >= 4096 && K <= 1024 && !xh && !e.resid && !e.copy[0].ptr && g_mi_tuning.f16_rgs == 0) {
+    if (ncols == 1 && groups >= 4096 && K <= 1024 && !xh && !e.resid && !e.copy[0].ptr && g_mi_tuning.f16_rgs == 0 && !pro.parts) {
         // tall matrix: grid-stride row groups (k_gemv_f16_tall)
         const dim3 grid((unsigned) std::min<int64_t>((groups + 3) / 4, 512));
         const size_t lds = (size_t) kp * sizeof(uint16_t);
@@ -464,7 +566,32 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
 #undef MI_GEMV_TALL
         return;
     }
-    if (pro.mode) {  // supported() guarantees one pass (K <= 3072)
+    if (pro.parts) {  // supported(): one column, K <= 1024, <= 16 parts
+        // waves per workgroup: enough workgroups to cover the CUs, few enough that the parts
+        // (nparts x 4 K bytes read per workgroup) stay a small fraction of the weight bytes
+        // (rw >= 2 and K <= 1024: at most 2 groups of 4 elements per thread)
+        const int rw = g_mi_tuning.f16_ps_waves > 0 ? g_mi_tuning.f16_ps_waves : 4;
+        const int qpt = (int) ((K / 4 + 64 * rw - 1) / (64 * rw));
+        const dim3 grid((unsigned) ((N + 4 * rw - 1) / (4 * rw)));
+        const size_t lds = (size_t) rw * kp * sizeof(uint16_t) + (size_t) kp * sizeof(float);
+        const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
+        const uint8_t * w = (const uint8_t *) W;
+#define MI_GEMV_PS(EP, NPM, QPT) hipLaunchKernelGGL((k_gemv_f16_ps<EP, 8, 4, NPM, QPT>), grid, dim3(64 * rw), lds, s, w, nb01, K, N, dst, e, pro, kp)
+#define MI_GEMV_PS_E(NPM, QPT)                     \
+        switch (epi) {                             \
+            case 0: MI_GEMV_PS(0, NPM, QPT); break; \
+            case 1: MI_GEMV_PS(1, NPM, QPT); break; \
+            case 2: MI_GEMV_PS(2, NPM, QPT); break; \
+            default: MI_GEMV_PS(3, NPM, QPT); break; \
+        }
+        if (qpt <= 1) {
+            if (pro.nparts <= 12) { MI_GEMV_PS_E(12, 1) } else { MI_GEMV_PS_E(16, 1) }
+        } else {
+            if (pro.nparts <= 12) { MI_GEMV_PS_E(12, 2) } else { MI_GEMV_PS_E(16, 2) }
+        }
+#undef MI_GEMV_PS_E
+#undef MI_GEMV_PS
+    } else if (pro.mode) {  // supported() guarantees one pass (K <= 3072)
         if (K <= 1024) launch_one<4>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
         else launch_one<12>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
     } else if (one) {

@@ -238,6 +238,8 @@ _SIGS = {
     "ggml_backend_mi355x_quantize_activations": ([c_void_p, c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p], c_bool),
     # GPT-2 driver (include/gpt2-mi355x.h)
     "gpt2_model_load": ([c_char_p, c_void_p, c_int, c_int], c_void_p),
+    "gpt2_model_load_ex": ([c_char_p, c_void_p, c_int, c_int, c_void_p], c_void_p),
+    "gpt2_logits_host": ([c_void_p], c_void_p),
     "gpt2_model_free": ([c_void_p], None),
     "gpt2_model_load_sched": ([c_char_p, c_void_p, c_int, c_int, c_int, c_int], c_void_p),
     "gpt2_model_load_sched_ex": ([c_char_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p], c_void_p),

@@ -192,20 +192,39 @@ def ensure_quantized_model(lib: G.Lib, qtype: str, path: str | None = None) -> s
 class Model:
     """One loaded GPT-2 on a backend (gpt2_model_load); eval() returns logits as numpy."""
 
-    def __init__(self, lib: G.Lib, path: str, backend, n_ctx: int = 0, n_batch: int = 8):
+    def __init__(self, lib: G.Lib, path: str, backend, n_ctx: int = 0, n_batch: int = 8, host_io: bool = True):
+        """host_io: on an MI355X backend, token ids / positions in pinned host memory read by the
+        device in place and the logits staged through it (gpt2_model_load_ex)."""
         if not lib.has("gpt2_model_load"):
             raise RuntimeError("this library set has no GPT-2 driver (lib/libgpt2_mi355x.so)")
         self.lib = lib
         self.backend = backend
-        self.m = lib.gpt2_model_load(path.encode(), backend, n_ctx, n_batch)
+        if host_io and lib.has("gpt2_model_load_ex") and lib.has("ggml_backend_is_mi355x") and lib.ggml_backend_is_mi355x(backend):
+            self.m = lib.gpt2_model_load_ex(path.encode(), backend, n_ctx, n_batch, lib.ggml_backend_mi355x_host_buffer_type())
+        else:
+            self.m = lib.gpt2_model_load(path.encode(), backend, n_ctx, n_batch)
         if not self.m:
             raise RuntimeError(f"gpt2_model_load({path}) failed")
         hp = gpt2_hparams_c()
         lib.gpt2_model_hparams(self.m, ctypes.byref(hp))
         self.hp = hp
         self.n_vocab = hp.n_vocab
+        # the host staging of the last token's logits (host_io), read in place by eval(copy=False)
+        self._staged = None
+        if lib.has("gpt2_logits_host"):
+            ptr = lib.gpt2_logits_host(self.m)
+            if ptr:
+                self._staged = np.ctypeslib.as_array((ctypes.c_float * hp.n_vocab).from_address(ptr)).reshape(1, hp.n_vocab)
+        self._tok = np.zeros(1, dtype=np.int32)
 
-    def eval(self, n_past: int, tokens, all_logits: bool = False) -> np.ndarray:
+    def eval(self, n_past: int, tokens, all_logits: bool = False, copy: bool = True) -> np.ndarray:
+        """copy=False (last token's logits, host_io models): a view of the host staging, valid
+        until the next eval."""
+        if not copy and not all_logits and self._staged is not None and len(tokens) == 1:
+            self._tok[0] = tokens[0]
+            if self.lib.gpt2_eval(self.m, n_past, self._tok.ctypes.data, 1, None, 0) != 0:
+                raise RuntimeError("gpt2_eval failed")
+            return self._staged
         tok = np.ascontiguousarray(np.asarray(tokens, dtype=np.int32))
         n = len(tok)
         out = np.empty((n if all_logits else 1, self.n_vocab), dtype=np.float32)

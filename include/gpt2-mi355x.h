@@ -28,6 +28,12 @@ struct gpt2_hparams_c {
 // and a graph allocator reserved for the worst-case graph of n_batch tokens (:832-846).
 // n_ctx <= 0 keeps the file's context. Returns NULL (with a message on stderr) on failure.
 GGML_API struct gpt2_model * gpt2_model_load(const char * fname, ggml_backend_t backend, int n_ctx, int n_batch);
+// The same, with host_buft (a host buffer type the backend's kernels can read, e.g.
+// ggml_backend_mi355x_host_buffer_type(); NULL = gpt2_model_load) holding the token ids and
+// positions, which the device then reads in place instead of receiving an upload per eval, and a
+// staging copy of the logits, copied into right behind the graph on the backend's queue.
+GGML_API struct gpt2_model * gpt2_model_load_ex(const char * fname, ggml_backend_t backend, int n_ctx, int n_batch,
+                                                ggml_backend_buffer_type_t host_buft);
 // examples/gpt-2/main-sched.cpp: layers split over `backends` (the last one is the CPU fallback,
 // as ggml_backend_sched requires) by n_gpu_layers, executed through ggml_backend_sched. Needs a
 // ggml runtime that provides the scheduler (the reference libggml: oracle/_ref/libgpt2_ref.so);
@@ -54,9 +60,12 @@ GGML_API size_t gpt2_compute_buffer_size(const struct gpt2_model * model);
 
 // gpt2_eval (main-backend.cpp:728): runs n_tokens tokens at positions n_past.. and writes the
 // logits of the last token (n_vocab floats), or of all tokens (n_tokens*n_vocab) if all_logits.
-// Returns 0 on success.
+// logits may be NULL for a model loaded with a host buffer type (gpt2_model_load_ex): the logits
+// are then only in gpt2_logits_host(), valid until the next eval. Returns 0 on success.
 GGML_API int gpt2_eval(struct gpt2_model * model, int n_past, const int32_t * tokens, int n_tokens, float * logits,
                        int all_logits);
+// the host staging of the logits (gpt2_model_load_ex with a host buffer type), or NULL
+GGML_API const float * gpt2_logits_host(const struct gpt2_model * model);
 
 // the vocabulary from the model file and the word-split + longest-match tokenizer of
 // examples/common.cpp:272-329. gpt2_tokenize returns the token count (may exceed max_tokens;

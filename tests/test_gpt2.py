@@ -249,20 +249,25 @@ def test_quantized_gpt2_logits_bit_identical_to_reference_cpu(quantized_paths, q
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("qtype", ["f16", "q4_k", "q8_0"])
-def test_gpt2_decode_launches_per_token(model_path, quantized_paths, qtype):
+@pytest.mark.parametrize("order", [0, 1])
+def test_gpt2_decode_launches_per_token(model_path, quantized_paths, qtype, order):
     """Node fusion keeps a decode token at 62 kernel launches for f16 and quantized models alike:
     per layer the norm chain rides in the GEMV prologue, bias / residual / GELU and the K/V-cache
     copies in its epilogue, the attention block is one kernel; the token + position embedding
-    (two GET_ROWS and their ADD) is one kernel."""
+    (two GET_ROWS and their ADD) is one kernel. The f16 model in the tree-order (default) mode
+    also runs each layer's attention with its output projection (k_attn_proj, partial sums added
+    by the next GEMV's norm prologue): 50."""
     lib = G.runtime()
     be = G.mi355x_backend(lib)
+    lib.ggml_backend_mi355x_set_tuning(b"mmv_order", order)
     m = gpt2.Model(lib, model_path if qtype == "f16" else quantized_paths[qtype], be, n_ctx=1024, n_batch=8)
     try:
         toks = m.tokenize(PROMPT)
         m.eval(0, toks[:8])
         m.eval(8, [toks[8]])
-        assert lib.ggml_backend_mi355x_last_launch_count(be) == 62
+        assert lib.ggml_backend_mi355x_last_launch_count(be) == (50 if qtype == "f16" and order == 0 else 62)
     finally:
+        lib.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
         m.free()
         lib.ggml_backend_free(be)
 
@@ -322,11 +327,18 @@ def test_gpt2_long_context_decode(model_path):
         a = ours.eval(512, toks[512:1000], all_logits=False)
         b = rm.eval(512, toks[512:1000], all_logits=False)
         e2 = _rel_err(a, b)
-        print(f"long context: rel logit error {e1:.2e} (512-token prompt), {e2:.2e} (488 more)")
+        # single-token decode at n_kv > 1000 (the fused attention + projection path, long KV)
+        e3 = []
+        for k in range(3):
+            nxt = [int(np.argmax(b[-1]))]
+            a = ours.eval(1000 + k, nxt)
+            b = rm.eval(1000 + k, nxt)
+            e3.append(_rel_err(a, b))
+        print(f"long context: rel logit error {e1:.2e} (512-token prompt), {e2:.2e} (488 more), decode {e3}")
         assert np.isfinite(a).all()
-        assert e1 <= LOGIT_TOL and e2 <= LOGIT_TOL
+        assert e1 <= LOGIT_TOL and e2 <= LOGIT_TOL and max(e3) <= LOGIT_TOL
         with pytest.raises(RuntimeError):
-            ours.eval(1000, toks[:100])  # past the 1024 positions of wpe
+            ours.eval(1003, toks[:100])  # past the 1024 positions of wpe
     finally:
         ours.free()
         rm.free()

@@ -8,7 +8,7 @@ n_decode = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 path = gpt2.ensure_model()
 lib = G.runtime()
 be = G.mi355x_backend(lib)
-m = gpt2.Model(lib, path, be, n_ctx=1024, n_batch=8)
+m = gpt2.Model(lib, path, be, n_ctx=1024, n_batch=8, host_io=os.environ.get("GPT2_HOST_IO", "1") == "1")
 toks = m.tokenize("Once upon a time the cat sat on the mat and the dog ran away")[:32]
 n_past = 0
 for i in range(0, len(toks), 8):
@@ -17,7 +17,7 @@ nxt = int(np.argmax(lg[-1]))
 st = {"us_build": 0, "us_alloc": 0, "us_inputs": 0, "us_compute": 0, "us_launch": 0, "us_prebuild": 0, "us_wait": 0, "us_readback": 0}
 t0 = time.perf_counter()
 for _ in range(n_decode):
-    lg = m.eval(n_past, [nxt]); n_past += 1
+    lg = m.eval(n_past, [nxt], copy=False); n_past += 1
     nxt = int(np.argmax(lg[-1]))
     s = m.stats()
     for k in st: st[k] += s.get(k, 0)

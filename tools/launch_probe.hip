@@ -25,6 +25,19 @@ __global__ void k_touch(const uint4 * __restrict__ w, float * __restrict__ y, in
     if (threadIdx.x == 0 && blockIdx.x == 0) y[gridDim.x] = (float) acc;
 }
 
+// the add with a large by-value argument block (as the backend's kernels take: tensor / epilogue
+// descriptors), to see what the argument size costs per launch
+struct big_args {
+    const float * x;
+    float * y;
+    int n;
+    char pad[240];
+};
+__global__ void k_add_big(big_args a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.n) a.y[i] = a.x[i] + 1.0f;
+}
+
 int main() {
     hipStream_t s;
     CK(hipStreamCreate(&s));
@@ -71,6 +84,13 @@ int main() {
     };
     if (run("add 768 floats, 1 WG x 256", [&](int k) { hipLaunchKernelGGL(k_add1, dim3(3), dim3(256), 0, s, (k & 1) ? b : a, (k & 1) ? a : b, 768); })) return 1;
     if (run("add 768 floats, 12 WG x 64", [&](int k) { hipLaunchKernelGGL(k_add1, dim3(12), dim3(64), 0, s, (k & 1) ? b : a, (k & 1) ? a : b, 768); })) return 1;
+    if (run("add 768 floats, 1 WG x 512", [&](int k) { hipLaunchKernelGGL(k_add1, dim3(2), dim3(512), 0, s, (k & 1) ? b : a, (k & 1) ? a : b, 768); })) return 1;
+    if (run("add 768 floats, 3 WG x 256, 256 B args", [&](int k) {
+            big_args ba{(k & 1) ? b : a, (k & 1) ? a : b, 768, {}};
+            hipLaunchKernelGGL(k_add_big, dim3(3), dim3(256), 0, s, ba); })) return 1;
+    if (run("add 768 floats, 3 WG x 256, 256 B args, 16 KB LDS", [&](int k) {
+            big_args ba{(k & 1) ? b : a, (k & 1) ? a : b, 768, {}};
+            hipLaunchKernelGGL(k_add_big, dim3(3), dim3(256), 16384, s, ba); })) return 1;
     // GEMV-shaped: 192 / 576 / 768 one-wave workgroups each reading 6 KB / 1.5 KB (1.2-4.7 MB, distinct per kernel)
     for (int wgs : {192, 576, 768}) {
         for (int kb : {1536, 6144}) {
