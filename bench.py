@@ -36,6 +36,7 @@ from ggml_mi355x import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense f16/bf16 MFMA
+I8_PEAK_TOPS = 2 * MFMA_PEAK_TFLOPS  # MI355X_MICROARCH.md, Matrix cores: I8 32x32x32 runs at 2x the BF16 rate per clock
 TYPE_NAMES = {"q4_K": 12, "q5_K": 13, "q4_0": 2, "q8_0": 8, "f16": 1}
 
 
@@ -565,10 +566,17 @@ def main():
                  "GB/s_effective": round(unit_bytes(12, 4096, 4096, bb) / (us / 1e6) / 1e9, 1),
                  "launches_per_mul_mat": lib.ggml_backend_mi355x_last_launch_count(backend) / 8}
             if bb == 512:
-                e["roofline"] = {"bound": "mfma", "achieved": round(flops / 8 / (us / 1e6) / 1e12, 2), "peak": MFMA_PEAK_TFLOPS,
-                                 "unit": "TFLOP/s", "frac": round(flops / 8 / (us / 1e6) / 1e12 / MFMA_PEAK_TFLOPS, 4),
-                                 "note": "2*N*K*B / HIP-event time of the whole mul_mat (activation quantizer + GEMM) vs the "
-                                         "dense f16 MFMA peak (the GEMM's operands are exact-integer f16)"}
+                peak = I8_PEAK_TOPS / 2  # Q4_K: two int8 weight planes per weight (mmq_exact.hip)
+                e["roofline"] = {"bound": "mfma", "achieved": round(flops / 8 / (us / 1e6) / 1e12, 2), "peak": peak,
+                                 "unit": "TFLOP/s", "frac": round(flops / 8 / (us / 1e6) / 1e12 / peak, 4),
+                                 "note": "useful 2*N*K*B / HIP-event time of the whole mul_mat (activation quantizer + GEMM) vs "
+                                         "the dense I8 MFMA peak (5 POP/s) / 2: the exact block sums run as two "
+                                         "v_mfma_i32_32x32x32_i8 per 32-deep K step (Q4_K weight planes q*(sc bit field))"}
+            elif bb == 64:
+                e["roofline"] = {"bound": "hbm", "achieved": e["GB/s_effective"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(e["GB/s_effective"] / HBM_PEAK_GBS, 4),
+                                 "note": "algorithmic bytes (weights + f32 activations + f32 outputs) / HIP-event time of the "
+                                         "whole mul_mat (activation quantizer + GEMM)"}
             sweep[f"q4_K_4096x4096_b{bb}_prefill"] = e
             w3.free()
         result["sweep"] = sweep
