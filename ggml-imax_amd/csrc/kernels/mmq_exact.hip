@@ -154,7 +154,7 @@ namespace {
 // one issues its MFMAs the other runs its dequantization / combine VALU.
 // Canonical combine order (shared by every kernel of this file): the superblock terms
 // (mmqx_term) left-folded in superblock order, y = term_0; y = y + term_1; ...
-template <int TYPE, bool XCD, int ABL = 0>
+template <int TYPE, bool XCD, int ABL = 0, int LEAD = 4, int SCT = 0>
 __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                               mi_act_mmx act, float * __restrict__ dst, size_t ycol) {
     using F = XFmt<TYPE>;
@@ -184,6 +184,24 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
         b0 = (t / nrt) * XBN;
     }
     const int S = (int) (K / 256);
+    // timing diagnostics (ABL & 8; results invalid): s_memtime of wave 0 of workgroups 0 and 97 into
+    // dst as uint64 [2][80]: 0 start, 1 after the prologue, 2 + 4 sb + {0 stage start, 1 after the
+    // MFMA steps, 2 after the combine, 3 after the barrier}
+    auto stamp = [&](int slot) {
+        if constexpr ((ABL & 8) != 0) {
+            const int wsel = blockIdx.x == 0 ? 0 : blockIdx.x == 97 ? 1 : -1;
+            if (wsel >= 0 && (threadIdx.x >> 6) == 0 && (threadIdx.x & 63) == 0 && slot < 80)
+                ((uint64_t *) dst)[wsel * 80 + slot] = __builtin_amdgcn_s_memtime();
+        }
+    };
+    // and every workgroup's start / end on the constant 100 MHz clock: uint64 [gridDim][2] at 160
+    auto rstamp = [&](int e) {
+        if constexpr ((ABL & 8) != 0) {
+            if (threadIdx.x == 0) ((uint64_t *) dst)[160 + 2 * blockIdx.x + e] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
+    rstamp(0);
+    stamp(0);
 
     // All global loads go through buffer descriptors with 32-bit per-lane offsets (the host
     // checks the sizes): one address register per load instead of a 64-bit pointer.
@@ -246,51 +264,79 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
     auto kmin = [](const KSel & k, uint32_t w1, uint32_t w2) {
         return __builtin_amdgcn_ubfe(k.hi ? w2 : w1, k.hi ? k.sh + 4 : k.sh, k.w) | (__builtin_amdgcn_ubfe(w1, k.shh, k.wh) << 4);
     };
-    auto store_stage = [&](int buf, const Raw & raw) {
-        if constexpr ((ABL & 1) != 0) return;  // timing ablation: no dequantization
-        char * base = lds + buf * kBuf;
-        const uint32_t sc0 = kscale(k0, raw.hdr.y, raw.hdr.w), sc1 = kscale(k1, raw.hdr.y, raw.hdr.w);
+    // dequantization of one thread's share of a superblock into LDS buffer `buf`, in pieces that
+    // the stage loop interleaves with its MFMAs: unpack (dq_prep), plane p half hh (dq_piece, k =
+    // 2 p + hh), the combine's row operands (dq_rows)
+    struct Dq {
+        uint32_t lo[4], hi[4], sc0, sc1;
+    };
+    auto dq_prep = [&](Dq & dq, const Raw & raw) {
+        dq.sc0 = kscale(k0, raw.hdr.y, raw.hdr.w);
+        dq.sc1 = kscale(k1, raw.hdr.y, raw.hdr.w);
         const uint32_t q[4] = {raw.qs.x, raw.qs.y, raw.qs.z, raw.qs.w};
         const uint32_t qh[4] = {raw.qh.x, raw.qh.y, raw.qh.z, raw.qh.w};
-        uint32_t lo[4], hi[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            lo[i] = q[i] & 0x0F0F0F0Fu;
-            hi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
+            dq.lo[i] = q[i] & 0x0F0F0F0Fu;
+            dq.hi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
             if constexpr (F::Q5) {
-                lo[i] |= ((qh[i] >> j0) & 0x01010101u) << 4;
-                hi[i] |= ((qh[i] >> (j0 + 1)) & 0x01010101u) << 4;
+                dq.lo[i] |= ((qh[i] >> j0) & 0x01010101u) << 4;
+                dq.hi[i] |= ((qh[i] >> (j0 + 1)) & 0x01010101u) << 4;
             }
         }
-        char * pl0 = base + ar * XR + 32 * j0 + 16 * hf;
-#pragma unroll
-        for (int p = 0; p < NP; p++) {
-            const uint32_t f0 = F::factor((int) sc0, p), f1 = F::factor((int) sc1, p);
-            *(uint4 *) (pl0 + p * kPlane) = make_uint4(mulb(lo[0], f0), mulb(lo[1], f0), mulb(lo[2], f0), mulb(lo[3], f0));
-            *(uint4 *) (pl0 + p * kPlane + 32) = make_uint4(mulb(hi[0], f1), mulb(hi[1], f1), mulb(hi[2], f1), mulb(hi[3], f1));
+    };
+    auto dq_piece = [&](int buf, const Dq & dq, int k) {
+        if constexpr ((ABL & 1) != 0) return;  // timing ablation: no dequantization
+        char * pl0 = lds + buf * kBuf + ar * XR + 32 * j0 + 16 * hf;
+        const int p = k >> 1;
+        if ((k & 1) == 0) {
+            const uint32_t f0 = F::factor((int) dq.sc0, p);
+            *(uint4 *) (pl0 + p * kPlane) = make_uint4(mulb(dq.lo[0], f0), mulb(dq.lo[1], f0), mulb(dq.lo[2], f0), mulb(dq.lo[3], f0));
+        } else {
+            const uint32_t f1 = F::factor((int) dq.sc1, p);
+            *(uint4 *) (pl0 + p * kPlane + 32) = make_uint4(mulb(dq.hi[0], f1), mulb(dq.hi[1], f1), mulb(dq.hi[2], f1), mulb(dq.hi[3], f1));
         }
+    };
+    auto dq_rows = [&](int buf, const Raw & raw) {
+        if constexpr ((ABL & 1) != 0) return;
         // row operands: U halves [m_c, 64 m_c] at slot c; d_w (c = 0), dmin_w (c = 1)
-        char * ro = base + NP * kPlane;
+        char * ro = lds + buf * kBuf + NP * kPlane;
         const uint32_t mc = kmin(kc, raw.hdr.z, raw.hdr.w);
         *(uint32_t *) (ro + ar * 32 + 4 * c8) = (uint32_t) mi_f2h((float) mc) | ((uint32_t) mi_f2h((float) (64 * mc)) << 16);
         if (c8 < 2) ((float *) (ro + XBM * 32))[c8 * XBM + ar] = mi_h2f((uint16_t) (c8 == 0 ? (raw.hdr.x & 0xFFFF) : (raw.hdr.x >> 16)));
     };
+    auto store_stage = [&](int buf, const Raw & raw) {
+        Dq dq;
+        dq_prep(dq, raw);
+#pragma unroll
+        for (int k = 0; k < 2 * NP; k++) dq_piece(buf, dq, k);
+        dq_rows(buf, raw);
+    };
 
     f32x16 y = {};
-    // one stage of lead for everything: the raw weights of superblock sb + 1 are staged at the end
-    // of stage sb and then reloaded with sb + 2; the activation fragment of step kk of sb + 1 is
-    // loaded into the register that step kk of sb has just consumed
-    Raw raw;
+    // The raw weights of superblock sb + 1 are dequantized into LDS at the end of stage sb; they
+    // were requested LEAD stages earlier (a ring of LEAD raw slots: HBM latency is several stage
+    // times). The activation fragment of step kk of sb + 1 is loaded into the register that step kk
+    // of sb has just consumed (L2-resident: one stage of lead is enough).
+    Raw raw[LEAD];
     Xs xs;
-    load_raw(raw, 0);
-    store_stage(0, raw);
+    {
+        Raw r0;
+        load_raw(r0, 0);
+        store_stage(0, r0);
+    }
     load_x(xs, 0);
-    load_raw(raw, 1);
+#pragma unroll
+    for (int u = 0; u < LEAD; u++) load_raw(raw[u], 1 + u);
     mi_lds_barrier();
+    stamp(1);
 
-    // one stage = superblock sb; LDS buffer sb & 1 (one loop body: the activation registers are
-    // loop-carried, so each fragment of the next superblock lands in the register just consumed)
-    for (int sb = 0; sb < S; sb++) {
+    // one stage = superblock sb; LDS buffer sb & 1. Unrolled by LEAD so every ring slot index is
+    // static (slot u = sb % LEAD holds superblock sb + 1); fully unrolled when S is a template
+    // constant (SCT), so no loop back-edge makes the compiler drain the ring.
+    const int S_ = SCT > 0 ? SCT : S;
+    auto stage = [&](const int sb, Raw & rslot) {
+        stamp(2 + 4 * sb);
         const int cur = sb & 1;
         const char * base = lds + cur * kBuf;
         const char * arow_p = base + (32 * rw + r) * XR + 16 * h;
@@ -305,6 +351,10 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
             an[0][p] = *(const i32x4 *) (arow_p + p * kPlane);
             an[1][p] = *(const i32x4 *) (arow_p + p * kPlane + 32);
         }
+        // the dequantization of superblock sb + 1 (raw loaded LEAD stages ago) into the other LDS
+        // buffer, one piece per 32-deep step, between this stage's MFMAs (the other buffer's
+        // readers finished at the previous stage's barrier); then the slot's next load
+        Dq dq;
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) {
             i32x4 a[NP];
@@ -324,53 +374,75 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
             }
             // step kk of the next superblock into the register just consumed
             xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kbn + (kk >> 1)) * xstep + 32 * (kk & 1), 0, 0));
+            if (kk == 0) dq_prep(dq, rslot);
+            if (kk >= 1 && kk <= 2 * NP) dq_piece(cur ^ 1, dq, kk - 1);
+            if (kk == 7) {
+                dq_rows(cur ^ 1, rslot);
+                load_raw(rslot, sb + 1 + LEAD);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
-        // nothing below may be hoisted above this stage's MFMAs: in particular not the unpacking of
-        // the next superblock's weights, whose loads must keep their stage of lead (vmcnt is
-        // in-order, so an early use would wait for every load issued before it)
-        __builtin_amdgcn_sched_barrier(0);
+        stamp(3 + 4 * sb);
         // U on the f16 MFMA, then the canonical combine
         if constexpr ((ABL & 2) != 0) {  // timing ablation: no combine
 #pragma unroll
             for (int i = 0; i < 16; i++) y[i] += (float) acc[0][i];
         } else {
-        const char * ro = base + NP * kPlane;
-        const float * dwv = (const float *) (ro + XBM * 32);
-        const half8 au = *(const half8 *) (ro + (32 * rw + r) * 32 + 16 * h);
-        const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(au, xs.bu, f32x16{}, 0, 0, 0);
-        const float da = xs.da;
-        {
-            const uint32_t sc = (uint32_t) nx * (uint32_t) ncols + bcol;
-            xs.bu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, sc * 32 + 16 * h, 0, 0));
-            xs.da = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, sc * 4, 0, 0));
-        }
+            const char * ro = base + NP * kPlane;
+            const float * dwv = (const float *) (ro + XBM * 32);
+            const half8 au = *(const half8 *) (ro + (32 * rw + r) * 32 + 16 * h);
+            const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(au, xs.bu, f32x16{}, 0, 0, 0);
+            const float da = xs.da;
+            {
+                const uint32_t sc = (uint32_t) nx * (uint32_t) ncols + bcol;
+                xs.bu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, sc * 32 + 16 * h, 0, 0));
+                xs.da = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, sc * 4, 0, 0));
+            }
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const float4 dw4 = *(const float4 *) (dwv + 32 * rw + 8 * g + 4 * h);
-            const float4 dm4 = *(const float4 *) (dwv + XBM + 32 * rw + 8 * g + 4 * h);
-            const float dw[4] = {dw4.x, dw4.y, dw4.z, dw4.w};
-            const float dm[4] = {dm4.x, dm4.y, dm4.z, dm4.w};
+            for (int g = 0; g < 4; g++) {
+                const float4 dw4 = *(const float4 *) (dwv + 32 * rw + 8 * g + 4 * h);
+                const float4 dm4 = *(const float4 *) (dwv + XBM + 32 * rw + 8 * g + 4 * h);
+                const float dw[4] = {dw4.x, dw4.y, dw4.z, dw4.w};
+                const float dm[4] = {dm4.x, dm4.y, dm4.z, dm4.w};
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int i = 4 * g + e;
-                int T = acc[NP - 1][i];
+                for (int e = 0; e < 4; e++) {
+                    const int i = 4 * g + e;
+                    int T = acc[NP - 1][i];
 #pragma unroll
-                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][i];
-                const float term = mmqx_term(T, Uv[i], dw[e], dm[e], da);
-                y[i] = sb == 0 ? term : y[i] + term;
+                    for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][i];
+                    const float term = mmqx_term(T, Uv[i], dw[e], dm[e], da);
+                    y[i] = sb == 0 ? term : y[i] + term;
+                }
             }
         }
-        }
-        // superblock sb + 1 into the other buffer, then the weights of sb + 2
-        __builtin_amdgcn_sched_barrier(0);
-        store_stage(cur ^ 1, raw);
-        load_raw(raw, sb + 2);
+        stamp(4 + 4 * sb);
         mi_lds_barrier();
+        stamp(5 + 4 * sb);
+    };
+    if constexpr (SCT > 0) {
+#pragma unroll
+        for (int sb = 0; sb < SCT; sb++) stage(sb, raw[sb % LEAD]);
+    } else {
+        for (int sb0 = 0; sb0 < S_; sb0 += LEAD) {
+#pragma unroll
+            for (int u = 0; u < LEAD; u++) {
+                if (sb0 + u < S_) stage(sb0 + u, raw[u]);
+            }
+        }
     }
 
     // D[n][b]: column b = lane & 31 of this wave's 32, rows n = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
     const int64_t b = b0 + 32 * cw + r;
+    rstamp(1);
+    if constexpr ((ABL & 8) != 0) {
+        // dst holds the stamps; keep the results alive (an unlikely-value store) so nothing is
+        // eliminated
+        float t = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; i++) t += y[i];
+        if (t == 1.2345e-30f) dst[4096 + threadIdx.x] = t;
+        return;
+    }
     if (b >= ncols) return;
     float * out = (float *) ((char *) dst + b * ycol);
 #pragma unroll
@@ -586,6 +658,18 @@ void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N
     }
     const int64_t nrt = (N + XBM - 1) / XBM, nct = (act.ncols + XBN - 1) / XBN;
     const dim3 grid((unsigned) (nrt * nct));
-    if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);
-    else hipLaunchKernelGGL((k_mmqx<13, false>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);
+    // weight ring depth LEAD (variant bits: 32 -> 2, 64 -> 1; default 4). (Fully unrolling the
+    // stage loop for K = 4096, SCT = 16, spills: the compiler hoists loads across stages.)
+#define MI_MMQX_T(TY, LD) hipLaunchKernelGGL((k_mmqx<TY, false, 0, LD, 0>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol)
+    const int lead = (var & 64) ? 1 : (var & 32) ? 2 : 4;
+    if (var & 1024) {  // timing stamps (results invalid)
+        if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false, 8, 4, 0>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);
+        return;
+    }
+    if (type == 12) {
+        if (lead == 1) MI_MMQX_T(12, 1); else if (lead == 2) MI_MMQX_T(12, 2); else MI_MMQX_T(12, 4);
+    } else {
+        if (lead == 1) MI_MMQX_T(13, 1); else if (lead == 2) MI_MMQX_T(13, 2); else MI_MMQX_T(13, 4);
+    }
+#undef MI_MMQX_T
 }
