@@ -10,7 +10,7 @@ from ggml_mi355x import ggml as G  # noqa: E402
 
 lib = G.runtime()
 be = G.mi355x_backend(lib, 0)
-lib.ggml_backend_mi355x_set_tuning(b"mmq_variant", 1024)
+lib.ggml_backend_mi355x_set_tuning(b"mmq_variant", 1024 | int(os.environ.get("STAMP_VARIANT", "0")))
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 wl = bench.MulMatWorkload(lib, be, 12, 4096, 4096, B, 1)
 for _ in range(20):
