@@ -432,6 +432,13 @@ struct mi_backend_ctx {
     std::vector<hipGraphExec_t> exec_pool;  // executable graphs of freed plans, for in-place update
     int graph_fail_streak = 0;         // consecutive re-instantiations (update refused)
     int64_t graph_stats[4] = {};       // captures, instantiations, updates, direct computes
+    // host-built RoPE {cos, sin} tables (rope_table_ensure), one per parameter set
+    struct rope_table {
+        int n_dims, ne0, mode, P;
+        float freq_base, freq_scale, ext_factor, attn_factor, corr0, corr1;
+        float * dev;
+    };
+    std::vector<rope_table> rope_tables;
     // a node value still held as partial sums (try_fuse_attn_proj): `out` = sum_h parts[h], to be
     // stored by its consumer's kernel (the next GEMV's norm prologue) or by mi_sum_parts
     struct {
@@ -929,6 +936,86 @@ static void rope_corr_dims(int n_dims, int n_orig_ctx, float freq_base, float be
     dims[1] = std::min((float) (n_dims - 1), end);
 }
 
+// ---- RoPE {cos, sin} tables, built on the host exactly as the reference CPU computes them ----
+// ggml_rope_cache_init / the NeoX loop of ggml_compute_forward_rope_f32 (src/ggml.c:13719-13948)
+// and rope_yarn (:13680-13700) over positions 0 .. P-1, with the host libm's sincosf (the function
+// the reference build calls) and the contractions its -mfma build makes (read off the object:
+// theta = fma(theta_interp, 1 - ramp_mix, theta_extrap * ramp_mix); mscale *= fma(logf(1 /
+// freq_scale), 0.1f, 1.0f)). Device positions outside [0, P) fall back to the kernel's own math.
+#pragma clang fp contract(off)
+static void rope_yarn_host(float theta_extrap, float freq_scale, const float corr[2], int64_t i0, float ext_factor, float mscale,
+                           float * c, float * s) {
+    const float theta_interp = freq_scale * theta_extrap;
+    float theta = theta_interp;
+    if (ext_factor != 0.0f) {
+        const float y = ((float) (i0 / 2) - corr[0]) / std::max(0.001f, corr[1] - corr[0]);
+        const float ramp_mix = (1.0f - std::min(1.0f, std::max(0.0f, y))) * ext_factor;
+        theta = std::fma(theta_interp, 1.0f - ramp_mix, theta_extrap * ramp_mix);
+        mscale *= std::fma(logf(1.0f / freq_scale), 0.1f, 1.0f);
+    }
+    float sv, cv;
+    sincosf(theta, &sv, &cv);
+    *c = cv * mscale;
+    *s = sv * mscale;
+}
+
+static const mi_backend_ctx::rope_table * rope_table_find(mi_backend_ctx * ctx, int n_dims, int ne0, int mode, float fb, float fs,
+                                                          float ef, float af, const float corr[2]) {
+    for (const auto & t : ctx->rope_tables) {
+        if (t.n_dims == n_dims && t.ne0 == ne0 && t.mode == mode && t.freq_base == fb && t.freq_scale == fs && t.ext_factor == ef &&
+            t.attn_factor == af && t.corr0 == corr[0] && t.corr1 == corr[1]) return &t;
+    }
+    return nullptr;
+}
+
+// builds the table of a ROPE node if missing (synchronous upload: never while capturing)
+static void rope_table_ensure(mi_backend_ctx * ctx, const ggml_tensor * node) {
+    const int32_t * pp = (const int32_t *) node->op_params;
+    const int n_dims = pp[1], mode = pp[2], n_ctx = pp[3], n_orig_ctx = pp[4];
+    const float fb = op_param_f(node, 5), fs = op_param_f(node, 6), ef = op_param_f(node, 7), af = op_param_f(node, 8);
+    float corr[2];
+    rope_corr_dims(n_dims, n_orig_ctx, fb, op_param_f(node, 9), op_param_f(node, 10), corr);
+    const int ne0 = (int) node->src[0]->ne[0];
+    if ((mode != 0 && mode != 2) || n_dims <= 0 || n_dims % 2 || rope_table_find(ctx, n_dims, ne0, mode, fb, fs, ef, af, corr)) return;
+    const int P = std::min(std::max({n_ctx, n_orig_ctx, 4096}), 1 << 16);
+    const int pairs = mode == 0 ? ne0 / 2 : n_dims / 2;
+    std::vector<float> h((size_t) P * pairs * 2);
+    const float theta_scale = powf(fb, -2.0f / n_dims);
+    const float inv_ndims = -1.f / n_dims;
+    for (int p = 0; p < P; p++) {
+        float * row = h.data() + (size_t) p * pairs * 2;
+        if (mode == 0) {
+            float theta = (float) p;
+            for (int k = 0; k < pairs; k++) {
+                rope_yarn_host(theta, fs, corr, 2 * k, ef, af, &row[2 * k], &row[2 * k + 1]);
+                theta *= theta_scale;
+            }
+        } else {
+            float theta = (float) p;
+            theta *= fs;
+            for (int k = 0; k < pairs; k++) {
+                const float cur_rot = inv_ndims * (float) (2 * k) - 0.0f;
+                rope_yarn_host(theta, fs, corr, (int64_t) cur_rot, ef, af, &row[2 * k], &row[2 * k + 1]);
+                theta *= theta_scale;
+            }
+        }
+    }
+    mi_backend_ctx::rope_table t{n_dims, ne0, mode, P, fb, fs, ef, af, corr[0], corr[1], nullptr};
+    mi_device_guard g(ctx->device);
+    MI_CHECK(hipMalloc(&t.dev, h.size() * sizeof(float)));
+    MI_CHECK(hipMemcpy(t.dev, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    ctx->rope_tables.push_back(t);
+}
+#pragma clang fp contract(on)
+
+// builds the RoPE tables a graph needs (before any capture: the uploads are synchronous)
+static void rope_tables_prepare(mi_backend_ctx * ctx, const ggml_cgraph * cgraph) {
+    for (int i = 0; i < cgraph->n_nodes; i++) {
+        const ggml_tensor * n = cgraph->nodes[i];
+        if (n->op == GGML_OP_ROPE && n->src[0] && n->src[0]->type == GGML_TYPE_F32) rope_table_ensure(ctx, n);
+    }
+}
+
 static void op_companion(mi_backend_ctx * ctx, ggml_tensor * node) {
     const ggml_tensor * a = node->src[0];
     const ggml_tensor * b = node->src[1];
@@ -970,8 +1057,9 @@ static void op_companion(mi_backend_ctx * ctx, ggml_tensor * node) {
             MI_ASSERT(n_dims <= a->ne[0] && n_dims % 2 == 0);
             float corr[2];
             rope_corr_dims(n_dims, n_orig_ctx, freq_base, beta_fast, beta_slow, corr);
+            const auto * tab = rope_table_find(ctx, n_dims, (int) a->ne[0], mode, freq_base, freq_scale, ext_factor, attn_factor, corr);
             mi_op_rope(desc(node), desc(a), (const int32_t *) b->data, n_dims, mode, freq_base, freq_scale, ext_factor,
-                       attn_factor, corr[0], corr[1], st);
+                       attn_factor, corr[0], corr[1], tab ? tab->dev : nullptr, tab ? tab->P : 0, st);
             break;
         }
         default:
@@ -1738,6 +1826,7 @@ static ggml_backend_graph_plan_t mi_graph_plan_create(ggml_backend_t backend, co
     // pass below then only enqueues kernels on ctx->stream. Scratch: the pass's own estimate plus
     // room for the attention planner's Q copies (at most every CONT node's bytes)
     op_tables(ctx);
+    rope_tables_prepare(ctx, cgraph);
     size_t cont_bytes = 0;
     for (int i = 0; i < cgraph->n_nodes; i++) {
         if (cgraph->nodes[i]->op == GGML_OP_CONT) cont_bytes += (ggml_nbytes(cgraph->nodes[i]) + kBufferAlign - 1) & ~(kBufferAlign - 1);
@@ -1804,6 +1893,11 @@ static enum ggml_status mi_graph_plan_compute(ggml_backend_t backend, ggml_backe
 }
 
 static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
+    {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        MI_CHECK(hipStreamIsCapturing(ctx->stream, &cs));
+        if (cs == hipStreamCaptureStatusNone) rope_tables_prepare(ctx, cgraph);
+    }
     scratch_reserve(ctx, graph_scratch_bytes(cgraph));
     ctx->scratch_used = 0;
     ctx->act_cache.clear();
@@ -1934,6 +2028,7 @@ static void mi_backend_free(ggml_backend_t backend) {
         for (hipGraphExec_t ex : ctx->exec_pool) MI_CHECK(hipGraphExecDestroy(ex));
         if (ctx->scratch) MI_CHECK(hipFree(ctx->scratch));
         if (ctx->tables) MI_CHECK(hipFree(ctx->tables));
+        for (auto & t : ctx->rope_tables) MI_CHECK(hipFree(t.dev));
         MI_CHECK(hipStreamDestroy(ctx->stream));
     }
     delete ctx;

@@ -176,9 +176,11 @@ void mi_op_diag_mask(const mi_tensor_desc & d, const mi_tensor_desc & a, int n_p
 // norm / rms_norm; g, b (optional, 1-D over ne0): the graph's following mul(., g) and add(., b)
 void mi_op_norm(const mi_tensor_desc & d, const mi_tensor_desc & a, float eps, bool rms, const float * g, const float * b,
                 hipStream_t s);
-// rope f32 forward, modes 0/2; corr = ggml_rope_yarn_corr_dims() computed on the host
+// rope f32 forward, modes 0/2; corr = ggml_rope_yarn_corr_dims() computed on the host; tab: the
+// backend's host-built {cos, sin} table [tab_p][pairs] for positions < tab_p (or null)
 void mi_op_rope(const mi_tensor_desc & d, const mi_tensor_desc & a, const int32_t * pos, int n_dims, int mode, float freq_base,
-                float freq_scale, float ext_factor, float attn_factor, float corr0, float corr1, hipStream_t s);
+                float freq_scale, float ext_factor, float attn_factor, float corr0, float corr1, const float * tab, int tab_p,
+                hipStream_t s);
 // soft_max (max_bias 0); n_past >= 0 fuses the preceding scale(pre_scale) + diag_mask_inf(n_past)
 void mi_op_soft_max(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & mask, float scale,
                     const uint16_t * exp_table, float pre_scale, int n_past, hipStream_t s);

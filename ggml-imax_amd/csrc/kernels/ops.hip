@@ -329,12 +329,18 @@ __global__ __launch_bounds__(256) void k_soft_max(mi_tensor_desc d, mi_tensor_de
 }
 
 // rope f32 (src/ggml.c:13719-13948), modes 0 (adjacent pairs) and 2 (neox halves), forward.
-// One thread per rotated pair. theta follows the reference's running product theta *= theta_scale
-// (so each thread replays k multiplications), and cos/sin are rounded from double so they match a
-// correctly rounded libm.
+// One thread per rotated pair. cos/sin come from the backend's host-built table (tab: the
+// reference's own running product theta *= theta_scale and the host libm's sincosf, so bit for bit
+// the reference CPU's values) for positions 0 <= p < tab_p; otherwise theta follows the same
+// running product on the device (each thread replays k multiplications) and cos/sin are rounded
+// from double (a correctly rounded libm: within an ulp of the host's). The pair is combined with
+// the fmas the reference's -mfma build emits (checked against its outputs): mode 0 fma(x0, cos,
+// -(x1 sin)) / fma(x1, cos, x0 sin), NeoX fma(x0, cos, -(x1 sin)) / fma(x0, sin, x1 cos).
 struct mi_rope_params {
     int n_dims, mode;
     float freq_scale, ext_factor, attn_factor, theta_scale, inv_ndims, corr0, corr1;
+    const float2 * tab;  // [tab_p][pairs] {cos, sin}, or null
+    int tab_p;
 };
 
 __device__ __forceinline__ void rope_yarn_dev(float theta_extrap, const mi_rope_params & r, int64_t i0, float & c, float & s) {
@@ -365,29 +371,43 @@ __global__ __launch_bounds__(256) void k_rope(mi_tensor_desc d, mi_tensor_desc a
         const float p = (float) pos[i2];
         const char * src = a.data + off4(a.nb, 0, i1, i2, i3);
         char * dst = d.data + off4(d.nb, 0, i1, i2, i3);
+        const int32_t pi = pos[i2];
+        const bool tabbed = r.tab && pi >= 0 && pi < r.tab_p;
         if (r.mode == 0) {
-            float theta = p;
-            for (int64_t j = 0; j < k; j++) theta = mul_rn(theta, r.theta_scale);
             float c, s;
-            rope_yarn_dev(theta, r, 2 * k, c, s);
+            if (tabbed) {
+                const float2 cs = r.tab[(int64_t) pi * pairs + k];
+                c = cs.x;
+                s = cs.y;
+            } else {
+                float theta = p;
+                for (int64_t j = 0; j < k; j++) theta = mul_rn(theta, r.theta_scale);
+                rope_yarn_dev(theta, r, 2 * k, c, s);
+            }
             const float x0 = *(const float *) (src + 2 * k * a.nb[0]);
             const float x1 = *(const float *) (src + (2 * k + 1) * a.nb[0]);
-            *(float *) (dst + 2 * k * d.nb[0]) = sub_rn(mul_rn(x0, c), mul_rn(x1, s));
-            *(float *) (dst + (2 * k + 1) * d.nb[0]) = add_rn(mul_rn(x0, s), mul_rn(x1, c));
+            *(float *) (dst + 2 * k * d.nb[0]) = __builtin_fmaf(x0, c, -mul_rn(x1, s));
+            *(float *) (dst + (2 * k + 1) * d.nb[0]) = __builtin_fmaf(x1, c, mul_rn(x0, s));
         } else {
             const int64_t ic = 2 * k;
             if (ic < r.n_dims) {
-                float theta = mul_rn(p, r.freq_scale);
-                for (int64_t j = 0; j < k; j++) theta = mul_rn(theta, r.theta_scale);
-                const float cur_rot = mul_rn(r.inv_ndims, (float) ic);
                 float c, s;
-                rope_yarn_dev(theta, r, (int64_t) cur_rot, c, s);
+                if (tabbed) {
+                    const float2 cs = r.tab[(int64_t) pi * (r.n_dims / 2) + k];
+                    c = cs.x;
+                    s = cs.y;
+                } else {
+                    float theta = mul_rn(p, r.freq_scale);
+                    for (int64_t j = 0; j < k; j++) theta = mul_rn(theta, r.theta_scale);
+                    const float cur_rot = mul_rn(r.inv_ndims, (float) ic);
+                    rope_yarn_dev(theta, r, (int64_t) cur_rot, c, s);
+                }
                 const int64_t i0 = ic / 2;
                 const int64_t h = r.n_dims / 2;
                 const float x0 = *(const float *) (src + i0 * a.nb[0]);
                 const float x1 = *(const float *) (src + (i0 + h) * a.nb[0]);
-                *(float *) (dst + i0 * d.nb[0]) = sub_rn(mul_rn(x0, c), mul_rn(x1, s));
-                *(float *) (dst + (i0 + h) * d.nb[0]) = add_rn(mul_rn(x0, s), mul_rn(x1, c));
+                *(float *) (dst + i0 * d.nb[0]) = __builtin_fmaf(x0, c, -mul_rn(x1, s));
+                *(float *) (dst + (i0 + h) * d.nb[0]) = __builtin_fmaf(x0, s, mul_rn(x1, c));
             } else {
                 *(float *) (dst + ic * d.nb[0]) = *(const float *) (src + ic * a.nb[0]);
                 *(float *) (dst + (ic + 1) * d.nb[0]) = *(const float *) (src + (ic + 1) * a.nb[0]);
@@ -473,8 +493,11 @@ void mi_op_soft_max(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi
 }
 
 void mi_op_rope(const mi_tensor_desc & d, const mi_tensor_desc & a, const int32_t * pos, int n_dims, int mode, float freq_base,
-                float freq_scale, float ext_factor, float attn_factor, float corr0, float corr1, hipStream_t s) {
+                float freq_scale, float ext_factor, float attn_factor, float corr0, float corr1, const float * tab, int tab_p,
+                hipStream_t s) {
     mi_rope_params r;
+    r.tab = (const float2 *) tab;
+    r.tab_p = tab ? tab_p : 0;
     r.n_dims = n_dims;
     r.mode = mode;
     r.freq_scale = freq_scale;
