@@ -337,3 +337,90 @@ def test_rope_exact(libs, mode):
           f"{float(np.max(np.abs(a[-1] - b[-1]))):.2e}")
     assert_exact(a[:-1], b[:-1], f"rope mode {mode}")
     assert np.max(np.abs(a[-1] - b[-1])) <= 1e-5 * max(1.0, float(np.max(np.abs(b[-1]))))
+
+
+def graph_outputs(lib, backend, build, n_tensors=128):
+    """Builds (feeds, outs, extra) in one context, computes once, returns every output's values and
+    the backend's launch count."""
+    overhead = lib.ggml_tensor_overhead() * n_tensors + lib.ggml_graph_overhead()
+    with G.Context(lib, overhead, no_alloc=True) as c:
+        feeds, outs, extra = build(c.ctx)
+        g = lib.ggml_new_graph(c.ctx)
+        for e in extra:
+            lib.ggml_build_forward_expand(g, e)
+        for o in outs:
+            lib.ggml_build_forward_expand(g, o)
+        buf = lib.ggml_backend_alloc_ctx_tensors(c.ctx, backend)
+        try:
+            for t, arr in feeds:
+                G.tensor_set(lib, t, arr)
+            assert lib.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
+            n = lib.ggml_backend_mi355x_last_launch_count(backend) if hasattr(lib, "ggml_backend_mi355x_last_launch_count") else 0
+            return [G.tensor_get(lib, o) for o in outs], n
+        finally:
+            lib.ggml_backend_buffer_free(buf)
+
+
+@pytest.mark.parametrize("consumer", ["ln_fc", "add"])
+@pytest.mark.parametrize("n_past", [7, 300])
+def test_attention_projection_fused(libs, consumer, n_past):
+    """Decode-token attention block + c_proj (F16) + bias + residual (main-backend.cpp:532-620):
+    in tree order one k_attn_proj launch leaves the projection as per-head partial sums; with an
+    LN -> F16 GEMV consumer (ln_2 -> c_fc + bias + GELU) the GEMV's prologue adds them and stores
+    the residual stream (k_gemv_f16_ps), with any other consumer mi_sum_parts stores it first.
+    Both the residual stream and the consumer's output are checked against the reference CPU (tree
+    order: within 5e-5 / 2e-4 of max |out|); with the LN consumer the fused graph launches fewer
+    kernels than the reference-order one."""
+    E, H, F, n_ctx, N = 768, 12, 3072, 1024, 1
+    D = E // H
+    cur_v = rnd(21, 3 * E, 1.0)
+    mem_k, mem_v = rnd(22, E * n_ctx, 1.0), rnd(23, E * n_ctx, 1.0)
+    wp = (rnd(24, E * E, 0.05)).astype(np.float16)
+    bp, res = rnd(25, E, 0.1), rnd(26, E, 1.0)
+    g2, b2 = rnd(27, E, 0.2) + np.float32(1.0), rnd(28, E, 0.1)
+    wf = (rnd(29, E * F, 0.05)).astype(np.float16)
+    bf = rnd(30, F, 0.1)
+
+    def build(L, c):
+        cur = L.ggml_new_tensor_2d(c, F32, 3 * E, N)
+        mk, mv = L.ggml_new_tensor_1d(c, F32, E * n_ctx), L.ggml_new_tensor_1d(c, F32, E * n_ctx)
+        Wp, Bp, R = L.ggml_new_tensor_2d(c, F16, E, E), L.ggml_new_tensor_1d(c, F32, E), L.ggml_new_tensor_2d(c, F32, E, N)
+        G2, B2 = L.ggml_new_tensor_1d(c, F32, E), L.ggml_new_tensor_1d(c, F32, E)
+        Wf, Bf = L.ggml_new_tensor_2d(c, F16, E, F), L.ggml_new_tensor_1d(c, F32, F)
+        nb1 = cur.contents.nb[1]
+        Qcur = L.ggml_view_2d(c, cur, E, N, nb1, 0)
+        Kcur = L.ggml_view_2d(c, cur, E, N, nb1, 4 * E)
+        Vcur = L.ggml_view_2d(c, cur, E, N, nb1, 8 * E)
+        ck = L.ggml_cpy(c, Kcur, L.ggml_view_1d(c, mk, N * E, 4 * E * n_past))
+        cv = L.ggml_cpy(c, Vcur, L.ggml_view_1d(c, mv, N * E, 4 * E * n_past))
+        Q = L.ggml_permute(c, L.ggml_cont_3d(c, Qcur, D, H, N), 0, 2, 1, 3)
+        K = L.ggml_permute(c, L.ggml_reshape_3d(c, L.ggml_view_1d(c, mk, (n_past + N) * E, 0), D, H, n_past + N), 0, 2, 1, 3)
+        sm = L.ggml_soft_max(c, L.ggml_diag_mask_inf(c, L.ggml_scale(c, L.ggml_mul_mat(c, K, Q), 1.0 / np.sqrt(D)), n_past))
+        Vt = L.ggml_cont_3d(c, L.ggml_permute(c, L.ggml_reshape_3d(c, L.ggml_view_1d(c, mv, (n_past + N) * E, 0), D, H, n_past + N),
+                                              1, 2, 0, 3), n_past + N, D, H)
+        att = L.ggml_cont_2d(c, L.ggml_permute(c, L.ggml_mul_mat(c, Vt, sm), 0, 2, 1, 3), E, N)
+        O = L.ggml_add(c, L.ggml_add(c, L.ggml_mul_mat(c, Wp, att), Bp), R)
+        if consumer == "ln_fc":
+            h = L.ggml_add(c, L.ggml_mul(c, L.ggml_norm(c, O, 1e-5), G2), B2)
+            y = L.ggml_gelu(c, L.ggml_add(c, L.ggml_mul_mat(c, Wf, h), Bf))
+        else:
+            y = L.ggml_add(c, O, O)
+        feeds = [(cur, cur_v), (mk, mem_k), (mv, mem_v), (Wp, wp), (Bp, bp), (R, res), (G2, g2), (B2, b2), (Wf, wf), (Bf, bf)]
+        return feeds, [y, O], [ck, cv]
+
+    rt, be, ref, cpu = libs
+    (y_a, o_a), n_fast = graph_outputs(rt, be, lambda c: build(rt, c))
+    assert rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 1)
+    try:
+        (y_1, o_1), n_ord = graph_outputs(rt, be, lambda c: build(rt, c))
+    finally:
+        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
+    (y_r, o_r), _ = graph_outputs(ref, cpu, lambda c: build(ref, c))
+    eo = float(np.max(np.abs(o_a - o_r)) / np.max(np.abs(o_r)))
+    ey = float(np.max(np.abs(y_a - y_r)) / np.max(np.abs(y_r)))
+    print(f"{consumer} n_past={n_past}: residual stream rel err {eo:.2e}, output {ey:.2e}; launches {n_fast} (fused) vs {n_ord}")
+    assert eo <= 5e-5 and ey <= 2e-4, (eo, ey)
+    # ln_fc: the projection's own GEMV launch is gone; add: it is traded for mi_sum_parts
+    assert n_fast < n_ord if consumer == "ln_fc" else n_fast <= n_ord
+    # reference order: the unfused kernels, bit for bit
+    assert_exact(o_1, o_r, "residual stream, reference order")
