@@ -429,14 +429,21 @@ __device__ void norm_prologue(const mi_mmv_group & g, const char * X, int ncols,
     const int64_t K = g.K;
     for (int c = 0; c < ncols; c++) {
         const float * xc = (const float *) (X + c * g.xcol);
+        // every load unconditional at a clamped index, then a select: a load under a lane branch
+        // makes the compiler wait for it (vmcnt(0)) at the branch's join, serialising all 3 kJ
+        // loads; absent g / b read x instead (a valid address; the value is replaced)
+        const float * gp = g.pro.g ? g.pro.g : xc;
+        const float * bp = g.pro.b ? g.pro.b : xc;
         float v[kJ], gv[kJ], bv[kJ];
 #pragma unroll
         for (int j = 0; j < kJ; j++) {
             const int64_t k = (int64_t) j * 64 + lane;
             const bool in = k < K;
-            v[j] = in ? xc[k] : 0.0f;
-            gv[j] = in && g.pro.g ? g.pro.g[k] : 1.0f;
-            bv[j] = in && g.pro.b ? g.pro.b[k] : 0.0f;
+            const int64_t kc = in ? k : K - 1;
+            const float xv = xc[kc], gl = gp[kc], bl = bp[kc];
+            v[j] = in ? xv : 0.0f;
+            gv[j] = in && g.pro.g ? gl : 1.0f;
+            bv[j] = in && g.pro.b ? bl : 0.0f;
         }
         float scale;
         if (g.pro.mode == 2) {

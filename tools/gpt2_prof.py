@@ -5,8 +5,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from ggml_mi355x import ggml as G, gpt2
 
 n_decode = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-path = gpt2.ensure_model()
 lib = G.runtime()
+path = gpt2.ensure_quantized_model(lib, os.environ["GPT2_QTYPE"]) if os.environ.get("GPT2_QTYPE") else gpt2.ensure_model()
 be = G.mi355x_backend(lib)
 m = gpt2.Model(lib, path, be, n_ctx=1024, n_batch=8, host_io=os.environ.get("GPT2_HOST_IO", "1") == "1")
 toks = m.tokenize("Once upon a time the cat sat on the mat and the dog ran away")[:32]
