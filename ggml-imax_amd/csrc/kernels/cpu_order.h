@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mi355x_common.h"
+
 // Bit-exactness with the CPU needs every multiply and add rounded separately unless written as
 // __fmaf_rn: HIP's __fmul_rn/__fadd_rn are plain operators defined in a header (so this file's
 // pragma does not reach them) that -ffp-contract=fast would fuse; mul_rn/add_rn below are
@@ -95,11 +97,9 @@ __device__ float wave_mean_cpu_order(const float (&v)[J], int64_t n) {
             a += fabs(t);
         }
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        s += __shfl_xor(s, off, 64);
-        a += __shfl_xor(a, off, 64);
-    }
+    // DPP wave sums (any order: the bound below holds for every order)
+    s = mi_wave_sum_u_f64(s);
+    a = mi_wave_sum_u_f64(a);
     const double B = 4.0 * (double) n * a * 0x1p-53 + 0x1p-1074;
     const float lo = (float) ((s - B) / (double) n);
     const float hi = (float) ((s + B) / (double) n);

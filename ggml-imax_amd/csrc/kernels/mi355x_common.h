@@ -75,6 +75,23 @@ __device__ __forceinline__ int mi_dpp(int old, int v) {
     return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xF, false);
 }
 
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ double mi_dpp_f64(double v) {  // both halves moved by the same DPP pattern (0.0 where masked)
+    const int lo = mi_dpp<CTRL, ROWMASK>(0, __double2loint(v));
+    const int hi = mi_dpp<CTRL, ROWMASK>(0, __double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double mi_wave_sum_u_f64(double v) {  // uniform result (some order)
+    v += mi_dpp_f64<MI_DPP_QP_1032>(v);
+    v += mi_dpp_f64<MI_DPP_QP_2301>(v);
+    v += mi_dpp_f64<MI_DPP_ROW_HALF_MIRROR>(v);
+    v += mi_dpp_f64<MI_DPP_ROW_MIRROR>(v);
+    v += mi_dpp_f64<MI_DPP_ROW_BCAST15, 0xA>(v);
+    v += mi_dpp_f64<MI_DPP_ROW_BCAST31, 0xC>(v);
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63), __builtin_amdgcn_readlane(__double2loint(v), 63));
+}
+
 __device__ __forceinline__ float mi_wave_sum_u(float v) {  // uniform result
     auto f = [](int x) { return __int_as_float(x); };
     auto i = [](float x) { return __float_as_int(x); };

@@ -168,14 +168,19 @@ __device__ __forceinline__ void stage_f16_activations(uint16_t * xs, double * sh
         if ((threadIdx.x >> 6) != 0) return;
         for (int c = 0; c < nc; c++) {
             const float * xc = (const float *) (x.base + (i11 + c) * x.nb1);
+            // unconditional loads at clamped indices + selects (no per-load waits at branch joins)
+            const float * gp = pro.g ? pro.g : xc;
+            const float * bp = pro.b ? pro.b : xc;
             float v[kJ], gv[kJ], bv[kJ];
 #pragma unroll
             for (int j = 0; j < kJ; j++) {
                 const int64_t k = (int64_t) j * 64 + lane;
                 const bool in = k < K;
-                v[j] = in ? xc[k] : 0.0f;
-                gv[j] = in && pro.g ? pro.g[k] : 1.0f;
-                bv[j] = in && pro.b ? pro.b[k] : 0.0f;
+                const int64_t kc = in ? k : K - 1;
+                const float xv = xc[kc], gl = gp[kc], bl = bp[kc];
+                v[j] = in ? xv : 0.0f;
+                gv[j] = in && pro.g ? gl : 1.0f;
+                bv[j] = in && pro.b ? bl : 0.0f;
             }
             float scale;
             if (pro.mode == 2) {
