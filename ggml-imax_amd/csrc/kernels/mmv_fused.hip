@@ -422,47 +422,58 @@ struct FmtQ0 {
 // in-line); PD = rows in flight ahead of the row being computed.
 // norm|rms_norm -> mul(g) -> add(b) of the group's activation columns into LDS (f32), by wave 0
 // with each column in registers -- the arithmetic of k_norm (ops.hip) and of the F16 GEMV's
-// prologue: certified double means, then every step rounded separately
-__device__ void norm_prologue(const mi_mmv_group & g, const char * X, int ncols, float * xn) {
-    constexpr int kJ = (int) (kMiMmvProMaxK / 64);
+// prologue: certified double means, then every step rounded separately. norm_cols: a column's x,
+// g, b in registers (every load unconditional at a clamped index, then a select: a load under a
+// lane branch makes the compiler wait for it at the branch's join; absent g / b read x instead).
+struct norm_cols {
+    static constexpr int kJ = (int) (kMiMmvProMaxK / 64);
+    float v[kJ], gv[kJ], bv[kJ];
+};
+
+__device__ __forceinline__ void norm_cols_load(const mi_mmv_group & g, const char * X, int c, norm_cols & r) {
+    const int lane = threadIdx.x & 63;
+    const int64_t K = g.K;
+    const float * xc = (const float *) (X + c * g.xcol);
+    const float * gp = g.pro.g ? g.pro.g : xc;
+    const float * bp = g.pro.b ? g.pro.b : xc;
+#pragma unroll
+    for (int j = 0; j < norm_cols::kJ; j++) {
+        const int64_t k = (int64_t) j * 64 + lane;
+        const bool in = k < K;
+        const int64_t kc = in ? k : K - 1;
+        const float xv = xc[kc], gl = gp[kc], bl = bp[kc];
+        r.v[j] = in ? xv : 0.0f;
+        r.gv[j] = in && g.pro.g ? gl : 1.0f;
+        r.bv[j] = in && g.pro.b ? bl : 0.0f;
+    }
+}
+
+// r: column 0, already loaded (before the weight stream, so that vmcnt does not make it wait for
+// the weights); the other columns are loaded here
+__device__ void norm_prologue(const mi_mmv_group & g, const char * X, int ncols, float * xn, norm_cols & r) {
+    constexpr int kJ = norm_cols::kJ;
     const int lane = threadIdx.x & 63;
     const int64_t K = g.K;
     for (int c = 0; c < ncols; c++) {
-        const float * xc = (const float *) (X + c * g.xcol);
-        // every load unconditional at a clamped index, then a select: a load under a lane branch
-        // makes the compiler wait for it (vmcnt(0)) at the branch's join, serialising all 3 kJ
-        // loads; absent g / b read x instead (a valid address; the value is replaced)
-        const float * gp = g.pro.g ? g.pro.g : xc;
-        const float * bp = g.pro.b ? g.pro.b : xc;
-        float v[kJ], gv[kJ], bv[kJ];
-#pragma unroll
-        for (int j = 0; j < kJ; j++) {
-            const int64_t k = (int64_t) j * 64 + lane;
-            const bool in = k < K;
-            const int64_t kc = in ? k : K - 1;
-            const float xv = xc[kc], gl = gp[kc], bl = bp[kc];
-            v[j] = in ? xv : 0.0f;
-            gv[j] = in && g.pro.g ? gl : 1.0f;
-            bv[j] = in && g.pro.b ? bl : 0.0f;
-        }
+        if (c > 0) norm_cols_load(g, X, c, r);
         float scale;
         if (g.pro.mode == 2) {
-            const float mean = wave_mean_cpu_order<true, kJ>(v, K);
+            const float mean = wave_mean_cpu_order<true, kJ>(r.v, K);
             scale = 1.0f / sqrtf(add_rn(mean, g.pro.eps));
         } else {
-            const float mean = wave_mean_cpu_order<false, kJ>(v, K);
+            const float mean = wave_mean_cpu_order<false, kJ>(r.v, K);
 #pragma unroll
-            for (int j = 0; j < kJ; j++) v[j] = sub_rn(v[j], mean);
-            const float variance = wave_mean_cpu_order<true, kJ>(v, K);
+            for (int j = 0; j < kJ; j++) r.v[j] = sub_rn(r.v[j], mean);
+            const float variance = wave_mean_cpu_order<true, kJ>(r.v, K);
             scale = 1.0f / sqrtf(add_rn(variance, g.pro.eps));
         }
 #pragma unroll
         for (int j = 0; j < kJ; j++) {
             const int64_t k = (int64_t) j * 64 + lane;
             if (k < K) {
-                float y = mul_rn(v[j], scale);
-                if (g.pro.g) y = mul_rn(y, gv[j]);
-                if (g.pro.b) y = add_rn(y, bv[j]);
+                float y = mul_rn(r.v[j], scale);
+                if (g.pro.g) y = mul_rn(y, r.gv[j]);
+                if (g.pro.b) y = add_rn(y, r.bv[j]);
                 xn[c * K + k] = y;
             }
         }
@@ -536,6 +547,11 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     };
     const int klast = nrows > 0 ? nrows - 1 : 0;
 
+    // 0) the norm prologue's first column, g and b (wave 0), requested before the weights
+    norm_cols nc0;
+    if constexpr (PRO) {
+        if (g.pro.mode && wave == 0) norm_cols_load(g, X, 0, nc0);
+    }
     // 1) the first PD rows' weights in flight
 #pragma unroll
     for (int u = 0; u < PD; u++) prefetch(ring[u], u < klast ? u : klast);
@@ -546,7 +562,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     size_t xcolq = g.xcol;
     if (PRO && g.pro.mode) {
         float * xn = (float *) (lds + g.pro_off);
-        if (wave == 0) norm_prologue(g, X, ncols, xn);
+        if (wave == 0) norm_prologue(g, X, ncols, xn, nc0);
         __syncthreads();
         Xq = (const char *) xn;
         xcolq = (size_t) K * sizeof(float);
