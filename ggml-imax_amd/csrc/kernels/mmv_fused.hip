@@ -547,10 +547,26 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     };
     const int klast = nrows > 0 ? nrows - 1 : 0;
 
-    // 0) the norm prologue's first column, g and b (wave 0), requested before the weights
+    // 0) what the prologue reads first, requested before the weights (vmcnt retires in order: a
+    //    use of it would otherwise wait for the weight loads too): the norm prologue's first
+    //    column, g and b (wave 0), or the activation slices of the first quantization round
     norm_cols nc0;
+    const int nsl = (int) (K / 256);
+    const int total = nsl * ncols;
+    float4 xfirst[4];
+    auto load_round = [&](float4 (&v)[4], const char * Xs, size_t xcs, int p0) {
+        // unconditional (clamped) loads: a predicated load makes hipcc wait vmcnt(0) per load
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = min(p0 + 4 * u, total - 1);
+            const int c = p / nsl, sl = p - c * nsl;
+            v[u] = *(const float4 *) (Xs + c * xcs + ((size_t) sl * 256 + lane * 4) * sizeof(float));
+        }
+    };
     if constexpr (PRO) {
         if (g.pro.mode && wave == 0) norm_cols_load(g, X, 0, nc0);
+    } else {
+        load_round(xfirst, X, g.xcol, wave);
     }
     // 1) the first PD rows' weights in flight
 #pragma unroll
@@ -568,16 +584,13 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
         xcolq = (size_t) K * sizeof(float);
     }
     {
-        const int nsl = (int) (K / 256);
-        const int total = nsl * ncols;
         for (int p0 = wave; p0 < total; p0 += 16) {
-            // unconditional (clamped) loads: a predicated load makes hipcc wait vmcnt(0) per load
             float4 v[4];
+            if (!PRO && p0 == wave) {
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int p = min(p0 + 4 * u, total - 1);
-                const int c = p / nsl, sl = p - c * nsl;
-                v[u] = *(const float4 *) (Xq + c * xcolq + ((size_t) sl * 256 + lane * 4) * sizeof(float));
+                for (int u = 0; u < 4; u++) v[u] = xfirst[u];
+            } else {
+                load_round(v, Xq, xcolq, p0);
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
