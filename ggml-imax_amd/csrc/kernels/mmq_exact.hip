@@ -467,7 +467,14 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
 // issued and applies its own row's d / dmin. Each wave's registers are reloaded with its next
 // round's superblock as soon as they are consumed (one round of lead).
 // C4: ncols % 4 == 0 (the four da of an accumulator row group are one aligned 16-byte load).
-template <int TYPE, bool C4>
+// PF: weight ring depth in rounds -- the raw weights of round rd + PF are requested as round rd
+// consumes its own, so with PF = 2 both rounds of a K = 4096 tile are in flight from the start (one
+// memory latency per tile instead of one per round); activations keep one round of lead (L2).
+// ABL: timing ablations (results invalid): 1 no MFMAs, 2 no weight reloads, 4 no activation
+// reloads, 8 no LDS fold / barriers
+// CH: independent accumulator chains per plane (steps kk alternate between them; their exact
+// int32 sums are added at the end)
+template <int TYPE, bool C4, int PF = 1, int ABL = 0, int CH = 1>
 __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
                                               float * __restrict__ dst, size_t ycol) {
     using F = XFmt<TYPE>;
@@ -514,30 +521,41 @@ __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, si
                                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 12, 0, 0)));
         }
     };
+    auto sb_of = [&](int rd) { const int s = rd * nw + w; return s < S ? s : S - 1; };
+    // raw weights of one round: header, four 16-byte quant chunks (+ the high bits of Q5_K)
+    struct Wt {
+        uint4 hdr, q4[4], qh;
+    };
+    auto ld_wt = [&](Wt & t, int sb) {
+        t.hdr = ld_w(sb, 0);
+#pragma unroll
+        for (int p = 0; p < 4; p++) t.q4[p] = ld_w(sb, kQs + 32 * p + 16 * h);
+        if constexpr (F::Q5) t.qh = ld_w(sb, 16 + 16 * h);
+    };
 
-    int sb = w < S ? w : S - 1;
     i32x4 xa[8];
+    Wt wt[PF];
+    {
+        const int sb = sb_of(0);
 #pragma unroll
-    for (int kk = 0; kk < 8; kk++) xa[kk] = ld_x(sb, kk);
-    uint4 hdr = ld_w(sb, 0);
-    uint4 q4[4];
-#pragma unroll
-    for (int p = 0; p < 4; p++) q4[p] = ld_w(sb, kQs + 32 * p + 16 * h);
-    uint4 qh = F::Q5 ? ld_w(sb, 16 + 16 * h) : uint4{};
-    half8 xu = ld_u(sb);
+        for (int kk = 0; kk < 8; kk++) xa[kk] = ld_x(sb, kk);
+        ld_wt(wt[0], sb);
+    }
+    half8 xu = ld_u(sb_of(0));
     float4 da[4];
 #pragma unroll
-    for (int g = 0; g < 4; g++) da[g] = ld_da(sb, g);
+    for (int g = 0; g < 4; g++) da[g] = ld_da(sb_of(0), g);
+#pragma unroll
+    for (int u = 1; u < PF; u++) ld_wt(wt[u], sb_of(u));
 
     f32x16 y = {};  // the fold (wave 0)
     float * mine = red + ((size_t) w * 64 + lane) * 16;
-    for (int rd = 0; rd < rounds; rd++) {
-        const int cur = rd * nw + w;
-        int sn = cur + nw;
-        sn = sn < S ? sn : S - 1;
+    auto round = [&](const int rd, Wt & t) {
+        const int sn = sb_of(rd + 1);   // activations: one round of lead
+        const int sw = sb_of(rd + PF);  // weights: PF rounds of lead
         // header -> plane factors (splat u16x2), U operand, d, dmin (get_scale_min_k4, ggml-quants.c)
-        const uint32_t w0 = hdr.y, w1 = hdr.z, w2 = hdr.w;
-        const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
+        const uint32_t w0 = t.hdr.y, w1 = t.hdr.z, w2 = t.hdr.w;
+        const float dw = mi_h2f((uint16_t) (t.hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (t.hdr.x >> 16));
         uint32_t fac[8][NP];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -551,18 +569,19 @@ __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, si
         }
         half8 mu;
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int j = 4 * h + t;  // this lane's k-halves of the U MFMA: sub-blocks 4h .. 4h + 3
+        for (int q = 0; q < 4; q++) {
+            const int j = 4 * h + q;  // this lane's k-halves of the U MFMA: sub-blocks 4h .. 4h + 3
             const int jj = j & 3;
             const uint32_t m = j < 4 ? ((w1 >> (8 * jj)) & 63) : (((w2 >> (8 * jj + 4)) & 0xF) | (((w1 >> (8 * jj + 6)) & 3) << 4));
-            mu[2 * t] = (_Float16) (float) m;
-            mu[2 * t + 1] = (_Float16) (float) (64 * m);
+            mu[2 * q] = (_Float16) (float) m;
+            mu[2 * q + 1] = (_Float16) (float) (64 * m);
         }
-        hdr = ld_w(sn, 0);
-        i32x16 acc[NP];
+        if constexpr ((ABL & 2) == 0) t.hdr = ld_w(sw, 0);
+        const uint4 qh = t.qh;
+        i32x16 acc[CH][NP];
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) {
-            const uint4 q = q4[kk >> 1];
+            const uint4 q = t.q4[kk >> 1];
             uint32_t v[4] = {q.x, q.y, q.z, q.w};
             const uint32_t hb[4] = {qh.x, qh.y, qh.z, qh.w};
 #pragma unroll
@@ -570,18 +589,20 @@ __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, si
                 v[e] = (kk & 1) ? (v[e] >> 4) & 0x0F0F0F0Fu : v[e] & 0x0F0F0F0Fu;
                 if constexpr (F::Q5) v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
             }
-            if (kk & 1) q4[kk >> 1] = ld_w(sn, kQs + 32 * (kk >> 1) + 16 * h);
+            if ((ABL & 2) == 0 && (kk & 1)) t.q4[kk >> 1] = ld_w(sw, kQs + 32 * (kk >> 1) + 16 * h);
 #pragma unroll
             for (int p = 0; p < NP; p++) {
                 const uint32_t f = fac[kk][p];
                 const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
-                acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[kk], b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
+                i32x16 & a = acc[kk % CH][p];
+                if constexpr ((ABL & 1) != 0) a[kk] = (kk < CH ? 0 : a[kk]) + xa[kk][0] * b[0];
+                else a = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[kk], b, kk < CH ? i32x16{} : a, 0, 0, 0);
             }
-            xa[kk] = ld_x(sn, kk);
+            if constexpr ((ABL & 4) == 0) xa[kk] = ld_x(sn, kk);
         }
-        if constexpr (F::Q5) qh = ld_w(sn, 16 + 16 * h);
+        if constexpr (F::Q5) t.qh = ld_w(sw, 16 + 16 * h);
         const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
-        xu = ld_u(sn);
+        if constexpr ((ABL & 4) == 0) xu = ld_u(sn);
         float term[16];
 #pragma unroll
         for (int g = 0; g < 4; g++) {
@@ -589,12 +610,18 @@ __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, si
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 const int el = 4 * g + e;
-                int T = acc[NP - 1][el];
+                auto P = [&](int p) { int v = acc[0][p][el]; if constexpr (CH > 1) v += acc[1][p][el]; return v; };
+                int T = P(NP - 1);
 #pragma unroll
-                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
+                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + P(p);
                 term[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
             }
-            da[g] = ld_da(sn, g);
+            if constexpr ((ABL & 4) == 0) da[g] = ld_da(sn, g);
+        }
+        if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+            for (int q = 0; q < 16; q++) y[q] = rd == 0 ? term[q] : y[q] + term[q];
+            return;
         }
         // the round's terms meet in LDS; wave 0 folds them in superblock order
 #pragma unroll
@@ -614,9 +641,148 @@ __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, si
             }
         }
         mi_lds_barrier();
+    };
+    // unrolled by PF so every ring slot index is static (round rd uses slot rd % PF)
+    for (int rd0 = 0; rd0 < rounds; rd0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            if (rd0 + u < rounds) round(rd0 + u, wt[u]);
+        }
     }
     if (w != 0) return;
     // store: element el = prompt column c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
+    const int64_t n = n0 + r;
+    if (n >= N) return;
+#pragma unroll
+    for (int el = 0; el < 16; el++) {
+        const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * h;
+        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y[el];
+    }
+}
+
+// ---- short prompts, K <= 4096: one round -------------------------------------------------------
+// A workgroup of S waves (one superblock each) per 32 x 32 tile, so every load of the tile is
+// requested at once and no wave runs a second round (k_mmqd's rounds each wait a full memory
+// latency: the load -> MFMA -> fold phases of the two waves of a SIMD do not overlap). Four waves
+// per SIMD at S = 16: <= 128 VGPRs, so the 16 da of a lane's accumulator elements go through a
+// wave-private LDS row instead of registers. Same operands, same exact T / U and the same
+// canonical fold (terms left-folded in superblock order) as k_mmqd / k_mmqx: bit-identical.
+template <int TYPE>
+__global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
+                                               float * __restrict__ dst, size_t ycol) {
+    using F = XFmt<TYPE>;
+    constexpr int NP = F::NP;
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [wave][lane][16] terms, then [wave][32] da
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t ncols = act.ncols;
+    const int S = (int) (K / 256);  // == waves of the workgroup
+    const int64_t nrt = (N + 31) / 32;
+    const int64_t n0 = (blockIdx.x % nrt) * 32, c0 = (blockIdx.x / nrt) * 32;
+    const int sb = w;
+
+    const int nrows = (int) std::min<int64_t>(32, N - n0);
+    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
+    const uint32_t wrow = (uint32_t) (min(r, nrows - 1) * nb01) + (uint32_t) sb * F::BS;
+    const uint32_t acol = (uint32_t) std::min<int64_t>(c0 + r, ncols - 1);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
+    const uint32_t xstep = (uint32_t) ncols * 64;
+    const uint32_t xcol = acol * 64 + 16 * h + (uint32_t) sb * 4 * xstep;
+    constexpr uint32_t kQs = F::Q5 ? 48 : 16;
+
+    // every load of the wave, weights first (HBM), then the activation fragments (L2)
+    auto ld_w = [&](uint32_t off) -> uint4 { return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wrow + off, 0, 0)); };
+    const uint4 hdr = ld_w(0);
+    uint4 q4[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) q4[p] = ld_w(kQs + 32 * p + 16 * h);
+    const uint4 qh = F::Q5 ? ld_w(16 + 16 * h) : uint4{};
+    i32x4 xa[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++)
+        xa[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kk >> 1) * xstep + 32 * (kk & 1), 0, 0));
+    const half8 xu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, ((uint32_t) sb * (uint32_t) ncols + acol) * 32 + 16 * h, 0, 0));
+    // da of prompt column c0 + r (lanes >= 32 duplicate), parked in this wave's LDS row: columns
+    // past ncols read a clamped column's value (never stored)
+    const float dal = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, ((uint32_t) sb * (uint32_t) ncols + acol) * 4, 0, 0));
+    float * dal_row = red + (size_t) S * 64 * 16 + w * 32;
+    if (h == 0) dal_row[r] = dal;
+    __builtin_amdgcn_wave_barrier();  // wave-private row: LDS ops of a wave complete in order
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+
+    const uint32_t w0 = hdr.y, w1 = hdr.z, w2 = hdr.w;
+    const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
+    i32x16 acc[NP];
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) {
+        const int jj = kk & 3;
+        const uint32_t sc = kk < 4 ? ((w0 >> (8 * jj)) & 63) : (((w2 >> (8 * jj)) & 0xF) | (((w0 >> (8 * jj + 6)) & 3) << 4));
+        const uint4 q = q4[kk >> 1];
+        uint32_t v[4] = {q.x, q.y, q.z, q.w};
+        const uint32_t hb[4] = {qh.x, qh.y, qh.z, qh.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            v[e] = (kk & 1) ? (v[e] >> 4) & 0x0F0F0F0Fu : v[e] & 0x0F0F0F0Fu;
+            if constexpr (F::Q5) v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
+        }
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            uint32_t f = F::factor((int) sc, p);
+            f |= f << 16;
+            const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+            acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[kk], b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
+        }
+    }
+    half8 mu;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int j = 4 * h + q;  // this lane's k-halves of the U MFMA: sub-blocks 4h .. 4h + 3
+        const int jj = j & 3;
+        const uint32_t m = j < 4 ? ((w1 >> (8 * jj)) & 63) : (((w2 >> (8 * jj + 4)) & 0xF) | (((w1 >> (8 * jj + 6)) & 3) << 4));
+        mu[2 * q] = (_Float16) (float) m;
+        mu[2 * q + 1] = (_Float16) (float) (64 * m);
+    }
+    const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
+    float * mine = red + ((size_t) w * 64 + lane) * 16;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const float4 d4 = *(const float4 *) (dal_row + 8 * g + 4 * h);
+        const float dav[4] = {d4.x, d4.y, d4.z, d4.w};
+        float term[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int el = 4 * g + e;
+            int T = acc[NP - 1][el];
+#pragma unroll
+            for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
+            term[e] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
+        }
+        *(float4 *) (mine + 4 * g) = make_float4(term[0], term[1], term[2], term[3]);
+    }
+    mi_lds_barrier();
+    // wave 0 left-folds the terms in superblock order and stores; element el = prompt column
+    // c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
+    if (w != 0) return;
+    f32x16 y;
+    {
+        const float * src = red + (size_t) lane * 16;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float4 t4 = *(const float4 *) (src + 4 * q);
+            y[4 * q] = t4.x; y[4 * q + 1] = t4.y; y[4 * q + 2] = t4.z; y[4 * q + 3] = t4.w;
+        }
+    }
+    for (int v = 1; v < S; v++) {
+        const float * src = red + ((size_t) v * 64 + lane) * 16;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float4 t4 = *(const float4 *) (src + 4 * q);
+            y[4 * q] = y[4 * q] + t4.x; y[4 * q + 1] = y[4 * q + 1] + t4.y;
+            y[4 * q + 2] = y[4 * q + 2] + t4.z; y[4 * q + 3] = y[4 * q + 3] + t4.w;
+        }
+    }
     const int64_t n = n0 + r;
     if (n >= N) return;
 #pragma unroll
@@ -646,14 +812,42 @@ void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N
     if (direct) {
         const int64_t nrt = (N + 31) / 32, nct = (act.ncols + 31) / 32;
         const int S = (int) (K / 256);
+        if (S <= 16 && !(var & 2048)) {  // one round: a wave per superblock (variant bit 2048: k_mmqd)
+            const dim3 grid((unsigned) (nrt * nct));
+            const size_t lds = (size_t) S * 64 * 16 * sizeof(float) + (size_t) S * 32 * sizeof(float);
+            if (type == 12) hipLaunchKernelGGL((k_mmqd1<12>), grid, dim3(64 * S), lds, s, w, nb01, K, N, act, dst, ycol);
+            else hipLaunchKernelGGL((k_mmqd1<13>), grid, dim3(64 * S), lds, s, w, nb01, K, N, act, dst, ycol);
+            return;
+        }
         const int nwv = std::min(S, 8);  // waves per tile (superblocks dealt round-robin)
         const dim3 grid((unsigned) (nrt * nct));
         const size_t lds = (size_t) nwv * 64 * 16 * sizeof(float);
         const bool c4 = act.ncols % 4 == 0;
-#define MI_MMQD(TY, C) hipLaunchKernelGGL((k_mmqd<TY, C>), grid, dim3(64 * nwv), lds, s, w, nb01, K, N, act, dst, ycol)
-        if (type == 12) { if (c4) MI_MMQD(12, true); else MI_MMQD(12, false); }
-        else { if (c4) MI_MMQD(13, true); else MI_MMQD(13, false); }
+        // weight ring depth (variant bit 256 -> two rounds of lead, default one); bit 512: two
+        // accumulator chains per plane
+#define MI_MMQD(TY, C, P, CHN) hipLaunchKernelGGL((k_mmqd<TY, C, P, 0, CHN>), grid, dim3(64 * nwv), lds, s, w, nb01, K, N, act, dst, ycol)
+#define MI_MMQDA(A) hipLaunchKernelGGL((k_mmqd<12, true, 1, A>), grid, dim3(64 * nwv), lds, s, w, nb01, K, N, act, dst, ycol)
+        if ((var >> 12) & 15) {  // timing ablations (results invalid): Q4_K, ncols % 4 == 0, PF 1
+            switch ((var >> 12) & 15) {
+            case 1: MI_MMQDA(1); break;
+            case 2: MI_MMQDA(2); break;
+            case 4: MI_MMQDA(4); break;
+            case 6: MI_MMQDA(6); break;
+            case 8: MI_MMQDA(8); break;
+            default: MI_MMQDA(15); break;
+            }
+        } else if (var & 256) {
+            if (type == 12) { if (c4) MI_MMQD(12, true, 2, 1); else MI_MMQD(12, false, 2, 1); }
+            else { if (c4) MI_MMQD(13, true, 2, 1); else MI_MMQD(13, false, 2, 1); }
+        } else if (var & 512) {
+            if (type == 12) { if (c4) MI_MMQD(12, true, 1, 2); else MI_MMQD(12, false, 1, 2); }
+            else { if (c4) MI_MMQD(13, true, 1, 2); else MI_MMQD(13, false, 1, 2); }
+        } else {
+            if (type == 12) { if (c4) MI_MMQD(12, true, 1, 1); else MI_MMQD(12, false, 1, 1); }
+            else { if (c4) MI_MMQD(13, true, 1, 1); else MI_MMQD(13, false, 1, 1); }
+        }
 #undef MI_MMQD
+#undef MI_MMQDA
         return;
     }
     const int64_t nrt = (N + XBM - 1) / XBM, nct = (act.ncols + XBN - 1) / XBN;

@@ -12,13 +12,16 @@ lib = G.runtime()
 be = G.mi355x_backend(lib, 0)
 sp = lib.ggml_backend_mi355x_get_stream(be)
 Bs = [int(b) for b in sys.argv[1:]] or [512, 64]
+VARS = [int(v) for v in os.environ.get("MMQ_VARIANTS", "0").split(",")]
 for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
     for B in Bs:
+      for var in VARS:
+        lib.ggml_backend_mi355x_set_tuning(b"mmq_variant", var)
         t = bench.TYPE_NAMES[tname]
         wl = bench.MulMatWorkload(lib, be, t, 4096, 4096, B, 8)
         for _ in range(3):
             wl.step()
         ms = np.median([bench.event_time_per_step(torch, wl, sp, iters=5) for _ in range(3)])
-        print(f"{tname:5s} B={B:4d}: {ms * 1e3 / 8:8.2f} us/mul_mat  {2 * 4096 * 4096 * B * 8 / (ms / 1e3) / 1e12:7.1f} TFLOP/s")
+        print(f"{tname:5s} B={B:4d} var={var:4d}: {ms * 1e3 / 8:8.2f} us/mul_mat  {2 * 4096 * 4096 * B * 8 / (ms / 1e3) / 1e12:7.1f} TFLOP/s")
         wl.free()
 lib.ggml_backend_free(be)
