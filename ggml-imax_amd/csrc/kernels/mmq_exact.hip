@@ -87,17 +87,25 @@ struct XRaw {
 
 // ---- activations: q8_K quants in the MFMA layouts ------------------------------------------------
 // xq [K/64][ncols][64] int8, xd [K/256][ncols] f32 (d), xu [K/256][ncols][16] f16 (S_j & 63,
-// S_j >> 6 for j = 0..7, S_j = sum of the 32 quants of sub-block j). One superblock per wave.
-__global__ __launch_bounds__(256) void k_quantize_q8_K_mmx(mi_src_cols x, int64_t K, mi_act_mmx act, int64_t nblocks_total) {
-    const int wave = threadIdx.x >> 6;
+// S_j >> 6 for j = 0..7, S_j = sum of the 32 quants of sub-block j). One superblock per wave;
+// grid (column, group of 4 superblocks): the column's address is wave-uniform scalar arithmetic
+// (32-bit, and no divisions at all for a plain 2-D src1), so the load issues at once.
+__global__ __launch_bounds__(256) void k_quantize_q8_K_mmx(mi_src_cols x, int64_t K, mi_act_mmx act) {
+    const int wave = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int64_t blk = (int64_t) blockIdx.x * 4 + wave;
-    if (blk >= nblocks_total) return;  // wave-uniform
-    const int64_t nb_per_col = K / 256;
-    const int64_t c = blk / nb_per_col;
-    const int64_t b = blk % nb_per_col;
-    const int64_t i1 = c % x.ne1, i2 = (c / x.ne1) % x.ne2, i3 = c / (x.ne1 * x.ne2);
-    const float * col = (const float *) (x.base + i1 * x.nb1 + i2 * x.nb2 + i3 * x.nb3);
+    const uint32_t nb_per_col = (uint32_t) (K / 256);
+    const uint32_t b = blockIdx.y * 4 + (uint32_t) wave;
+    if (b >= nb_per_col) return;  // wave-uniform
+    const uint32_t c = blockIdx.x;
+    const char * cbase;
+    if (x.ne2 == 1 && x.ne3 == 1) {
+        cbase = x.base + (size_t) c * x.nb1;
+    } else {
+        const uint32_t ne1 = (uint32_t) x.ne1, ne2 = (uint32_t) x.ne2;
+        const uint32_t i1 = c % ne1, i2 = (c / ne1) % ne2, i3 = c / (ne1 * ne2);
+        cbase = x.base + (size_t) i1 * x.nb1 + (size_t) i2 * x.nb2 + (size_t) i3 * x.nb3;
+    }
+    const float * col = (const float *) cbase;
     const float4 v4 = *(const float4 *) (col + b * 256 + lane * 4);
     const float v[4] = {v4.x, v4.y, v4.z, v4.w};
     // quantize_row_q8_K_reference as the reference's -mfma build computes it (mi355x_common.h:
@@ -138,8 +146,7 @@ mi_act_mmx mi_act_mmx_carve(void * base, int64_t K, int64_t ncols) {
 }
 
 void mi_quantize_q8_K_mmx(const mi_src_cols & x, int64_t K, const mi_act_mmx & act, hipStream_t s) {
-    const int64_t nblk = (K / 256) * act.ncols;
-    hipLaunchKernelGGL(k_quantize_q8_K_mmx, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, act, nblk);
+    hipLaunchKernelGGL(k_quantize_q8_K_mmx, dim3((unsigned) act.ncols, (unsigned) ((K / 256 + 3) / 4)), dim3(256), 0, s, x, K, act);
 }
 
 namespace {
