@@ -161,8 +161,10 @@ namespace {
 // one issues its MFMAs the other runs its dequantization / combine VALU.
 // Canonical combine order (shared by every kernel of this file): the superblock terms
 // (mmqx_term) left-folded in superblock order, y = term_0; y = y + term_1; ...
-template <int TYPE, bool XCD, int ABL = 0, int LEAD = 4, int SCT = 0>
-__global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+// NWV = 4: half-width workgroups (64 rows x 64 columns, 4 waves, each thread stages two rows), two
+// per CU, so one workgroup's barrier wait overlaps the other's MFMA steps.
+template <int TYPE, bool XCD, int ABL = 0, int LEAD = 4, int SCT = 0, int NWV = 8>
+__global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                               mi_act_mmx act, float * __restrict__ dst, size_t ycol) {
     using F = XFmt<TYPE>;
     constexpr int NP = F::NP;
@@ -170,6 +172,9 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
     constexpr int kPlane = XBM * XR;         // one plane of a superblock
     constexpr int kRow = XBM * 32 + XBM * 8; // row operands of the combine: U halves, d_w, dmin_w
     constexpr int kBuf = NP * kPlane + kRow;
+    constexpr int XBN_ = 16 * NWV;              // columns per workgroup
+    constexpr int ROWP = 8 / NWV;               // staging passes (rows per thread)
+    constexpr int RSTEP = 8 * NWV;              // rows per staging pass
     __shared__ __attribute__((aligned(16))) char lds[2 * kBuf];
 
     const int tid = (int) threadIdx.x;
@@ -178,7 +183,7 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
     const int64_t ncols = act.ncols;
     int64_t n0, b0;
     {
-        const int64_t nrt = (N + XBM - 1) / XBM, nct = (ncols + XBN - 1) / XBN;
+        const int64_t nrt = (N + XBM - 1) / XBM, nct = (ncols + XBN_ - 1) / XBN_;
         int64_t t = blockIdx.x;
         if constexpr (XCD) {
             // workgroup i runs on XCD i % 8: give each XCD a contiguous run of tiles, row tiles
@@ -188,7 +193,7 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
             if (t >= T) return;
         }
         n0 = (t % nrt) * XBM;
-        b0 = (t / nrt) * XBN;
+        b0 = (t / nrt) * XBN_;
     }
     const int S = (int) (K / 256);
     // timing diagnostics (ABL & 8; results invalid): s_memtime of wave 0 of workgroups 0 and 97 into
@@ -218,7 +223,9 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
     const int ar = tid >> 3, c8 = tid & 7;
     const int nrows = (int) std::min<int64_t>(XBM, N - n0);
     const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
-    const uint32_t wrow = (uint32_t) (std::min(ar, nrows - 1) * nb01);
+    uint32_t wrow[ROWP];
+#pragma unroll
+    for (int pr = 0; pr < ROWP; pr++) wrow[pr] = (uint32_t) (std::min(ar + pr * RSTEP, nrows - 1) * nb01);
     const uint32_t qoff = (F::Q5 ? 48 : 16) + 16 * c8;
     const int j0 = 2 * (c8 >> 1), hf = c8 & 1;
 
@@ -234,9 +241,9 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
     struct Raw {
         uint4 hdr, qs, qh;
     };
-    auto load_raw = [&](Raw & raw, int sb) {
+    auto load_raw = [&](Raw & raw, int sb, int pr) {
         sb = sb < S ? sb : S - 1;
-        const uint32_t blk = wrow + (uint32_t) sb * F::BS;
+        const uint32_t blk = wrow[pr] + (uint32_t) sb * F::BS;
         raw.hdr = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, blk, 0, 0));
         raw.qs = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, blk + qoff, 0, 0));
         if constexpr (F::Q5) raw.qh = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, blk + 16 + 16 * hf, 0, 0));
@@ -292,9 +299,9 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
             }
         }
     };
-    auto dq_piece = [&](int buf, const Dq & dq, int k) {
+    auto dq_piece = [&](int buf, const Dq & dq, int k, int pr) {
         if constexpr ((ABL & 1) != 0) return;  // timing ablation: no dequantization
-        char * pl0 = lds + buf * kBuf + ar * XR + 32 * j0 + 16 * hf;
+        char * pl0 = lds + buf * kBuf + (ar + pr * RSTEP) * XR + 32 * j0 + 16 * hf;
         const int p = k >> 1;
         if ((k & 1) == 0) {
             const uint32_t f0 = F::factor((int) dq.sc0, p);
@@ -304,20 +311,21 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
             *(uint4 *) (pl0 + p * kPlane + 32) = make_uint4(mulb(dq.hi[0], f1), mulb(dq.hi[1], f1), mulb(dq.hi[2], f1), mulb(dq.hi[3], f1));
         }
     };
-    auto dq_rows = [&](int buf, const Raw & raw) {
+    auto dq_rows = [&](int buf, const Raw & raw, int pr) {
         if constexpr ((ABL & 1) != 0) return;
+        const int ar = (tid >> 3) + pr * RSTEP;
         // row operands: U halves [m_c, 64 m_c] at slot c; d_w (c = 0), dmin_w (c = 1)
         char * ro = lds + buf * kBuf + NP * kPlane;
         const uint32_t mc = kmin(kc, raw.hdr.z, raw.hdr.w);
         *(uint32_t *) (ro + ar * 32 + 4 * c8) = (uint32_t) mi_f2h((float) mc) | ((uint32_t) mi_f2h((float) (64 * mc)) << 16);
         if (c8 < 2) ((float *) (ro + XBM * 32))[c8 * XBM + ar] = mi_h2f((uint16_t) (c8 == 0 ? (raw.hdr.x & 0xFFFF) : (raw.hdr.x >> 16)));
     };
-    auto store_stage = [&](int buf, const Raw & raw) {
+    auto store_stage = [&](int buf, const Raw & raw, int pr) {
         Dq dq;
         dq_prep(dq, raw);
 #pragma unroll
-        for (int k = 0; k < 2 * NP; k++) dq_piece(buf, dq, k);
-        dq_rows(buf, raw);
+        for (int k = 0; k < 2 * NP; k++) dq_piece(buf, dq, k, pr);
+        dq_rows(buf, raw, pr);
     };
 
     f32x16 y = {};
@@ -325,16 +333,19 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
     // were requested LEAD stages earlier (a ring of LEAD raw slots: HBM latency is several stage
     // times). The activation fragment of step kk of sb + 1 is loaded into the register that step kk
     // of sb has just consumed (L2-resident: one stage of lead is enough).
-    Raw raw[LEAD];
+    Raw raw[LEAD][ROWP];
     Xs xs;
-    {
+#pragma unroll
+    for (int pr = 0; pr < ROWP; pr++) {
         Raw r0;
-        load_raw(r0, 0);
-        store_stage(0, r0);
+        load_raw(r0, 0, pr);
+        store_stage(0, r0, pr);
     }
     load_x(xs, 0);
 #pragma unroll
-    for (int u = 0; u < LEAD; u++) load_raw(raw[u], 1 + u);
+    for (int u = 0; u < LEAD; u++)
+#pragma unroll
+        for (int pr = 0; pr < ROWP; pr++) load_raw(raw[u][pr], 1 + u, pr);
     mi_lds_barrier();
     stamp(1);
 
@@ -342,7 +353,7 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
     // static (slot u = sb % LEAD holds superblock sb + 1); fully unrolled when S is a template
     // constant (SCT), so no loop back-edge makes the compiler drain the ring.
     const int S_ = SCT > 0 ? SCT : S;
-    auto stage = [&](const int sb, Raw & rslot) {
+    auto stage = [&](const int sb, Raw (&rslot)[ROWP]) {
         stamp(2 + 4 * sb);
         const int cur = sb & 1;
         const char * base = lds + cur * kBuf;
@@ -361,7 +372,7 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
         // the dequantization of superblock sb + 1 (raw loaded LEAD stages ago) into the other LDS
         // buffer, one piece per 32-deep step, between this stage's MFMAs (the other buffer's
         // readers finished at the previous stage's barrier); then the slot's next load
-        Dq dq;
+        Dq dq[ROWP];
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) {
             i32x4 a[NP];
@@ -381,11 +392,14 @@ __global__ __launch_bounds__(512) void k_mmqx(const uint8_t * __restrict__ W, si
             }
             // step kk of the next superblock into the register just consumed
             xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kbn + (kk >> 1)) * xstep + 32 * (kk & 1), 0, 0));
-            if (kk == 0) dq_prep(dq, rslot);
-            if (kk >= 1 && kk <= 2 * NP) dq_piece(cur ^ 1, dq, kk - 1);
-            if (kk == 7) {
-                dq_rows(cur ^ 1, rslot);
-                load_raw(rslot, sb + 1 + LEAD);
+#pragma unroll
+            for (int pr = 0; pr < ROWP; pr++) {
+                if (kk == 0) dq_prep(dq[pr], rslot[pr]);
+                if (kk >= 1 && kk <= 2 * NP) dq_piece(cur ^ 1, dq[pr], kk - 1, pr);
+                if (kk == 7) {
+                    dq_rows(cur ^ 1, rslot[pr], pr);
+                    load_raw(rslot[pr], sb + 1 + LEAD, pr);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -857,7 +871,17 @@ void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N
 #undef MI_MMQDA
         return;
     }
-    const int64_t nrt = (N + XBM - 1) / XBM, nct = (act.ncols + XBN - 1) / XBN;
+    const int64_t nrt = (N + XBM - 1) / XBM;
+    // half-width workgroups (two per CU) when full-width tiles would leave CUs idle: Q4_K B=256
+    // 27.8 -> 26.4 us (B=512 41.7 vs 34.7 us: the per-workgroup dequantization then doubles)
+    const bool half = (var & 65536) || (type == 12 && nrt * ((act.ncols + XBN - 1) / XBN) < 256 && !(var & 131072));
+    if (half) {
+        const dim3 grid4((unsigned) (nrt * ((act.ncols + 63) / 64)));
+        if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, w, nb01, K, N, act, dst, ycol);
+        else hipLaunchKernelGGL((k_mmqx<13, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, w, nb01, K, N, act, dst, ycol);
+        return;
+    }
+    const int64_t nct = (act.ncols + XBN - 1) / XBN;
     const dim3 grid((unsigned) (nrt * nct));
     // weight ring depth LEAD (variant bits: 32 -> 2, 64 -> 1; default 4). (Fully unrolling the
     // stage loop for K = 4096, SCT = 16, spills: the compiler hoists loads across stages.)

@@ -12,6 +12,7 @@ lib = G.runtime()
 be = G.mi355x_backend(lib, 0)
 sp = lib.ggml_backend_mi355x_get_stream(be)
 Bs = [int(b) for b in sys.argv[1:]] or [512, 64]
+refs = {}
 VARS = [int(v) for v in os.environ.get("MMQ_VARIANTS", "0").split(",")]
 for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
     for B in Bs:
@@ -22,6 +23,10 @@ for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
         for _ in range(3):
             wl.step()
         ms = np.median([bench.event_time_per_step(torch, wl, sp, iters=5) for _ in range(3)])
-        print(f"{tname:5s} B={B:4d} var={var:4d}: {ms * 1e3 / 8:8.2f} us/mul_mat  {2 * 4096 * 4096 * B * 8 / (ms / 1e3) / 1e12:7.1f} TFLOP/s")
+        torch.cuda.synchronize()
+        y = G.tensor_get(lib, wl.y[0])
+        ref = refs.setdefault((tname, B), y)
+        same = "bit-equal to the first variant" if np.array_equal(y.view(np.uint32), ref.view(np.uint32)) else "DIFFERS from the first variant"
+        print(f"{tname:5s} B={B:4d} var={var:5d}: {ms * 1e3 / 8:8.2f} us/mul_mat  {2 * 4096 * 4096 * B * 8 / (ms / 1e3) / 1e12:7.1f} TFLOP/s  {same}")
         wl.free()
 lib.ggml_backend_free(be)
