@@ -146,6 +146,7 @@ mi_act_mmx mi_act_mmx_carve(void * base, int64_t K, int64_t ncols) {
 }
 
 void mi_quantize_q8_K_mmx(const mi_src_cols & x, int64_t K, const mi_act_mmx & act, hipStream_t s) {
+    if (act.ncols == 0 || K < 256) return;
     hipLaunchKernelGGL(k_quantize_q8_K_mmx, dim3((unsigned) act.ncols, (unsigned) ((K / 256 + 3) / 4)), dim3(256), 0, s, x, K, act);
 }
 

@@ -15,11 +15,13 @@
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
 
-static __device__ __forceinline__ const float * col_ptr(const mi_src_cols & x, int64_t c) {
-    const int64_t i1 = c % x.ne1;
-    const int64_t i2 = (c / x.ne1) % x.ne2;
-    const int64_t i3 = c / (x.ne1 * x.ne2);
-    return (const float *) (x.base + i1 * x.nb1 + i2 * x.nb2 + i3 * x.nb3);
+// column c of src1 (c = blockIdx.x in every kernel here: wave-uniform scalar arithmetic, and no
+// division at all for a plain 2-D src1)
+static __device__ __forceinline__ const float * col_ptr(const mi_src_cols & x, uint32_t c) {
+    if (x.ne2 == 1 && x.ne3 == 1) return (const float *) (x.base + (size_t) c * x.nb1);
+    const uint32_t ne1 = (uint32_t) x.ne1, ne2 = (uint32_t) x.ne2;
+    const uint32_t i1 = c % ne1, i2 = (c / ne1) % ne2, i3 = c / (ne1 * ne2);
+    return (const float *) (x.base + (size_t) i1 * x.nb1 + (size_t) i2 * x.nb2 + (size_t) i3 * x.nb3);
 }
 
 // f16 GEMM operand layouts: row-major [ncols][K], or K-blocked [K/16][ncols][16] (nblk > 0 =
@@ -48,18 +50,17 @@ mi_act_q8 mi_act_q8_carve(void * base, int64_t K, int64_t ncols, bool is_q8K) {
     return a;
 }
 
-// One 32-element block per half-wave, one element per lane. XH: write f16(d * q) to xh[c*K + k]
-// (the batched-prompt GEMM's operand, mmq.hip) instead of the q8 blocks.
+// One 32-element block per half-wave, one element per lane; grid (column, group of 8 blocks).
+// XH: write f16(d * q) to xh[c*K + k] (the batched-prompt GEMM's operand, mmq.hip) instead of the
+// q8 blocks.
 template <bool XH>
 __global__ __launch_bounds__(256) void k_quantize_q8_0(mi_src_cols x, int64_t K, mi_act_q8 act, uint16_t * xh,
-                                                       int64_t nblocks_total, int64_t xh_blk = 0) {
-    const int64_t gid = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t blk = gid >> 5;
-    const int l = threadIdx.x & 31;
-    if (blk >= nblocks_total) return;  // whole half-waves exit together (nblocks*32 threads)
+                                                       int64_t xh_blk = 0) {
     const int64_t nb_per_col = K / 32;
-    const int64_t c = blk / nb_per_col;
-    const int64_t b = blk % nb_per_col;
+    const int64_t b = (int64_t) blockIdx.y * 8 + (threadIdx.x >> 5);
+    const int l = threadIdx.x & 31;
+    if (b >= nb_per_col) return;  // whole half-waves exit together
+    const int64_t c = blockIdx.x;
     const float v = col_ptr(x, c)[b * 32 + l];
     float amax = fabsf(v);
 #pragma unroll
@@ -75,17 +76,17 @@ __global__ __launch_bounds__(256) void k_quantize_q8_0(mi_src_cols x, int64_t K,
     if (l == 0) act.d[c * nb_per_col + b] = mi_h2f(mi_f2h(d));
 }
 
-// One 256-element superblock per wave, four consecutive elements per lane (XH as for q8_0).
+// One 256-element superblock per wave, four consecutive elements per lane; grid (column, group of
+// 4 superblocks) (XH as for q8_0).
 template <bool XH>
 __global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K, mi_act_q8 act, uint16_t * xh,
-                                                       int64_t nblocks_total, int64_t xh_blk = 0) {
-    const int wave = threadIdx.x >> 6;
+                                                       int64_t xh_blk = 0) {
+    const int wave = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int64_t blk = (int64_t) blockIdx.x * 4 + wave;
-    if (blk >= nblocks_total) return;  // wave-uniform
     const int64_t nb_per_col = K / 256;
-    const int64_t c = blk / nb_per_col;
-    const int64_t b = blk % nb_per_col;
+    const int64_t b = (int64_t) blockIdx.y * 4 + wave;
+    if (b >= nb_per_col) return;  // wave-uniform
+    const int64_t c = blockIdx.x;
     const float4 v4 = *(const float4 *) (col_ptr(x, c) + b * 256 + lane * 4);
     const float v[4] = {v4.x, v4.y, v4.z, v4.w};
 
@@ -150,40 +151,42 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K,
     if (lane == 0) act.d[c * nb_per_col + b] = 1.0f / iscale;
 }
 
-__global__ __launch_bounds__(256) void k_convert_f16(mi_src_cols x, int64_t K, uint16_t * out, int64_t total, int64_t xh_blk) {
-    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    const int64_t c = i / K, k = i % K;
-    out[xh_index(c, k, K, xh_blk)] = mi_f2h(col_ptr(x, c)[k]);
+// grid (column, group of 256 elements)
+__global__ __launch_bounds__(256) void k_convert_f16(mi_src_cols x, int64_t K, uint16_t * out, int64_t xh_blk) {
+    const int64_t k = (int64_t) blockIdx.y * 256 + threadIdx.x;
+    if (k >= K) return;
+    const int64_t c = blockIdx.x;
+    out[xh_index(c, k, K, xh_blk)] = mi_f2h(col_ptr(x, (uint32_t) c)[k]);
 }
 
 void mi_quantize_q8_0(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s) {
-    const int64_t nblk = (K / 32) * act.ncols;
-    const int64_t threads = nblk * 32;
-    hipLaunchKernelGGL(k_quantize_q8_0<false>, dim3((unsigned) ((threads + 255) / 256)), dim3(256), 0, s, x, K, act, nullptr,
-                       nblk);
+    if (act.ncols == 0 || K < 32) return;
+    hipLaunchKernelGGL(k_quantize_q8_0<false>, dim3((unsigned) act.ncols, (unsigned) ((K / 32 + 7) / 8)), dim3(256), 0, s, x, K, act,
+                       nullptr);
 }
 
 void mi_quantize_q8_K(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s) {
-    const int64_t nblk = (K / 256) * act.ncols;
-    hipLaunchKernelGGL(k_quantize_q8_K<false>, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, act, nullptr, nblk);
+    if (act.ncols == 0 || K < 256) return;
+    hipLaunchKernelGGL(k_quantize_q8_K<false>, dim3((unsigned) act.ncols, (unsigned) ((K / 256 + 3) / 4)), dim3(256), 0, s, x, K, act,
+                       nullptr);
 }
 
 void mi_quantize_expand_f16(const mi_src_cols & x, int64_t K, int64_t ncols, bool is_q8K, uint16_t * xh, hipStream_t s,
                             bool blocked) {
     const int64_t xb = blocked ? ncols : 0;
+    if (ncols == 0 || K < 32) return;
     if (is_q8K) {
-        const int64_t nblk = (K / 256) * ncols;
-        hipLaunchKernelGGL(k_quantize_q8_K<true>, dim3((unsigned) ((nblk + 3) / 4)), dim3(256), 0, s, x, K, mi_act_q8{}, xh, nblk, xb);
+        hipLaunchKernelGGL(k_quantize_q8_K<true>, dim3((unsigned) ncols, (unsigned) ((K / 256 + 3) / 4)), dim3(256), 0, s, x, K,
+                           mi_act_q8{}, xh, xb);
     } else {
-        const int64_t nblk = (K / 32) * ncols;
-        hipLaunchKernelGGL(k_quantize_q8_0<true>, dim3((unsigned) ((nblk * 32 + 255) / 256)), dim3(256), 0, s, x, K, mi_act_q8{},
-                           xh, nblk, xb);
+        hipLaunchKernelGGL(k_quantize_q8_0<true>, dim3((unsigned) ncols, (unsigned) ((K / 32 + 7) / 8)), dim3(256), 0, s, x, K,
+                           mi_act_q8{}, xh, xb);
     }
 }
 
 void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s, bool blocked) {
-    const int64_t total = K * x.ne1 * x.ne2 * x.ne3;
-    const int64_t xb = blocked ? x.ne1 * x.ne2 * x.ne3 : 0;
-    hipLaunchKernelGGL(k_convert_f16, dim3((unsigned) ((total + 255) / 256)), dim3(256), 0, s, x, K, out, total, xb);
+    const int64_t ncols = x.ne1 * x.ne2 * x.ne3;
+    const int64_t xb = blocked ? ncols : 0;
+    if (ncols == 0 || K == 0) return;
+    hipLaunchKernelGGL(k_convert_f16, dim3((unsigned) ncols, (unsigned) ((K + 255) / 256)), dim3(256), 0, s, x, K, out, xb);
 }
