@@ -689,7 +689,9 @@ __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, si
 // per SIMD at S = 16: <= 128 VGPRs, so the 16 da of a lane's accumulator elements go through a
 // wave-private LDS row instead of registers. Same operands, same exact T / U and the same
 // canonical fold (terms left-folded in superblock order) as k_mmqd / k_mmqx: bit-identical.
-template <int TYPE>
+// ABL (timing ablations, results invalid): 1 no MFMAs, 2 one activation load reused, 4 no fold,
+// 8 weight header only
+template <int TYPE, int ABL = 0>
 __global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
                                                float * __restrict__ dst, size_t ycol) {
     using F = XFmt<TYPE>;
@@ -719,12 +721,12 @@ __global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, 
     const uint4 hdr = ld_w(0);
     uint4 q4[4];
 #pragma unroll
-    for (int p = 0; p < 4; p++) q4[p] = ld_w(kQs + 32 * p + 16 * h);
+    for (int p = 0; p < 4; p++) q4[p] = (ABL & 8) ? hdr : ld_w(kQs + 32 * p + 16 * h);
     const uint4 qh = F::Q5 ? ld_w(16 + 16 * h) : uint4{};
     i32x4 xa[8];
 #pragma unroll
     for (int kk = 0; kk < 8; kk++)
-        xa[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kk >> 1) * xstep + 32 * (kk & 1), 0, 0));
+        xa[kk] = ((ABL & 2) && kk) ? xa[0] : __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kk >> 1) * xstep + 32 * (kk & 1), 0, 0));
     const half8 xu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, ((uint32_t) sb * (uint32_t) ncols + acol) * 32 + 16 * h, 0, 0));
     // da of prompt column c0 + r (lanes >= 32 duplicate), parked in this wave's LDS row: columns
     // past ncols read a clamped column's value (never stored)
@@ -754,7 +756,8 @@ __global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, 
             uint32_t f = F::factor((int) sc, p);
             f |= f << 16;
             const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
-            acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[kk], b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
+            if constexpr ((ABL & 1) != 0) acc[p][kk] = (kk == 0 ? 0 : acc[p][kk]) + xa[kk][0] * b[0];
+            else acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[kk], b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
         }
     }
     half8 mu;
@@ -796,7 +799,7 @@ __global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, 
             y[4 * q] = t4.x; y[4 * q + 1] = t4.y; y[4 * q + 2] = t4.z; y[4 * q + 3] = t4.w;
         }
     }
-    for (int v = 1; v < S; v++) {
+    for (int v = 1; v < ((ABL & 4) ? 1 : S); v++) {
         const float * src = red + ((size_t) v * 64 + lane) * 16;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -837,6 +840,20 @@ void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N
         if (S <= 16 && !(var & 2048)) {  // one round: a wave per superblock (variant bit 2048: k_mmqd)
             const dim3 grid((unsigned) (nrt * nct));
             const size_t lds = (size_t) S * 64 * 16 * sizeof(float) + (size_t) S * 32 * sizeof(float);
+            const int abl = (var >> 12) & 15;
+            if (abl && type == 12) {  // timing ablations (results invalid)
+#define MI_MMQD1A(A) hipLaunchKernelGGL((k_mmqd1<12, A>), grid, dim3(64 * S), lds, s, w, nb01, K, N, act, dst, ycol)
+                switch (abl) {
+                case 1: MI_MMQD1A(1); break;
+                case 2: MI_MMQD1A(2); break;
+                case 4: MI_MMQD1A(4); break;
+                case 8: MI_MMQD1A(8); break;
+                case 10: MI_MMQD1A(10); break;
+                default: MI_MMQD1A(15); break;
+                }
+#undef MI_MMQD1A
+                return;
+            }
             if (type == 12) hipLaunchKernelGGL((k_mmqd1<12>), grid, dim3(64 * S), lds, s, w, nb01, K, N, act, dst, ycol);
             else hipLaunchKernelGGL((k_mmqd1<13>), grid, dim3(64 * S), lds, s, w, nb01, K, N, act, dst, ycol);
             return;

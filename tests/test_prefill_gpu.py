@@ -133,3 +133,28 @@ def test_prefill_edge_values(rt, backend):
     ref = orc.mul_mat(t, wq, K, N, np.ascontiguousarray(x).ravel(), B)
     assert np.all(np.isfinite(y))
     assert rel_err(y, ref) <= EXACT_TOL
+
+
+@pytest.mark.parametrize("tname", ["q4_K", "q5_K"])
+def test_prefill_kernels_bit_equal(rt, backend, tname):
+    """Every prefill kernel shares the canonical combine (exact T and U per superblock, terms
+    left-folded in superblock order), so any kernel choice gives the same bits: k_mmqd1 (the
+    default for <= 128 columns), k_mmqd (one and two rounds of weight lead, one and two
+    accumulator chains) and k_mmqx (full- and half-width workgroups)."""
+    t = orc.TYPES_BY_NAME[tname]
+    K, N, B = 4096, 320, 72
+    w = synth.uniform(11, K * N)
+    x = synth.uniform(12, K * B)
+    wq = orc.quantize(t, w, K)
+    variants = [0, 2048, 2048 | 256, 2048 | 512, 128 | 131072, 128 | 65536]
+    outs = {}
+    try:
+        for v in variants:
+            assert rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", v)
+            outs[v] = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
+    finally:
+        rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", 0)
+    ref = orc.mul_mat(t, wq, K, N, x, B)
+    assert rel_err(outs[0], ref) <= EXACT_TOL
+    for v in variants[1:]:
+        assert np.array_equal(outs[v].view(np.uint32), outs[0].view(np.uint32)), (v, rel_err(outs[v], outs[0]))
