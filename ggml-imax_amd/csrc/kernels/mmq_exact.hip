@@ -817,6 +817,129 @@ __global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, 
     }
 }
 
+// ---- very short prompts (<= 16 columns), K <= 4096: 16 x 16 tiles --------------------------------
+// k_mmqd1 on v_mfma_i32_16x16x64_i8: a 16-row x 16-column tile per workgroup (one wave per
+// superblock), so a 16-column prompt spreads over N / 16 workgroups (every CU at N = 4096) instead
+// of N / 32 with half of each 32-column tile idle. Lane (g = lane / 16, i = lane % 16): prompt
+// column / weight row i, K bytes 16 g .. 16 g + 15 of each 64-deep step (step t = sub-blocks 2t,
+// 2t + 1: Q4_K quant bytes 32 t + 16 (g & 1), low nibbles for g < 2, high for g >= 2). The
+// accumulator element e of a lane is prompt column 4 g + e, weight row i. Same exact T / U and
+// the same fold as every kernel of this file: bit-identical.
+template <int TYPE>
+__global__ __launch_bounds__(1024) void k_mmqd16(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
+                                                float * __restrict__ dst, size_t ycol) {
+    using F = XFmt<TYPE>;
+    constexpr int NP = F::NP;
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [wave][lane][4] terms, then [wave][16] da
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int64_t ncols = act.ncols;
+    const int S = (int) (K / 256);  // == waves of the workgroup
+    const int64_t nrt = (N + 15) / 16;
+    const int64_t n0 = (blockIdx.x % nrt) * 16, c0 = (blockIdx.x / nrt) * 16;
+    const int sb = w;
+
+    const int nrows = (int) std::min<int64_t>(16, N - n0);
+    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
+    const uint32_t wrow = (uint32_t) (min(i, nrows - 1) * nb01) + (uint32_t) sb * F::BS;
+    const uint32_t acol = (uint32_t) std::min<int64_t>(c0 + i, ncols - 1);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
+    const uint32_t xstep = (uint32_t) ncols * 64;
+    const uint32_t xcol = acol * 64 + 16 * g + (uint32_t) sb * 4 * xstep;
+    constexpr uint32_t kQs = F::Q5 ? 48 : 16;
+
+    auto ld_w = [&](uint32_t off) -> uint4 { return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wrow + off, 0, 0)); };
+    const uint4 hdr = ld_w(0);
+    uint4 q4[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) q4[t] = ld_w(kQs + 32 * t + 16 * (g & 1));
+    const uint4 qh = F::Q5 ? ld_w(16 + 16 * (g & 1)) : uint4{};
+    i32x4 xa[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) xa[t] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + t * xstep, 0, 0));
+    // U operand: sub-block halves of lanes g < 2 (g >= 2: zero K padding of the 16x16x32 MFMA)
+    half8 xu = {};
+    {
+        const half8 u = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, ((uint32_t) sb * (uint32_t) ncols + acol) * 32 + 16 * (g & 1), 0, 0));
+        if (g < 2) xu = u;
+    }
+    const float dal = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, ((uint32_t) sb * (uint32_t) ncols + acol) * 4, 0, 0));
+    float * dal_row = red + (size_t) S * 64 * 4 + w * 16;
+    if (g == 0) dal_row[i] = dal;
+    __builtin_amdgcn_wave_barrier();  // wave-private row: LDS ops of a wave complete in order
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+
+    const uint32_t w0 = hdr.y, w1 = hdr.z, w2 = hdr.w;
+    const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
+    const int hi = g >> 1;  // high nibbles: the odd sub-block of each step
+    i32x4 acc[NP];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int j = 2 * t + hi;  // this lane's sub-block (lane-dependent: no unrolled constant)
+        const int jj = j & 3;
+        const uint32_t sc = j < 4 ? ((w0 >> (8 * jj)) & 63) : (((w2 >> (8 * jj)) & 0xF) | (((w0 >> (8 * jj + 6)) & 3) << 4));
+        const uint4 q = q4[t];
+        uint32_t v[4] = {q.x, q.y, q.z, q.w};
+        const uint32_t hb[4] = {qh.x, qh.y, qh.z, qh.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            v[e] = (v[e] >> (4 * hi)) & 0x0F0F0F0Fu;
+            if constexpr (F::Q5) v[e] |= ((hb[e] >> j) & 0x01010101u) << 4;
+        }
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            uint32_t f = F::factor((int) sc, p);
+            f |= f << 16;
+            const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+            acc[p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[t], b, t == 0 ? i32x4{} : acc[p], 0, 0, 0);
+        }
+    }
+    half8 mu = {};
+    if (g < 2) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int j = 4 * g + q;  // K halves 8 g .. 8 g + 7: sub-blocks 4 g .. 4 g + 3
+            const int jj = j & 3;
+            const uint32_t m = j < 4 ? ((w1 >> (8 * jj)) & 63) : (((w2 >> (8 * jj + 4)) & 0xF) | (((w1 >> (8 * jj + 6)) & 3) << 4));
+            mu[2 * q] = (_Float16) (float) m;
+            mu[2 * q + 1] = (_Float16) (float) (64 * m);
+        }
+    }
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    const f32x4v Uv = __builtin_amdgcn_mfma_f32_16x16x32_f16(xu, mu, f32x4v{}, 0, 0, 0);
+    float * mine = red + ((size_t) w * 64 + lane) * 4;
+    {
+        const float4 d4 = *(const float4 *) (dal_row + 4 * g);
+        const float dav[4] = {d4.x, d4.y, d4.z, d4.w};
+        float term[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            int T = acc[NP - 1][e];
+#pragma unroll
+            for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][e];
+            term[e] = mmqx_term(T, Uv[e], dw, dm, dav[e]);
+        }
+        *(float4 *) mine = make_float4(term[0], term[1], term[2], term[3]);
+    }
+    mi_lds_barrier();
+    if (w != 0) return;
+    float4 y = *(const float4 *) (red + (size_t) lane * 4);
+    for (int v = 1; v < S; v++) {
+        const float4 t4 = *(const float4 *) (red + ((size_t) v * 64 + lane) * 4);
+        y.x = y.x + t4.x; y.y = y.y + t4.y; y.z = y.z + t4.z; y.w = y.w + t4.w;
+    }
+    const int64_t n = n0 + i;
+    if (n >= N) return;
+    const float yv[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const int64_t c = c0 + 4 * g + e;
+        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = yv[e];
+    }
+}
+
 } // namespace
 
 bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t nb01) {
@@ -837,6 +960,14 @@ void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N
     if (direct) {
         const int64_t nrt = (N + 31) / 32, nct = (act.ncols + 31) / 32;
         const int S = (int) (K / 256);
+        const int64_t lim16 = (var & (1 << 22)) ? 128 : 16;  // bit 2^22: 16 x 16 tiles up to 128 columns
+        if (S <= 16 && act.ncols <= lim16 && !(var & (2048 | 4096 | (1 << 21)))) {  // 16 x 16 tiles (bit 2^21: k_mmqd1)
+            const dim3 grid16((unsigned) (((N + 15) / 16) * ((act.ncols + 15) / 16)));
+            const size_t lds16 = (size_t) S * 64 * 4 * sizeof(float) + (size_t) S * 16 * sizeof(float);
+            if (type == 12) hipLaunchKernelGGL((k_mmqd16<12>), grid16, dim3(64 * S), lds16, s, w, nb01, K, N, act, dst, ycol);
+            else hipLaunchKernelGGL((k_mmqd16<13>), grid16, dim3(64 * S), lds16, s, w, nb01, K, N, act, dst, ycol);
+            return;
+        }
         if (S <= 16 && !(var & 2048)) {  // one round: a wave per superblock (variant bit 2048: k_mmqd)
             const dim3 grid((unsigned) (nrt * nct));
             const size_t lds = (size_t) S * 64 * 16 * sizeof(float) + (size_t) S * 32 * sizeof(float);

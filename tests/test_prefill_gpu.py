@@ -136,17 +136,19 @@ def test_prefill_edge_values(rt, backend):
 
 
 @pytest.mark.parametrize("tname", ["q4_K", "q5_K"])
-def test_prefill_kernels_bit_equal(rt, backend, tname):
+@pytest.mark.parametrize("B", [72, 13])
+def test_prefill_kernels_bit_equal(rt, backend, tname, B):
     """Every prefill kernel shares the canonical combine (exact T and U per superblock, terms
     left-folded in superblock order), so any kernel choice gives the same bits: k_mmqd1 (the
     default for <= 128 columns), k_mmqd (one and two rounds of weight lead, one and two
-    accumulator chains) and k_mmqx (full- and half-width workgroups)."""
+    accumulator chains), k_mmqx (full- and half-width workgroups) and, for <= 16 columns,
+    k_mmqd16 (the default there; 16 x 16 tiles on the 16x16x64 MFMA)."""
     t = orc.TYPES_BY_NAME[tname]
-    K, N, B = 4096, 320, 72
+    K, N = 4096, 320
     w = synth.uniform(11, K * N)
     x = synth.uniform(12, K * B)
     wq = orc.quantize(t, w, K)
-    variants = [0, 2048, 2048 | 256, 2048 | 512, 128 | 131072, 128 | 65536]
+    variants = [0, 2048, 2048 | 256, 2048 | 512, 128 | 131072, 128 | 65536] + ([1 << 21] if B <= 16 else [])
     outs = {}
     try:
         for v in variants:
