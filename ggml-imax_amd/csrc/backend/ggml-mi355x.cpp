@@ -427,11 +427,29 @@ struct mi_backend_ctx {
     int last_launches = 0;
     uint16_t * tables = nullptr;  // device: exp, gelu, silu fp16 tables (3 x 65536)
     hipEvent_t split_ready = nullptr;  // src1 of a split mul_mat is ready on `stream`
+    uint64_t scratch_gen = 0;     // bumped whenever `scratch` is reallocated (captures refer to it)
     // hipGraph plans (mi_graph_plan_create): captured launches of a whole ggml graph
     bool graphs = true;
     std::vector<hipGraphExec_t> exec_pool;  // executable graphs of freed plans, for in-place update
     int graph_fail_streak = 0;         // consecutive re-instantiations (update refused)
-    int64_t graph_stats[4] = {};       // captures, instantiations, updates, direct computes
+    // counters: [0] captures (plans and graph_compute), [1] instantiations, [2] in-place updates,
+    // [3] direct (uncaptured) computes, [4] graph_compute replays of a cached capture,
+    // [5] graph_compute captures
+    int64_t graph_stats[6] = {};
+    // graph_compute's own captures (ggml-cuda.cu:2456-2713 analogue): executable graphs keyed by
+    // the exact launch-relevant content of the cgraph (mi_graph_key); an entry whose topology
+    // matches a new graph is updated in place (hipGraphExecUpdate) before a new one is built
+    struct gcache_entry {
+        std::vector<uint64_t> key;
+        uint64_t topo = 0;
+        hipGraphExec_t exec = nullptr;
+        hipEvent_t done = nullptr;  // recorded behind every launch of `exec`
+        uint64_t last_use = 0;
+        int launches = 0;
+    };
+    std::vector<gcache_entry> gcache;
+    uint64_t gclock = 0;
+    std::unordered_map<uint64_t, int> topo_launches;  // kernel launches of a topology's last direct run
     // host-built RoPE {cos, sin} tables (rope_table_ensure), one per parameter set
     struct rope_table {
         int n_dims, ne0, mode, P;
@@ -472,6 +490,7 @@ static void scratch_reserve(mi_backend_ctx * ctx, size_t bytes) {
     const size_t want = std::max(bytes + bytes / 2, (size_t) 16 << 20);
     MI_CHECK(hipMalloc(&ctx->scratch, want));
     ctx->scratch_size = want;
+    ctx->scratch_gen++;  // executable graphs captured against the old buffer must not run again
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -652,8 +671,9 @@ static int mm_act_kind(const mi_mm_desc & m, const ggml_tensor * src1) {
     if (kind < 0) return -1;
     if (!mm_batched(m, src1)) return kind;
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
-    // GGML_MI355X_MMQ_VARIANT bit 32 selects the f16 GEMM for K-quants too (A/B timing)
-    if (kind == 1 && (g_mi_tuning.mmq_variant & 32) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01)) return 8;
+    // GGML_MI355X_MMQ_VARIANT bit 2^30 selects the f16 GEMM for K-quants too (A/B timing; the low
+    // bits are mmq_exact.hip's own kernel variants)
+    if (kind == 1 && (g_mi_tuning.mmq_variant & (1 << 30)) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01)) return 8;
     return (kind == 2 ? 2 : kind + 3) + (mi_mmq_wants_blocked() ? 3 : 0);
 }
 
@@ -1083,9 +1103,10 @@ static size_t graph_scratch_bytes(const ggml_cgraph * cgraph) {
     for (int i = 0; i < cgraph->n_nodes; i++) {
         const ggml_tensor * n = cgraph->nodes[i];
         if (n->op != GGML_OP_MUL_MAT) continue;
-        if (n->src[0]->type == GGML_TYPE_F16 && n->src[1]->op == GGML_OP_CONT && n->src[1]->ne[1] == 1) {
-            // an attention output projection: room for its per-head partial sums (try_fuse_attn_proj;
-            // head dim >= 64, so at most K / 64 heads)
+        if (n->src[0]->type == GGML_TYPE_F16 && n->src[1]->ne[1] == 1) {
+            // a possible attention output projection (whatever op merged the heads -- ggml_cont as
+            // main-backend.cpp:603 or ggml_cpy as main-ctx.cpp:566): room for its per-head partial
+            // sums (try_fuse_attn_proj; head dim >= 64, so at most K / 64 heads)
             total += ((size_t) (n->src[0]->ne[0] / 64) * n->src[0]->ne[1] * sizeof(float) + kBufferAlign - 1) & ~(kBufferAlign - 1);
         }
         const int kind = act_kind(n->src[0]->type);
@@ -1784,13 +1805,196 @@ static int try_fuse_copies(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
 
 static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph * cgraph);
 
-// graph_compute: every kernel launched directly (the device starts on the first one while the
-// host still launches the rest)
+static bool graphs_enabled(const mi_backend_ctx * ctx) {
+    static const bool env_no_graphs = getenv("GGML_MI355X_DISABLE_GRAPHS") != nullptr;
+    return ctx->graphs && !env_no_graphs;
+}
+
+// a graph that can be captured: no split-buffer mul_mat (several streams, events, peer copies)
+static bool graph_capturable(const ggml_cgraph * cgraph) {
+    for (int i = 0; i < cgraph->n_nodes; i++) {
+        const ggml_tensor * n = cgraph->nodes[i];
+        if (n->op == GGML_OP_MUL_MAT && is_split_tensor(n->src[0])) return false;
+    }
+    return true;
+}
+
+// Everything the node pass does synchronously -- table uploads, scratch growth -- done up front,
+// so that a capture of the pass only enqueues kernels on ctx->stream. Scratch: the pass's own
+// estimate plus room for the attention planner's Q copies (at most every CONT node's bytes).
+static void prepare_for_capture(mi_backend_ctx * ctx, const ggml_cgraph * cgraph) {
+    op_tables(ctx);
+    rope_tables_prepare(ctx, cgraph);
+    size_t cont_bytes = 0;
+    for (int i = 0; i < cgraph->n_nodes; i++) {
+        if (cgraph->nodes[i]->op == GGML_OP_CONT) cont_bytes += (ggml_nbytes(cgraph->nodes[i]) + kBufferAlign - 1) & ~(kBufferAlign - 1);
+    }
+    scratch_reserve(ctx, graph_scratch_bytes(cgraph) + cont_bytes);
+}
+
+// Captures the node pass of `cgraph` into a hipGraph (nullptr if something in it could not be
+// captured; the backend then launches directly from now on). The stream may still be running
+// earlier work: the capture records only what follows.
+static hipGraph_t capture_pass(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
+    MI_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    const ggml_status st = mi_graph_launch_nodes(ctx, cgraph);
+    hipGraph_t graph = nullptr;
+    const hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    if (st != GGML_STATUS_SUCCESS || ec != hipSuccess || !graph) {
+        (void) hipGetLastError();
+        if (graph) (void) hipGraphDestroy(graph);
+        ctx->graphs = false;
+        return nullptr;
+    }
+    ctx->graph_stats[0]++;
+    return graph;
+}
+
+// The exact launch-relevant content of a graph: per node its output address, op, type, shape,
+// strides, op_params, view source and every source's address, type, shape and strides; plus the
+// scratch buffer the captured kernels use and the tuning knobs that choose kernels. Two graphs
+// with equal keys launch identical kernels with identical arguments.
+static void graph_key(const mi_backend_ctx * ctx, const ggml_cgraph * g, std::vector<uint64_t> & k) {
+    k.clear();
+    k.reserve((size_t) g->n_nodes * 40 + 16);
+    k.push_back((uint64_t) g->n_nodes);
+    k.push_back((uint64_t) (g->size == 0 && g->visited_hash_table.size == 0));  // mi_uses::partial
+    k.push_back((uint64_t) (uintptr_t) ctx->scratch);
+    k.push_back(ctx->scratch_gen);
+    {
+        uint64_t tw[(sizeof(mi_tuning) + 7) / 8] = {};
+        memcpy(tw, &g_mi_tuning, sizeof(mi_tuning));
+        for (uint64_t w : tw) k.push_back(w);
+    }
+    auto tensor = [&](const ggml_tensor * t) {
+        k.push_back((uint64_t) (uintptr_t) t->data);
+        k.push_back((uint64_t) t->type | ((uint64_t) t->op << 16));
+        for (int d = 0; d < 4; d++) k.push_back((uint64_t) t->ne[d]);
+        for (int d = 0; d < 4; d++) k.push_back((uint64_t) t->nb[d]);
+    };
+    for (int i = 0; i < g->n_nodes; i++) {
+        const ggml_tensor * t = g->nodes[i];
+        tensor(t);
+        k.push_back((uint64_t) (uintptr_t) t->view_src);
+        uint64_t pw[GGML_MAX_OP_PARAMS / 8];
+        memcpy(pw, t->op_params, sizeof(pw));
+        for (uint64_t w : pw) k.push_back(w);
+        int ns = 0;
+        for (int j = 0; j < GGML_MAX_SRC; j++) if (t->src[j]) ns = j + 1;
+        k.push_back((uint64_t) ns);
+        for (int j = 0; j < ns; j++) {
+            if (t->src[j]) tensor(t->src[j]);
+            else k.push_back(0);
+        }
+    }
+}
+
+// topology of a graph (ops, types, source counts): graphs that differ only in addresses, shapes
+// or parameters -- a decode step at the next position -- share it, so the executable graph of one
+// can be updated in place for the other
+static uint64_t graph_topology(const ggml_cgraph * g) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+    mix((uint64_t) g->n_nodes);
+    for (int i = 0; i < g->n_nodes; i++) {
+        const ggml_tensor * t = g->nodes[i];
+        int ns = 0;
+        for (int j = 0; j < GGML_MAX_SRC; j++) if (t->src[j]) ns = j + 1;
+        mix((uint64_t) t->op | ((uint64_t) t->type << 8) | ((uint64_t) ns << 16) | ((uint64_t) (t->view_src != nullptr) << 24));
+    }
+    return h;
+}
+
+// captures below this many kernel launches are not worth a replay (one small graph launches
+// faster directly than through hipGraphLaunch); GGML_MI355X_GRAPH_MIN_LAUNCHES overrides
+static int graph_min_launches() {
+    static const int v = getenv("GGML_MI355X_GRAPH_MIN_LAUNCHES") ? atoi(getenv("GGML_MI355X_GRAPH_MIN_LAUNCHES")) : 4;
+    return v;
+}
+
+static constexpr size_t kGraphCacheEntries = 8;
+
+static void gcache_launch(mi_backend_ctx * ctx, mi_backend_ctx::gcache_entry & e) {
+    MI_CHECK(hipGraphLaunch(e.exec, ctx->stream));
+    MI_CHECK(hipEventRecord(e.done, ctx->stream));
+    e.last_use = ++ctx->gclock;
+    ctx->last_launches = e.launches;
+}
+
+// graph_compute (ggml-cuda.cu:2456-2713 analogue: capture at :2576, exec update at :2690, the
+// GGML_CUDA_DISABLE_GRAPHS switch at :2462). A graph whose exact content (graph_key) was captured
+// before is replayed with one hipGraphLaunch. Otherwise: the first graph of a topology runs
+// directly (its launch count decides whether capturing it pays); a later one is captured, an
+// executable graph of the same topology is updated in place when only kernel arguments changed,
+// else a new one is instantiated (at most kGraphCacheEntries per backend, least recently used
+// evicted). Anything that cannot be captured runs directly.
 static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * cgraph) {
     auto * ctx = (mi_backend_ctx *) backend->context;
     mi_device_guard g(ctx->device);
-    ctx->graph_stats[3]++;
-    return mi_graph_launch_nodes(ctx, cgraph);
+    if (!graphs_enabled(ctx) || !graph_capturable(cgraph)) {
+        ctx->graph_stats[3]++;
+        return mi_graph_launch_nodes(ctx, cgraph);
+    }
+    prepare_for_capture(ctx, cgraph);
+    static thread_local std::vector<uint64_t> key;
+    graph_key(ctx, cgraph, key);
+    for (auto & e : ctx->gcache) {
+        if (e.key == key) {
+            ctx->graph_stats[4]++;
+            gcache_launch(ctx, e);
+            return GGML_STATUS_SUCCESS;
+        }
+    }
+    const uint64_t topo = graph_topology(cgraph);
+    auto seen = ctx->topo_launches.find(topo);
+    if (seen == ctx->topo_launches.end() || seen->second < graph_min_launches()) {
+        ctx->graph_stats[3]++;
+        const ggml_status st = mi_graph_launch_nodes(ctx, cgraph);
+        ctx->topo_launches[topo] = ctx->last_launches;
+        return st;
+    }
+    hipGraph_t graph = capture_pass(ctx, cgraph);
+    if (!graph) {
+        ctx->graph_stats[3]++;
+        return mi_graph_launch_nodes(ctx, cgraph);
+    }
+    ctx->graph_stats[5]++;
+    const int launches = ctx->last_launches;
+    mi_backend_ctx::gcache_entry * slot = nullptr;
+    for (auto & e : ctx->gcache) {
+        if (e.topo != topo) continue;
+        MI_CHECK(hipEventSynchronize(e.done));  // never update an executable graph still in flight
+        hipGraphNode_t err_node = nullptr;
+        hipGraphExecUpdateResult res;
+        if (hipGraphExecUpdate(e.exec, graph, &err_node, &res) == hipSuccess && res == hipGraphExecUpdateSuccess) {
+            ctx->graph_stats[2]++;
+            slot = &e;
+        } else {
+            (void) hipGetLastError();
+        }
+        break;
+    }
+    if (!slot) {
+        if (ctx->gcache.size() >= kGraphCacheEntries) {
+            auto lru = std::min_element(ctx->gcache.begin(), ctx->gcache.end(),
+                                        [](const auto & a, const auto & b) { return a.last_use < b.last_use; });
+            MI_CHECK(hipEventSynchronize(lru->done));
+            MI_CHECK(hipGraphExecDestroy(lru->exec));
+            MI_CHECK(hipEventDestroy(lru->done));
+            ctx->gcache.erase(lru);
+        }
+        ctx->gcache.emplace_back();
+        slot = &ctx->gcache.back();
+        MI_CHECK(hipGraphInstantiate(&slot->exec, graph, nullptr, nullptr, 0));
+        MI_CHECK(hipEventCreateWithFlags(&slot->done, hipEventDisableTiming));
+        ctx->graph_stats[1]++;
+    }
+    MI_CHECK(hipGraphDestroy(graph));
+    slot->key = key;
+    slot->topo = topo;
+    slot->launches = launches;
+    gcache_launch(ctx, *slot);
+    return GGML_STATUS_SUCCESS;
 }
 
 // Graph plans (ggml_backend_graph_plan_create / _compute, ggml-backend.h): a plan is the graph's
@@ -1799,11 +2003,12 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
 // whose next graph depends on positions only -- creates the plan while the device still runs the
 // current one. Executable graphs are pooled per backend: a new plan updates a pooled one in place
 // (hipGraphExecUpdate) when only kernel arguments changed (KV length, cache offsets), and
-// instantiates otherwise. ggml-cuda.cu:2456-2713 is the reference's CUDA-graph analogue (there
-// captured inside graph_compute).
+// instantiates otherwise.
 struct mi_graph_plan {
     ggml_cgraph graph;              // the caller's graph (node arrays stay the caller's)
     hipGraphExec_t exec = nullptr;  // null: launched directly at compute time
+    uint64_t scratch_gen = 0;       // the scratch buffer generation the capture refers to
+    int launches = 0;
 };
 
 // consecutive refused updates after which a backend stops capturing (as ggml-cuda.cu's
@@ -1815,36 +2020,12 @@ static ggml_backend_graph_plan_t mi_graph_plan_create(ggml_backend_t backend, co
     mi_device_guard g(ctx->device);
     auto * plan = new mi_graph_plan();
     plan->graph = *cgraph;
-    static const bool env_no_graphs = getenv("GGML_MI355X_DISABLE_GRAPHS") != nullptr;
-    bool capture = ctx->graphs && !env_no_graphs;
-    for (int i = 0; capture && i < cgraph->n_nodes; i++) {
-        const ggml_tensor * n = cgraph->nodes[i];
-        if (n->op == GGML_OP_MUL_MAT && is_split_tensor(n->src[0])) capture = false;  // multi-stream, events
-    }
-    if (!capture) return plan;
-    // everything that allocates or copies synchronously happens before the capture: the node
-    // pass below then only enqueues kernels on ctx->stream. Scratch: the pass's own estimate plus
-    // room for the attention planner's Q copies (at most every CONT node's bytes)
-    op_tables(ctx);
-    rope_tables_prepare(ctx, cgraph);
-    size_t cont_bytes = 0;
-    for (int i = 0; i < cgraph->n_nodes; i++) {
-        if (cgraph->nodes[i]->op == GGML_OP_CONT) cont_bytes += (ggml_nbytes(cgraph->nodes[i]) + kBufferAlign - 1) & ~(kBufferAlign - 1);
-    }
-    scratch_reserve(ctx, graph_scratch_bytes(cgraph) + cont_bytes);
-    // the stream may still be running earlier work: the capture records only what follows
-    MI_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-    const ggml_status st = mi_graph_launch_nodes(ctx, &plan->graph);
-    hipGraph_t graph = nullptr;
-    const hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
-    if (st != GGML_STATUS_SUCCESS || ec != hipSuccess || !graph) {
-        // something in the pass could not be captured: this backend launches directly from now on
-        (void) hipGetLastError();
-        if (graph) (void) hipGraphDestroy(graph);
-        ctx->graphs = false;
-        return plan;
-    }
-    ctx->graph_stats[0]++;
+    if (!graphs_enabled(ctx) || !graph_capturable(cgraph)) return plan;
+    prepare_for_capture(ctx, cgraph);
+    hipGraph_t graph = capture_pass(ctx, &plan->graph);
+    if (!graph) return plan;
+    plan->scratch_gen = ctx->scratch_gen;
+    plan->launches = ctx->last_launches;
     while (!ctx->exec_pool.empty() && !plan->exec) {
         hipGraphExec_t ex = ctx->exec_pool.back();
         ctx->exec_pool.pop_back();
@@ -1884,11 +2065,14 @@ static enum ggml_status mi_graph_plan_compute(ggml_backend_t backend, ggml_backe
     auto * ctx = (mi_backend_ctx *) backend->context;
     auto * plan = (mi_graph_plan *) p;
     mi_device_guard g(ctx->device);
-    if (!plan->exec) {
+    // a plan captured against a scratch buffer that has since been reallocated (a later, larger
+    // graph) would launch on freed memory: such a plan runs its nodes directly
+    if (!plan->exec || plan->scratch_gen != ctx->scratch_gen) {
         ctx->graph_stats[3]++;
         return mi_graph_launch_nodes(ctx, &plan->graph);
     }
     MI_CHECK(hipGraphLaunch(plan->exec, ctx->stream));
+    ctx->last_launches = plan->launches;
     return GGML_STATUS_SUCCESS;
 }
 
@@ -2026,6 +2210,10 @@ static void mi_backend_free(ggml_backend_t backend) {
         mi_device_guard g(ctx->device);
         MI_CHECK(hipStreamSynchronize(ctx->stream));
         for (hipGraphExec_t ex : ctx->exec_pool) MI_CHECK(hipGraphExecDestroy(ex));
+        for (auto & e : ctx->gcache) {
+            MI_CHECK(hipGraphExecDestroy(e.exec));
+            MI_CHECK(hipEventDestroy(e.done));
+        }
         if (ctx->scratch) MI_CHECK(hipFree(ctx->scratch));
         if (ctx->tables) MI_CHECK(hipFree(ctx->tables));
         for (auto & t : ctx->rope_tables) MI_CHECK(hipFree(t.dev));
@@ -2266,9 +2454,15 @@ void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable) 
 }
 
 void ggml_backend_mi355x_graph_stats(ggml_backend_t backend, int64_t * stats4) {
+    ggml_backend_mi355x_graph_stats_ex(backend, stats4, 4);
+}
+
+int ggml_backend_mi355x_graph_stats_ex(ggml_backend_t backend, int64_t * stats, int n) {
     MI_ASSERT(ggml_backend_is_mi355x(backend));
     const auto * ctx = (const mi_backend_ctx *) backend->context;
-    for (int i = 0; i < 4; i++) stats4[i] = ctx->graph_stats[i];
+    const int m = std::min(n, (int) (sizeof(ctx->graph_stats) / sizeof(ctx->graph_stats[0])));
+    for (int i = 0; i < m; i++) stats[i] = ctx->graph_stats[i];
+    return m;
 }
 
 bool ggml_backend_mi355x_set_tuning(const char * name, int value) {

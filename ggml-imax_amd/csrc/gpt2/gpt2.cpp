@@ -79,6 +79,8 @@ struct gpt2_model {
     std::vector<ggml_backend_buffer_t> buffers_w;
     ggml_backend_buffer_t buffer_input = nullptr;
     ggml_context * ctx_in = nullptr;
+    ggml_backend_buffer_t buffer_pos = nullptr;  // host_io: the constant positions, device-resident
+    ggml_context * ctx_pos = nullptr;
     ggml_tensor * embd_in = nullptr, * pos_in = nullptr;  // persistent input tensors
     void * sched = nullptr;                     // ggml_backend_sched_t
     int n_gpu_layers = 0;
@@ -315,7 +317,7 @@ ggml_cgraph * build_graph(gpt2_model & m, int n_past, int N, int slot = 0) {
 
     ggml_tensor * embd, * position;
     if (m.host_io) {
-        // host-resident inputs: pos_in holds 0 .. n_ctx - 1 for good, so a graph's positions are a
+        // pinned host token ids read in place; pos_in (device) holds 0 .. n_ctx - 1 for good, so a graph's positions are a
         // view at n_past and only the token ids change per eval
         embd = ggml_view_1d(ctx, m.embd_in, N, 0);
         position = ggml_view_1d(ctx, m.pos_in, N, (size_t) n_past * sizeof(int32_t));
@@ -437,15 +439,20 @@ gpt2_model * gpt2_model_load_ex(const char * fname, ggml_backend_t backend, int 
         ggml_init_params ip = {ggml_tensor_overhead() * 3, nullptr, true};
         m->ctx_in = ggml_init(ip);
         m->embd_in = ggml_new_tensor_1d(m->ctx_in, GGML_TYPE_I32, m->hp.n_ctx);
-        m->pos_in = ggml_new_tensor_1d(m->ctx_in, GGML_TYPE_I32, m->hp.n_ctx);
         m->logits_host = ggml_new_tensor_2d(m->ctx_in, GGML_TYPE_F32, m->hp.n_vocab, n_tokens);
+        // positions never change (0 .. n_ctx - 1, a graph views its slice): they live on the
+        // device, so a decode step's only host read is its token id
+        m->ctx_pos = ggml_init(ip);
+        m->pos_in = ggml_new_tensor_1d(m->ctx_pos, GGML_TYPE_I32, m->hp.n_ctx);
+        m->buffer_pos = ggml_backend_alloc_ctx_tensors(m->ctx_pos, backend);
         ggml_set_name(m->embd_in, "in/embd");
         ggml_set_name(m->pos_in, "in/position");
         ggml_set_name(m->logits_host, "out/logits");
         m->buffer_input = ggml_backend_alloc_ctx_tensors_from_buft(m->ctx_in, host_buft);
         // the device reads these in place: a buffer the type fell back to (e.g. pageable memory,
         // another buffer type) will not do
-        if (!m->buffer_input || m->buffer_input->buft != host_buft || !ggml_backend_buffer_is_host(m->buffer_input)) {
+        if (!m->buffer_input || m->buffer_input->buft != host_buft || !ggml_backend_buffer_is_host(m->buffer_input) ||
+            !m->buffer_pos) {
             fprintf(stderr, "gpt2_model_load: host input buffer allocation failed (or not a host buffer type)\n");
             gpt2_model_free(m);
             return nullptr;
@@ -541,6 +548,8 @@ void gpt2_model_free(gpt2_model * m) {
 #endif
     if (m->buffer_input) ggml_backend_buffer_free(m->buffer_input);
     if (m->ctx_in) ggml_free(m->ctx_in);
+    if (m->buffer_pos) ggml_backend_buffer_free(m->buffer_pos);
+    if (m->ctx_pos) ggml_free(m->ctx_pos);
     for (ggml_backend_buffer_t b : m->buffers_w) if (b) ggml_backend_buffer_free(b);
     if (m->allocr) ggml_gallocr_free(m->allocr);
     if (m->buffer_w) ggml_backend_buffer_free(m->buffer_w);
@@ -601,17 +610,18 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
     if (m->next_gf && m->next_n_past == n_past && N == 1) {
         // built and allocated while the device ran the previous token (graph_slot ^ 1)
         gf = m->next_gf;
-        plan = m->next_plan;
+        plan = m->next_plan;  // owned here from now on: freed once its graph has run
+        m->next_plan = nullptr;
         m->graph_slot ^= 1;
         t1 = t1b = t0;
     } else {
         if (m->next_plan) ggml_backend_graph_plan_free(m->backend, m->next_plan);
+        m->next_plan = nullptr;
         m->graph_slot ^= 1;
         gf = build_graph(*m, n_past, N, m->graph_slot);
         t1 = now_us();
         if (!ggml_gallocr_alloc_graph(m->allocr, gf)) {
             m->next_gf = nullptr;
-    m->next_plan = nullptr;
             fprintf(stderr, "gpt2_eval: graph allocation failed\n");
             return 1;
         }

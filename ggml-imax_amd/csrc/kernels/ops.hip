@@ -199,15 +199,20 @@ __device__ __forceinline__ float emb_elem(const mi_tensor_desc & a, int32_t r, i
     else return dequant_elem<T>((const uint8_t *) a.data + (size_t) r * a.nb[1], c);
 }
 
+// grid (column chunks, rows). Both indices are read once per thread before any gather, the
+// position index first: in a decode step the token id may sit in pinned host memory (a PCIe round
+// trip) while the position table is device-resident, so the position row's loads issue while the
+// id is still in flight (vmcnt retires in issue order).
 template <int TA, int TB>
 __global__ __launch_bounds__(256) void k_get_rows_add(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc ia, mi_tensor_desc b,
-                                                      mi_tensor_desc ib, int64_t n) {
-    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
-        const int64_t c = i % d.ne[0], r = i / d.ne[0];
-        const int32_t ra = *(const int32_t *) (ia.data + r * ia.nb[0]);
-        const int32_t rb = *(const int32_t *) (ib.data + r * ib.nb[0]);
-        const float va = emb_elem<TA>(a, ra, c), vb = emb_elem<TB>(b, rb, c);
-        *(float *) (d.data + c * d.nb[0] + r * d.nb[1]) = va + vb;
+                                                      mi_tensor_desc ib, int ne0) {
+    const int r = (int) blockIdx.y;
+    const int32_t rb = *(const int32_t *) (ib.data + (size_t) r * ib.nb[0]);
+    const int32_t ra = *(const int32_t *) (ia.data + (size_t) r * ia.nb[0]);
+    for (int c = (int) (blockIdx.x * blockDim.x + threadIdx.x); c < ne0; c += (int) (gridDim.x * blockDim.x)) {
+        const float vb = emb_elem<TB>(b, rb, c);
+        const float va = emb_elem<TA>(a, ra, c);
+        *(float *) (d.data + (size_t) c * d.nb[0] + (size_t) r * d.nb[1]) = va + vb;
     }
 }
 
@@ -453,13 +458,16 @@ void mi_op_get_rows(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi
 template <int TA>
 static void launch_get_rows_add(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & ia, const mi_tensor_desc & b,
                                 const mi_tensor_desc & ib, int64_t n, hipStream_t s) {
-    const dim3 g(grid_for(n));
+    (void) n;
+    if (d.ne[1] > 65535 || d.ne[0] >= ((int64_t) 1 << 31)) abort();
+    const int ne0 = (int) d.ne[0];
+    const dim3 g((unsigned) std::min<int64_t>((ne0 + 1023) / 1024, 64), (unsigned) d.ne[1]);
     switch (b.type) {
-        case 2: hipLaunchKernelGGL((k_get_rows_add<TA, 2>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
-        case 8: hipLaunchKernelGGL((k_get_rows_add<TA, 8>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
-        case 12: hipLaunchKernelGGL((k_get_rows_add<TA, 12>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
-        case 13: hipLaunchKernelGGL((k_get_rows_add<TA, 13>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
-        default: hipLaunchKernelGGL((k_get_rows_add<TA, 0>), g, dim3(256), 0, s, d, a, ia, b, ib, n); break;
+        case 2: hipLaunchKernelGGL((k_get_rows_add<TA, 2>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
+        case 8: hipLaunchKernelGGL((k_get_rows_add<TA, 8>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
+        case 12: hipLaunchKernelGGL((k_get_rows_add<TA, 12>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
+        case 13: hipLaunchKernelGGL((k_get_rows_add<TA, 13>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
+        default: hipLaunchKernelGGL((k_get_rows_add<TA, 0>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
     }
 }
 

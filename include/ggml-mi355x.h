@@ -54,15 +54,21 @@ GGML_API void * ggml_backend_mi355x_get_stream(ggml_backend_t backend);
 // Number of kernels launched by the last graph_compute (for tests / profiling).
 GGML_API int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend);
 
-// Graph plans (ggml_backend_graph_plan_create / _compute) are hipGraphs: the plan's launches
-// are captured at creation (updating a pooled executable graph in place when only kernel
-// arguments changed) and computing it is one hipGraphLaunch. graph_compute launches directly.
-// GGML_MI355X_DISABLE_GRAPHS=1 (process-wide, as GGML_CUDA_DISABLE_GRAPHS, ggml-cuda.cu:2462) or
-// set_graph_capture(false) makes plans launch directly too.
+// hipGraphs. graph_compute captures a graph's launches and replays the capture whenever the same
+// graph (same nodes, addresses, shapes, parameters) is computed again, updating an executable
+// graph of the same topology in place when only kernel arguments changed (the reference's CUDA
+// graphs, ggml-cuda.cu:2456-2713); the first graph of a topology, and graphs of fewer than 4
+// kernel launches (GGML_MI355X_GRAPH_MIN_LAUNCHES), launch directly. Graph plans
+// (ggml_backend_graph_plan_create / _compute) are captured at creation and computed with one
+// hipGraphLaunch. GGML_MI355X_DISABLE_GRAPHS=1 (process-wide, as GGML_CUDA_DISABLE_GRAPHS,
+// ggml-cuda.cu:2462) or set_graph_capture(false) makes both launch directly.
 GGML_API void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable);
-// counters since init: [0] captured plans, [1] graph instantiations, [2] in-place updates,
-// [3] direct (uncaptured) computes
+// counters since init: [0] captures (plans and graph_compute), [1] graph instantiations,
+// [2] in-place updates, [3] direct (uncaptured) computes
 GGML_API void ggml_backend_mi355x_graph_stats(ggml_backend_t backend, int64_t * stats4);
+// the same counters and more: [4] graph_compute replays of a cached capture, [5] graph_compute
+// captures; fills min(n, available) entries and returns that count
+GGML_API int ggml_backend_mi355x_graph_stats_ex(ggml_backend_t backend, int64_t * stats, int n);
 
 // Launch-shape knobs of the streaming kernels, for A/B tuning inside one process:
 // "mmv_blocks" (resident workgroups of the fused GEMV), "mmv_variant" (see mi355x_kernels.h).

@@ -346,6 +346,36 @@ def test_gpt2_long_context_decode(model_path):
         ref.ggml_backend_free(rbe)
 
 
+@pytest.mark.gpu
+def test_gpt2_decode_to_context_end_then_restart(model_path):
+    """Decode single tokens up to the last KV slot (where no next-step plan can be prebuilt), then
+    restart from position 0 and repeat, then free: every prebuilt graph plan is freed exactly once
+    (a plan taken by the fast path is owned by that eval), and the second pass reproduces the first
+    pass's logits bit for bit."""
+    lib = G.runtime()
+    be = G.mi355x_backend(lib)
+    n_ctx = 24
+    m = gpt2.Model(lib, model_path, be, n_ctx=n_ctx, n_batch=8)
+    try:
+        toks = m.tokenize(PROMPT)[:8]
+        passes = []
+        for _ in range(2):
+            outs = [m.eval(0, toks)]
+            n_past, nxt = len(toks), int(np.argmax(outs[-1][-1]))
+            while n_past < n_ctx:
+                outs.append(m.eval(n_past, [nxt]))
+                n_past += 1
+                nxt = int(np.argmax(outs[-1][-1]))
+            passes.append(np.concatenate(outs))
+        assert np.isfinite(passes[0]).all()
+        assert np.array_equal(passes[0].view(np.uint32), passes[1].view(np.uint32))
+        with pytest.raises(RuntimeError):
+            m.eval(n_ctx, [0])  # past the KV cache
+    finally:
+        m.free()
+        lib.ggml_backend_free(be)
+
+
 # ---- ggml_backend_sched: the backend as a drop-in under the reference scheduler -------------------
 
 SCHED_CHILD = os.path.join(REPO, "tests", "_sched_child.py")
