@@ -611,13 +611,29 @@ static mi_src_cols src_cols(const ggml_tensor * t) {
 
 // Converted activations for (src1, kind), reused by later mul_mats of the same graph that read
 // the same, unmodified src1 (Q/K/V or gate/up projections share their input).
-static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, int kind, int64_t K) {
+static void * find_activations(const mi_backend_ctx * ctx, const ggml_tensor * src1, int kind) {
     for (const auto & e : ctx->act_cache) {
         if (e.data == src1->data && e.kind == kind && memcmp(e.ne, src1->ne, sizeof(e.ne)) == 0 &&
             memcmp(e.nb, src1->nb, sizeof(e.nb)) == 0) {
             return e.dev;
         }
     }
+    return nullptr;
+}
+
+static void cache_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, int kind, void * dev) {
+    mi_act_cache_entry e;
+    e.data = src1->data;
+    e.nbytes = ggml_nbytes(src1);
+    e.kind = kind;
+    memcpy(e.ne, src1->ne, sizeof(e.ne));
+    memcpy(e.nb, src1->nb, sizeof(e.nb));
+    e.dev = dev;
+    ctx->act_cache.push_back(e);
+}
+
+static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, int kind, int64_t K) {
+    if (void * hit = find_activations(ctx, src1, kind)) return hit;
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
     void * dev = scratch_take(ctx, act_bytes(kind, K, ncols));
     const mi_src_cols x = src_cols(src1);
@@ -633,14 +649,7 @@ static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, in
         else mi_quantize_q8_0(x, K, act, ctx->stream);
     }
     ctx->last_launches++;
-    mi_act_cache_entry e;
-    e.data = src1->data;
-    e.nbytes = ggml_nbytes(src1);
-    e.kind = kind;
-    memcpy(e.ne, src1->ne, sizeof(e.ne));
-    memcpy(e.nb, src1->nb, sizeof(e.nb));
-    e.dev = dev;
-    ctx->act_cache.push_back(e);
+    cache_activations(ctx, src1, kind, dev);
     return dev;
 }
 
@@ -727,6 +736,29 @@ static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const vo
         }
     }
     ctx->last_launches++;
+}
+
+// the mul_mat descriptor of a whole MUL_MAT node (as mul_mat_run builds it)
+static mi_mm_desc mm_desc_of(const ggml_tensor * node) {
+    const ggml_tensor * src0 = node->src[0], * src1 = node->src[1];
+    mi_mm_desc m{};
+    m.W = src0->data;
+    m.type = src0->type;
+    m.K = src0->ne[0];
+    m.N = src0->ne[1];
+    m.ne02 = src0->ne[2];
+    m.ne03 = src0->ne[3];
+    m.nb01 = src0->nb[1];
+    m.nb02 = src0->nb[2];
+    m.nb03 = src0->nb[3];
+    m.ne11 = src1->ne[1];
+    m.ne12 = src1->ne[2];
+    m.ne13 = src1->ne[3];
+    m.dst = (float *) node->data;
+    m.nb1 = node->nb[1];
+    m.nb2 = node->nb[2];
+    m.nb3 = node->nb[3];
+    return m;
 }
 
 static void op_mul_mat(mi_backend_ctx * ctx, ggml_tensor * dst) {
@@ -1745,6 +1777,82 @@ static int try_fuse_attn_proj(mi_backend_ctx * ctx, ggml_cgraph * g, int i, cons
     return k2;
 }
 
+// a MUL_MAT node that runs on the exact int8 prefill GEMM (Q4_K / Q5_K weights, > 8 plain
+// columns; mm_act_kind 8)
+static bool prefill_mmx_eligible(const ggml_tensor * n) {
+    if (n->op != GGML_OP_MUL_MAT || is_split_tensor(n->src[0])) return false;
+    const ggml_tensor * a = n->src[0], * b = n->src[1];
+    if (b->type != GGML_TYPE_F32 || a->nb[0] != ggml_type_size(a->type) || b->nb[0] != sizeof(float) || n->nb[0] != sizeof(float)) return false;
+    if (a->ne[0] != b->ne[0]) return false;
+    return mm_act_kind(mm_desc_of(n), b) == 8;
+}
+
+// Batched (prompt) mul_mats that follow each other in the graph and are independent of each other
+// (Q/K/V or gate/up projections of one prompt, independent prompts), same weight type, K and
+// column count: their activations are quantized by ONE launch (each distinct src1 once) and their
+// GEMMs run as ONE grouped launch (mi_mul_mat_mmqx_group: every member's tiles in one grid), so
+// a short prompt pays two kernel boundaries per group instead of per mul_mat. Each member's
+// output is what op_mul_mat computes for it, bit for bit (same kernels, same fold). Returns the
+// index of the last node consumed, or -1 (fewer than two members).
+static int run_prefill_group(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
+    static const bool no_group = getenv("GGML_MI355X_NO_PREFILL_GROUP") != nullptr;
+    ggml_tensor * first = g->nodes[i];
+    if (no_group || !prefill_mmx_eligible(first)) return -1;
+    const ggml_type type = first->src[0]->type;
+    const int64_t K = first->src[0]->ne[0];
+    auto cols_of = [](const ggml_tensor * n) { return n->src[1]->ne[1] * n->src[1]->ne[2] * n->src[1]->ne[3]; };
+    const int64_t ncols = cols_of(first);
+    std::vector<ggml_tensor *> members = {first};
+    int last = i;
+    for (int j = next_node(g, i); j >= 0 && (int) members.size() < kMiMaxPrefillMembers; j = next_node(g, j)) {
+        ggml_tensor * n = g->nodes[j];
+        if (!prefill_mmx_eligible(n) || n->src[0]->type != type || n->src[0]->ne[0] != K || cols_of(n) != ncols) break;
+        bool independent = true;
+        for (ggml_tensor * m : members) {
+            if (overlaps(n->src[1], m) || overlaps(n->src[0], m) || overlaps(n, m->src[0]) || overlaps(n, m->src[1]) || overlaps(n, m)) {
+                independent = false;
+                break;
+            }
+        }
+        if (!independent) break;
+        members.push_back(n);
+        last = j;
+    }
+    if (members.size() < 2) return -1;
+    // activations: cached conversions are reused; the missing distinct src1s in one quantizer launch
+    mi_mmx_qgroup q;
+    q.K = K;
+    std::vector<void *> xa(members.size(), nullptr);
+    for (size_t k = 0; k < members.size(); k++) {
+        const ggml_tensor * x = members[k]->src[1];
+        xa[k] = find_activations(ctx, x, 8);
+        if (xa[k]) continue;
+        void * dev = scratch_take(ctx, act_bytes(8, K, ncols));
+        q.m[q.n].x = src_cols(x);
+        q.m[q.n].act = mi_act_mmx_carve(dev, K, ncols);
+        q.n++;
+        cache_activations(ctx, x, 8, dev);
+        xa[k] = dev;
+    }
+    if (q.n > 0) {
+        mi_quantize_q8_K_mmx_group(q, ctx->stream);
+        ctx->last_launches++;
+    }
+    mi_mmx_group gg;
+    gg.type = type;
+    gg.K = K;
+    gg.n = (int) members.size();
+    for (size_t k = 0; k < members.size(); k++) {
+        const ggml_tensor * n = members[k];
+        gg.m[k] = mi_mmx_member{n->src[0]->data, n->src[0]->nb[1], n->src[0]->ne[1], mi_act_mmx_carve(xa[k], K, ncols), (float *) n->data,
+                                n->nb[1], 0};
+    }
+    mi_mul_mat_mmqx_group(gg, ctx->stream);
+    ctx->last_launches++;
+    for (ggml_tensor * m : members) invalidate_activations(ctx, m);
+    return last;
+}
+
 static bool is_copy(const ggml_tensor * t) {
     return (t->op == GGML_OP_CPY || t->op == GGML_OP_DUP || t->op == GGML_OP_CONT) && is_f16_or_f32(t->src[0]) && is_f16_or_f32(t) &&
            ggml_nelements(t) == ggml_nelements(t->src[0]);
@@ -2176,13 +2284,19 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
         }
         flush_pending(ctx);
         switch (node->op) {
-            case GGML_OP_MUL_MAT:
+            case GGML_OP_MUL_MAT: {
                 if (!no_fuse && fused_mv_eligible(node)) {
                     i = run_fused_group(ctx, cgraph, i);
                     continue;
                 }
+                const int lastg = run_prefill_group(ctx, cgraph, i);
+                if (lastg >= 0) {
+                    i = lastg;
+                    continue;
+                }
                 op_mul_mat(ctx, node);
                 break;
+            }
             default:
                 op_companion(ctx, node);
         }

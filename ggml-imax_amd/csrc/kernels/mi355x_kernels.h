@@ -147,8 +147,38 @@ struct mi_act_mmx {
 size_t mi_act_mmx_bytes(int64_t K, int64_t ncols);
 mi_act_mmx mi_act_mmx_carve(void * base, int64_t K, int64_t ncols);
 void mi_quantize_q8_K_mmx(const mi_src_cols & x, int64_t K, const mi_act_mmx & act, hipStream_t s);
+// several activation sources (same K) quantized by one launch
+constexpr int kMiMaxPrefillMembers = 16;
+struct mi_mmx_qgroup {
+    int n = 0;
+    int64_t K = 0;
+    struct member {
+        mi_src_cols x;
+        mi_act_mmx act;
+        int64_t col_begin;  // set by the launcher
+    } m[kMiMaxPrefillMembers];
+};
+void mi_quantize_q8_K_mmx_group(mi_mmx_qgroup & q, hipStream_t s);
 bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t nb01);
-// 2-D Q4_K / Q5_K weights [K, N] x act.ncols columns -> dst (column stride ycol bytes)
+// Independent Q4_K / Q5_K mul_mats (same type, K and activation column count) in one launch:
+// member i = 2-D weights [K, N_i] x act_i.ncols columns -> dst_i (column stride ycol_i bytes)
+struct mi_mmx_member {
+    const void * W;
+    size_t nb01;
+    int64_t N;
+    mi_act_mmx act;
+    float * dst;
+    size_t ycol;
+    int64_t tile_begin;  // set by the launcher
+};
+struct mi_mmx_group {
+    int type = 0;
+    int n = 0;
+    int64_t K = 0;
+    mi_mmx_member m[kMiMaxPrefillMembers];
+};
+void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s);
+// one member
 void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_mmx & act, float * dst,
                      size_t ycol, hipStream_t s);
 

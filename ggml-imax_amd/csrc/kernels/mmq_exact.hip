@@ -65,6 +65,19 @@ __device__ __forceinline__ float mmqx_term(int T, float U, float dw, float dm, f
     return __builtin_fmaf(da, t, 0.0f);
 }
 
+// The canonical combine order of an output's superblock terms, shared by every kernel of this
+// file (so any column shard of a prompt gives the same bits whichever kernel computes it): the S
+// superblocks form 4 contiguous groups of gs = ceil(S / 4) (the last ones shorter or empty), each
+// group's terms are left-folded (g = t_first; g = g + t; ...), then the group sums are
+// left-folded (y = g_0; y = y + g_1; ...). A pipelined kernel gives each group to one wave.
+__host__ __device__ constexpr int cfold_gs(int S) { return (S + 3) / 4; }
+// term t of superblock sb (terms arrive in superblock order): g / y updated in place
+__device__ __forceinline__ void cfold(float & g, float & y, float t, int sb, int gs, int S) {
+    const int pos = sb % gs;
+    g = pos == 0 ? t : g + t;
+    if (pos == gs - 1 || sb == S - 1) y = sb < gs ? g : y + g;
+}
+
 template <int TYPE>
 struct XFmt {
     static constexpr bool Q5 = TYPE == 13;
@@ -83,20 +96,44 @@ struct XRaw {
     uint4 hdr, qs, qh;
 };
 
+// The member of a grouped launch that workgroup blockIdx.x belongs to (members' tiles are dealt
+// consecutively: tile_begin ascending), and the workgroup's tile inside it. blockIdx.x is
+// wave-uniform, so the scan is scalar; the member's fields are scalar loads from the kernel
+// arguments. Defines W, nb01, K, N, act, dst, ycol and mmx_tile.
+#define MI_MMX_MEMBER(g)                                                                   \
+    int mmx_i_ = 0;                                                                        \
+    while (mmx_i_ + 1 < (g).n && (int64_t) blockIdx.x >= (g).m[mmx_i_ + 1].tile_begin) mmx_i_++; \
+    const int64_t mmx_tile = (int64_t) blockIdx.x - (g).m[mmx_i_].tile_begin;               \
+    const uint8_t * __restrict__ W = (const uint8_t *) (g).m[mmx_i_].W;                    \
+    const size_t nb01 = (g).m[mmx_i_].nb01;                                                \
+    const int64_t K = (g).K;                                                               \
+    const int64_t N = (g).m[mmx_i_].N;                                                     \
+    const mi_act_mmx act = (g).m[mmx_i_].act;                                              \
+    float * __restrict__ dst = (g).m[mmx_i_].dst;                                          \
+    const size_t ycol = (g).m[mmx_i_].ycol;                                                \
+    (void) nb01; (void) N; (void) dst; (void) ycol
+
 } // namespace
 
 // ---- activations: q8_K quants in the MFMA layouts ------------------------------------------------
-// xq [K/64][ncols][64] int8, xd [K/256][ncols] f32 (d), xu [K/256][ncols][16] f16 (S_j & 63,
+// xq [K/32][ncols][32] int8 (a 32-deep MFMA step of 32 columns is one contiguous 1 KB), xd
+// [K/256][ncols] f32 (d), xu [K/256][ncols][16] f16 (S_j & 63,
 // S_j >> 6 for j = 0..7, S_j = sum of the 32 quants of sub-block j). One superblock per wave;
 // grid (column, group of 4 superblocks): the column's address is wave-uniform scalar arithmetic
 // (32-bit, and no divisions at all for a plain 2-D src1), so the load issues at once.
-__global__ __launch_bounds__(256) void k_quantize_q8_K_mmx(mi_src_cols x, int64_t K, mi_act_mmx act) {
+__global__ __launch_bounds__(256) void k_quantize_q8_K_mmx(mi_mmx_qgroup q) {
     const int wave = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    const int64_t K = q.K;
     const uint32_t nb_per_col = (uint32_t) (K / 256);
     const uint32_t b = blockIdx.y * 4 + (uint32_t) wave;
     if (b >= nb_per_col) return;  // wave-uniform
-    const uint32_t c = blockIdx.x;
+    // the member this column belongs to (scalar scan over the kernel arguments)
+    int mi = 0;
+    while (mi + 1 < q.n && (int64_t) blockIdx.x >= q.m[mi + 1].col_begin) mi++;
+    const mi_src_cols x = q.m[mi].x;
+    const mi_act_mmx act = q.m[mi].act;
+    const uint32_t c = (uint32_t) ((int64_t) blockIdx.x - q.m[mi].col_begin);
     const char * cbase;
     if (x.ne2 == 1 && x.ne3 == 1) {
         cbase = x.base + (size_t) c * x.nb1;
@@ -116,8 +153,8 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K_mmx(mi_src_cols x, int64_
     float d;
     mi_q8K_superblock(v, lane, packed, sum, d);
     const int64_t ncols = act.ncols;
-    // element k = lane*4 .. +3 of the superblock: 64-block lane/16, offset (lane%16)*4
-    *(uint32_t *) (act.xq + ((b * 4 + (lane >> 4)) * ncols + c) * 64 + (lane & 15) * 4) = packed;
+    // element k = lane*4 .. +3 of the superblock: 32-block lane/8, offset (lane%8)*4
+    *(uint32_t *) (act.xq + ((b * 8 + (lane >> 3)) * ncols + c) * 32 + (lane & 7) * 4) = packed;
     if ((lane & 7) == 0) {
         const int j = lane >> 3;
         const uint32_t lo = mi_f2h((float) (sum & 63)), hi = mi_f2h((float) (sum >> 6));
@@ -145,9 +182,23 @@ mi_act_mmx mi_act_mmx_carve(void * base, int64_t K, int64_t ncols) {
     return a;
 }
 
+void mi_quantize_q8_K_mmx_group(mi_mmx_qgroup & q, hipStream_t s) {
+    int64_t cols = 0;
+    for (int i = 0; i < q.n; i++) {
+        q.m[i].col_begin = cols;
+        cols += q.m[i].act.ncols;
+    }
+    if (cols == 0 || q.K < 256) return;
+    hipLaunchKernelGGL(k_quantize_q8_K_mmx, dim3((unsigned) cols, (unsigned) ((q.K / 256 + 3) / 4)), dim3(256), 0, s, q);
+}
+
 void mi_quantize_q8_K_mmx(const mi_src_cols & x, int64_t K, const mi_act_mmx & act, hipStream_t s) {
-    if (act.ncols == 0 || K < 256) return;
-    hipLaunchKernelGGL(k_quantize_q8_K_mmx, dim3((unsigned) act.ncols, (unsigned) ((K / 256 + 3) / 4)), dim3(256), 0, s, x, K, act);
+    mi_mmx_qgroup q;
+    q.n = 1;
+    q.K = K;
+    q.m[0].x = x;
+    q.m[0].act = act;
+    mi_quantize_q8_K_mmx_group(q, s);
 }
 
 namespace {
@@ -165,8 +216,8 @@ namespace {
 // NWV = 4: half-width workgroups (64 rows x 64 columns, 4 waves, each thread stages two rows), two
 // per CU, so one workgroup's barrier wait overlaps the other's MFMA steps.
 template <int TYPE, bool XCD, int ABL = 0, int LEAD = 4, int SCT = 0, int NWV = 8>
-__global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
-                                              mi_act_mmx act, float * __restrict__ dst, size_t ycol) {
+__global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
+    MI_MMX_MEMBER(g);
     using F = XFmt<TYPE>;
     constexpr int NP = F::NP;
     constexpr int XR = 256 + 16;             // LDS row stride of a plane (bytes): conflict-free b128 reads / writes
@@ -185,10 +236,10 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ 
     int64_t n0, b0;
     {
         const int64_t nrt = (N + XBM - 1) / XBM, nct = (ncols + XBN_ - 1) / XBN_;
-        int64_t t = blockIdx.x;
+        int64_t t = mmx_tile;
         if constexpr (XCD) {
             // workgroup i runs on XCD i % 8: give each XCD a contiguous run of tiles, row tiles
-            // fastest, so an XCD's L2 holds few activation column tiles
+            // fastest, so an XCD's L2 holds few activation column tiles (one-member launches)
             const int64_t T = nrt * nct, per = (T + 7) / 8;
             t = (int64_t) (blockIdx.x % 8) * per + blockIdx.x / 8;
             if (t >= T) return;
@@ -236,8 +287,8 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ 
     const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
     const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
     const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
-    const uint32_t xcol = bcol * 64 + 16 * h;
-    const uint32_t xstep = (uint32_t) ncols * 64;  // bytes per 64-deep K block
+    const uint32_t xcol = bcol * 32 + 16 * h;
+    const uint32_t xstep = (uint32_t) ncols * 32;  // bytes per 32-deep K step
 
     struct Raw {
         uint4 hdr, qs, qh;
@@ -256,10 +307,10 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ 
     };
     auto load_x = [&](Xs & xs, int sb) {
         sb = sb < S ? sb : S - 1;
-        const uint32_t kb = (uint32_t) sb * 4;  // first 64-block
+        const uint32_t kb = (uint32_t) sb * 8;  // first 32-deep step
 #pragma unroll
         for (int kk = 0; kk < 8; kk++)
-            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kb + (kk >> 1)) * xstep + 32 * (kk & 1), 0, 0));
+            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kb + kk) * xstep, 0, 0));
         const uint32_t sc = (uint32_t) sb * (uint32_t) ncols + bcol;
         xs.bu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, sc * 32 + 16 * h, 0, 0));
         xs.da = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, sc * 4, 0, 0));
@@ -329,7 +380,8 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ 
         dq_rows(buf, raw, pr);
     };
 
-    f32x16 y = {};
+    f32x16 y = {}, gsum = {};
+    const int gs = cfold_gs(S);
     // The raw weights of superblock sb + 1 are dequantized into LDS at the end of stage sb; they
     // were requested LEAD stages earlier (a ring of LEAD raw slots: HBM latency is several stage
     // times). The activation fragment of step kk of sb + 1 is loaded into the register that step kk
@@ -360,7 +412,7 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ 
         const char * base = lds + cur * kBuf;
         const char * arow_p = base + (32 * rw + r) * XR + 16 * h;
         const int nx = sb + 1 < S ? sb + 1 : S - 1;
-        const uint32_t kbn = (uint32_t) nx * 4;
+        const uint32_t kbn = (uint32_t) nx * 8;
         i32x16 acc[NP];
         // weight fragments two 32-deep steps ahead (explicit ring; the sched_barrier per step
         // keeps the compiler from hoisting every step's LDS reads: registers)
@@ -392,7 +444,7 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ 
                 }
             }
             // step kk of the next superblock into the register just consumed
-            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kbn + (kk >> 1)) * xstep + 32 * (kk & 1), 0, 0));
+            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kbn + kk) * xstep, 0, 0));
 #pragma unroll
             for (int pr = 0; pr < ROWP; pr++) {
                 if (kk == 0) dq_prep(dq[pr], rslot[pr]);
@@ -408,7 +460,12 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ 
         // U on the f16 MFMA, then the canonical combine
         if constexpr ((ABL & 2) != 0) {  // timing ablation: no combine
 #pragma unroll
-            for (int i = 0; i < 16; i++) y[i] += (float) acc[0][i];
+            for (int i = 0; i < 16; i++) {
+                float gg = gsum[i], yy = y[i];
+                cfold(gg, yy, (float) acc[0][i], sb, gs, S);
+                gsum[i] = gg;
+                y[i] = yy;
+            }
         } else {
             const char * ro = base + NP * kPlane;
             const float * dwv = (const float *) (ro + XBM * 32);
@@ -433,7 +490,10 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ 
 #pragma unroll
                     for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][i];
                     const float term = mmqx_term(T, Uv[i], dw[e], dm[e], da);
-                    y[i] = sb == 0 ? term : y[i] + term;
+                    float gg = gsum[i], yy = y[i];
+                    cfold(gg, yy, term, sb, gs, S);
+                    gsum[i] = gg;
+                    y[i] = yy;
                 }
             }
         }
@@ -480,35 +540,38 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(const uint8_t * __restrict__ 
 }
 
 
-// ---- short prompts: a workgroup of NWV waves per 32 x 32 tile, superblocks dealt round-robin ---
-// Wave w of the tile computes the terms of superblocks w, w + NWV, ... (one per round) for the
-// tile's 32 prompt columns x 32 weight rows; after each round wave 0 left-folds the round's terms
-// from LDS in superblock order. Orientation: the activations are the MFMA A operand (accumulator
-// row = prompt column), the weights the B operand (accumulator column = weight row = the lane's
-// own row), so every lane dequantizes its own weight row straight from the 16-byte loads it
-// issued and applies its own row's d / dmin. Each wave's registers are reloaded with its next
-// round's superblock as soon as they are consumed (one round of lead).
-// C4: ncols % 4 == 0 (the four da of an accumulator row group are one aligned 16-byte load).
-// PF: weight ring depth in rounds -- the raw weights of round rd + PF are requested as round rd
-// consumes its own, so with PF = 2 both rounds of a K = 4096 tile are in flight from the start (one
-// memory latency per tile instead of one per round); activations keep one round of lead (L2).
-// ABL: timing ablations (results invalid): 1 no MFMAs, 2 no weight reloads, 4 no activation
-// reloads, 8 no LDS fold / barriers
-// CH: independent accumulator chains per plane (steps kk alternate between them; their exact
-// int32 sums are added at the end)
-template <int TYPE, bool C4, int PF = 1, int ABL = 0, int CH = 1>
-__global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
-                                              float * __restrict__ dst, size_t ycol) {
+// ---- short prompts, pipelined: 4 waves per 32 x 32 tile, one superblock group each --------------
+// A workgroup computes one tile of 32 weight rows x 32 prompt columns; wave w computes the terms of
+// superblock group w of the canonical order (cfold: the S superblocks in 4 contiguous groups) one
+// superblock after the other and left-folds them in registers, with the next superblock's weights
+// and activation fragments requested before the current one's MFMAs (a register double buffer:
+// the load of superblock s + 1 streams under the MFMAs of s). The 4 group sums meet in LDS and
+// are folded by all 4 waves at once. Two workgroups per CU (<= 256 VGPRs: two waves per SIMD), so
+// one workgroup's loads also overlap the other's MFMAs / VALU, and a grouped launch (many members'
+// tiles in one grid) streams tile after tile through every CU.
+// MFMA orientation as k_mmqd1: A = activation fragment (accumulator row = prompt column), B =
+// the dequantized weight planes (accumulator column = the lane's own weight row r), so every lane
+// dequantizes its row from the 16-byte loads it issued and applies its row's d / dmin.
+// C4: every member has ncols % 4 == 0 (the four da of an accumulator row group: one 16-byte load)
+// ABL (timing ablations, results invalid): 1 weight loads addressed as a tile-major repacked
+// layout (a wave's superblocks of its 32 rows contiguous, [chunk][row] 16-byte chunks), 2 every
+// superblock reuses the activation bytes of the wave's first one (no further activation
+// traffic), 4 no MFMAs
+template <int TYPE, bool C4, int ABL = 0>
+__global__ __launch_bounds__(256, 2) void k_mmqp(mi_mmx_group grp) {
+    MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
     constexpr int NP = F::NP;
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [wave][lane][16] terms of a round
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __shared__ __attribute__((aligned(16))) float red[4 * 16 * 64];  // [wave][el][lane] group sums
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
     const int64_t ncols = act.ncols;
     const int S = (int) (K / 256);
-    const int rounds = (S + nw - 1) / nw;
+    const int gs = cfold_gs(S);
+    const int sb0 = w * gs, sb1 = min(S, sb0 + gs);  // this wave's superblock group (may be empty)
     const int64_t nrt = (N + 31) / 32;
-    const int64_t n0 = (blockIdx.x % nrt) * 32, c0 = (blockIdx.x / nrt) * 32;
+    const int64_t n0 = (mmx_tile % nrt) * 32, c0 = (mmx_tile / nrt) * 32;
 
     const int nrows = (int) std::min<int64_t>(32, N - n0);
     const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
@@ -517,76 +580,75 @@ __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, si
     const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
     const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
     const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
-    const uint32_t xstep = (uint32_t) ncols * 64;
-    const uint32_t xcol = acol * 64 + 16 * h;
+    const uint32_t xstep = (uint32_t) ncols * 32;
+    const uint32_t xcol = acol * 32 + 16 * h;
     constexpr uint32_t kQs = F::Q5 ? 48 : 16;
 
-    auto ld_x = [&](int sb, int kk) -> i32x4 {
-        return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + ((uint32_t) sb * 4 + (kk >> 1)) * xstep + 32 * (kk & 1), 0, 0));
+    struct Ops {
+        uint4 hdr, q4[4], qh;
+        i32x4 xa[8];
+        half8 xu;
+        float4 da[4];
     };
-    auto ld_w = [&](int sb, uint32_t off) -> uint4 {
-        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wrow + (uint32_t) sb * F::BS + off, 0, 0));
-    };
-    auto ld_u = [&](int sb) -> half8 {
-        return __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, ((uint32_t) sb * (uint32_t) ncols + acol) * 32 + 16 * h, 0, 0));
-    };
-    // da of accumulator elements 4g .. 4g + 3: prompt columns c0 + 8 g + 4 h + 0..3 (columns past
-    // ncols read another superblock's scales or, past the buffer, zeros: never stored)
-    auto ld_da = [&](int sb, int g) -> float4 {
-        const uint32_t off = (uint32_t) ((int64_t) sb * ncols + c0 + 8 * g + 4 * h) * 4;
-        if constexpr (C4) {
-            return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dres, off, 0, 0));
+    auto ld = [](__amdgpu_buffer_rsrc_t res, uint32_t off) -> uint4 { return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(res, off, 0, 0)); };
+    // weights first (HBM), then the activation fragments (L2)
+    auto load = [&](Ops & o, int sb) {
+        if constexpr ((ABL & 1) != 0) {
+            const uint32_t tb = (uint32_t) sb * 32 * F::BS;  // tile-major: [sb][chunk][row]
+            o.hdr = ld(wres, tb + (uint32_t) r * 16);
+#pragma unroll
+            for (int p = 0; p < 4; p++) o.q4[p] = ld(wres, tb + (uint32_t) ((1 + 2 * p + h) * 32 + r) * 16);
         } else {
-            return make_float4(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off, 0, 0)),
-                               __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 4, 0, 0)),
-                               __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 8, 0, 0)),
-                               __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 12, 0, 0)));
+            const uint32_t wb = wrow + (uint32_t) sb * F::BS;
+            o.hdr = ld(wres, wb);
+#pragma unroll
+            for (int p = 0; p < 4; p++) o.q4[p] = ld(wres, wb + kQs + 32 * p + 16 * h);
+            if constexpr (F::Q5) o.qh = ld(wres, wb + 16 + 16 * h);
+        }
+        const int sbx = (ABL & 2) ? sb0 : sb;
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) o.xa[kk] = __builtin_bit_cast(i32x4, ld(xres, xcol + ((uint32_t) sbx * 8 + kk) * xstep));
+        o.xu = __builtin_bit_cast(half8, ld(ures, ((uint32_t) sb * (uint32_t) ncols + acol) * 32 + 16 * h));
+        // da of accumulator elements 4 g .. 4 g + 3: prompt columns c0 + 8 g + 4 h + 0..3 (columns
+        // past ncols read another superblock's scales or, past the buffer, zeros: never stored)
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint32_t off = (uint32_t) ((int64_t) sb * ncols + c0 + 8 * g + 4 * h) * 4;
+            if constexpr (C4) {
+                o.da[g] = __builtin_bit_cast(float4, ld(dres, off));
+            } else {
+                o.da[g] = make_float4(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off, 0, 0)),
+                                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 4, 0, 0)),
+                                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 8, 0, 0)),
+                                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 12, 0, 0)));
+            }
         }
     };
-    auto sb_of = [&](int rd) { const int s = rd * nw + w; return s < S ? s : S - 1; };
-    // raw weights of one round: header, four 16-byte quant chunks (+ the high bits of Q5_K)
-    struct Wt {
-        uint4 hdr, q4[4], qh;
-    };
-    auto ld_wt = [&](Wt & t, int sb) {
-        t.hdr = ld_w(sb, 0);
+    f32x16 gsum = {};
+    // the superblock's exact T (plane MFMAs) and U (f16 MFMA), the canonical term, left-folded
+    auto compute = [&](const Ops & o, const bool first) {
+        const uint32_t w0 = o.hdr.y, w1 = o.hdr.z, w2 = o.hdr.w;
+        const float dw = mi_h2f((uint16_t) (o.hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (o.hdr.x >> 16));
+        i32x16 acc[NP];
 #pragma unroll
-        for (int p = 0; p < 4; p++) t.q4[p] = ld_w(sb, kQs + 32 * p + 16 * h);
-        if constexpr (F::Q5) t.qh = ld_w(sb, 16 + 16 * h);
-    };
-
-    i32x4 xa[8];
-    Wt wt[PF];
-    {
-        const int sb = sb_of(0);
+        for (int kk = 0; kk < 8; kk++) {
+            const int jj = kk & 3;
+            const uint32_t sc = kk < 4 ? ((w0 >> (8 * jj)) & 63) : (((w2 >> (8 * jj)) & 0xF) | (((w0 >> (8 * jj + 6)) & 3) << 4));
+            const uint4 q = o.q4[kk >> 1];
+            uint32_t v[4] = {q.x, q.y, q.z, q.w};
+            const uint32_t hb[4] = {o.qh.x, o.qh.y, o.qh.z, o.qh.w};
 #pragma unroll
-        for (int kk = 0; kk < 8; kk++) xa[kk] = ld_x(sb, kk);
-        ld_wt(wt[0], sb);
-    }
-    half8 xu = ld_u(sb_of(0));
-    float4 da[4];
-#pragma unroll
-    for (int g = 0; g < 4; g++) da[g] = ld_da(sb_of(0), g);
-#pragma unroll
-    for (int u = 1; u < PF; u++) ld_wt(wt[u], sb_of(u));
-
-    f32x16 y = {};  // the fold (wave 0)
-    float * mine = red + ((size_t) w * 64 + lane) * 16;
-    auto round = [&](const int rd, Wt & t) {
-        const int sn = sb_of(rd + 1);   // activations: one round of lead
-        const int sw = sb_of(rd + PF);  // weights: PF rounds of lead
-        // header -> plane factors (splat u16x2), U operand, d, dmin (get_scale_min_k4, ggml-quants.c)
-        const uint32_t w0 = t.hdr.y, w1 = t.hdr.z, w2 = t.hdr.w;
-        const float dw = mi_h2f((uint16_t) (t.hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (t.hdr.x >> 16));
-        uint32_t fac[8][NP];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int jj = j & 3;
-            const uint32_t sc = j < 4 ? ((w0 >> (8 * jj)) & 63) : (((w2 >> (8 * jj)) & 0xF) | (((w0 >> (8 * jj + 6)) & 3) << 4));
+            for (int e = 0; e < 4; e++) {
+                v[e] = (kk & 1) ? (v[e] >> 4) & 0x0F0F0F0Fu : v[e] & 0x0F0F0F0Fu;
+                if constexpr (F::Q5) v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
+            }
 #pragma unroll
             for (int p = 0; p < NP; p++) {
-                const uint32_t f = F::factor((int) sc, p);
-                fac[j][p] = f | (f << 16);
+                uint32_t f = F::factor((int) sc, p);
+                f |= f << 16;
+                const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+                if constexpr ((ABL & 4) != 0) acc[p][kk] = (kk == 0 ? 0 : acc[p][kk]) + o.xa[kk][0] * b[0];
+                else acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.xa[kk], b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
             }
         }
         half8 mu;
@@ -598,87 +660,48 @@ __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, si
             mu[2 * q] = (_Float16) (float) m;
             mu[2 * q + 1] = (_Float16) (float) (64 * m);
         }
-        if constexpr ((ABL & 2) == 0) t.hdr = ld_w(sw, 0);
-        const uint4 qh = t.qh;
-        i32x16 acc[CH][NP];
-#pragma unroll
-        for (int kk = 0; kk < 8; kk++) {
-            const uint4 q = t.q4[kk >> 1];
-            uint32_t v[4] = {q.x, q.y, q.z, q.w};
-            const uint32_t hb[4] = {qh.x, qh.y, qh.z, qh.w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                v[e] = (kk & 1) ? (v[e] >> 4) & 0x0F0F0F0Fu : v[e] & 0x0F0F0F0Fu;
-                if constexpr (F::Q5) v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
-            }
-            if ((ABL & 2) == 0 && (kk & 1)) t.q4[kk >> 1] = ld_w(sw, kQs + 32 * (kk >> 1) + 16 * h);
-#pragma unroll
-            for (int p = 0; p < NP; p++) {
-                const uint32_t f = fac[kk][p];
-                const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
-                i32x16 & a = acc[kk % CH][p];
-                if constexpr ((ABL & 1) != 0) a[kk] = (kk < CH ? 0 : a[kk]) + xa[kk][0] * b[0];
-                else a = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[kk], b, kk < CH ? i32x16{} : a, 0, 0, 0);
-            }
-            if constexpr ((ABL & 4) == 0) xa[kk] = ld_x(sn, kk);
-        }
-        if constexpr (F::Q5) t.qh = ld_w(sw, 16 + 16 * h);
-        const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
-        if constexpr ((ABL & 4) == 0) xu = ld_u(sn);
-        float term[16];
+        const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(o.xu, mu, f32x16{}, 0, 0, 0);
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            const float dav[4] = {da[g].x, da[g].y, da[g].z, da[g].w};
+            const float dav[4] = {o.da[g].x, o.da[g].y, o.da[g].z, o.da[g].w};
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 const int el = 4 * g + e;
-                auto P = [&](int p) { int v = acc[0][p][el]; if constexpr (CH > 1) v += acc[1][p][el]; return v; };
-                int T = P(NP - 1);
+                int T = acc[NP - 1][el];
 #pragma unroll
-                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + P(p);
-                term[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
-            }
-            if constexpr ((ABL & 4) == 0) da[g] = ld_da(sn, g);
-        }
-        if constexpr ((ABL & 8) != 0) {
-#pragma unroll
-            for (int q = 0; q < 16; q++) y[q] = rd == 0 ? term[q] : y[q] + term[q];
-            return;
-        }
-        // the round's terms meet in LDS; wave 0 folds them in superblock order
-#pragma unroll
-        for (int q = 0; q < 4; q++) *(float4 *) (mine + 4 * q) = make_float4(term[4 * q], term[4 * q + 1], term[4 * q + 2], term[4 * q + 3]);
-        mi_lds_barrier();
-        if (w == 0) {
-            const int nv = min(nw, S - rd * nw);
-            for (int v = 0; v < nv; v++) {
-                const float * src = red + ((size_t) v * 64 + lane) * 16;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const float4 t4 = *(const float4 *) (src + 4 * q);
-                    const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
-#pragma unroll
-                    for (int e = 0; e < 4; e++) y[4 * q + e] = (rd == 0 && v == 0) ? tv[e] : y[4 * q + e] + tv[e];
-                }
+                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
+                const float term = mmqx_term(T, Uv[el], dw, dm, dav[e]);
+                gsum[el] = first ? term : gsum[el] + term;
             }
         }
-        mi_lds_barrier();
     };
-    // unrolled by PF so every ring slot index is static (round rd uses slot rd % PF)
-    for (int rd0 = 0; rd0 < rounds; rd0 += PF) {
-#pragma unroll
-        for (int u = 0; u < PF; u++) {
-            if (rd0 + u < rounds) round(rd0 + u, wt[u]);
+    // superblocks sb0 .. sb1 - 1, two register sets alternating; every load unconditional (the
+    // superblock index clamped into the group: a past-the-end prefetch re-reads the last one)
+    if (sb0 < sb1) {
+        Ops a, b;
+        load(a, sb0);
+        for (int sb = sb0; sb < sb1; sb += 2) {
+            load(b, min(sb + 1, sb1 - 1));
+            compute(a, sb == sb0);
+            if (sb + 1 >= sb1) break;
+            load(a, min(sb + 2, sb1 - 1));
+            compute(b, false);
         }
-    }
-    if (w != 0) return;
-    // store: element el = prompt column c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
-    const int64_t n = n0 + r;
-    if (n >= N) return;
 #pragma unroll
-    for (int el = 0; el < 16; el++) {
+        for (int el = 0; el < 16; el++) red[(w * 16 + el) * 64 + lane] = gsum[el];
+    }
+    mi_lds_barrier();
+    // the group sums left-folded (canonical order); wave w folds accumulator elements el = w,
+    // w + 4, w + 8, w + 12 of every lane: lanes 0..31 store 32 consecutive rows of one column
+    const int ngroups = (S + gs - 1) / gs;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int el = w + 4 * i;
+        float y = red[el * 64 + lane];
+        for (int v = 1; v < ngroups; v++) y = y + red[(v * 16 + el) * 64 + lane];
+        const int64_t n = n0 + r;
         const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * h;
-        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y[el];
+        if (n < N && c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y;
     }
 }
 
@@ -690,10 +713,11 @@ __global__ __launch_bounds__(512) void k_mmqd(const uint8_t * __restrict__ W, si
 // wave-private LDS row instead of registers. Same operands, same exact T / U and the same
 // canonical fold (terms left-folded in superblock order) as k_mmqd / k_mmqx: bit-identical.
 // ABL (timing ablations, results invalid): 1 no MFMAs, 2 one activation load reused, 4 no fold,
-// 8 weight header only
+// 8 weight header only, 16 weight loads addressed as a wave-contiguous repacked layout ([chunk][row]
+// 16-byte chunks per 32-row x superblock tile: every load instruction one contiguous 1 KB)
 template <int TYPE, int ABL = 0>
-__global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
-                                               float * __restrict__ dst, size_t ycol) {
+__global__ __launch_bounds__(1024) void k_mmqd1(mi_mmx_group g) {
+    MI_MMX_MEMBER(g);
     using F = XFmt<TYPE>;
     constexpr int NP = F::NP;
     extern __shared__ __attribute__((aligned(16))) float red[];  // [wave][lane][16] terms, then [wave][32] da
@@ -702,7 +726,7 @@ __global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, 
     const int64_t ncols = act.ncols;
     const int S = (int) (K / 256);  // == waves of the workgroup
     const int64_t nrt = (N + 31) / 32;
-    const int64_t n0 = (blockIdx.x % nrt) * 32, c0 = (blockIdx.x / nrt) * 32;
+    const int64_t n0 = (mmx_tile % nrt) * 32, c0 = (mmx_tile / nrt) * 32;
     const int sb = w;
 
     const int nrows = (int) std::min<int64_t>(32, N - n0);
@@ -712,21 +736,27 @@ __global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, 
     const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
     const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
     const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
-    const uint32_t xstep = (uint32_t) ncols * 64;
-    const uint32_t xcol = acol * 64 + 16 * h + (uint32_t) sb * 4 * xstep;
+    const uint32_t xstep = (uint32_t) ncols * 32;
+    const uint32_t xcol = acol * 32 + 16 * h + (uint32_t) sb * 8 * xstep;
     constexpr uint32_t kQs = F::Q5 ? 48 : 16;
 
     // every load of the wave, weights first (HBM), then the activation fragments (L2)
     auto ld_w = [&](uint32_t off) -> uint4 { return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wrow + off, 0, 0)); };
-    const uint4 hdr = ld_w(0);
+    // ABL 16: the same loads at the offsets of a [chunk][row] repacked tile (chunk 0 = header,
+    // 1 + 2 p + h = quant chunk p, half h)
+    const uint32_t wtile = (uint32_t) sb * 32 * F::BS;
+    auto ld_wc = [&](int chunk) -> uint4 {
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wtile + (uint32_t) (chunk * 32 + r) * 16, 0, 0));
+    };
+    const uint4 hdr = (ABL & 16) ? ld_wc(0) : ld_w(0);
     uint4 q4[4];
 #pragma unroll
-    for (int p = 0; p < 4; p++) q4[p] = (ABL & 8) ? hdr : ld_w(kQs + 32 * p + 16 * h);
+    for (int p = 0; p < 4; p++) q4[p] = (ABL & 8) ? hdr : (ABL & 16) ? ld_wc(1 + 2 * p + h) : ld_w(kQs + 32 * p + 16 * h);
     const uint4 qh = F::Q5 ? ld_w(16 + 16 * h) : uint4{};
     i32x4 xa[8];
 #pragma unroll
     for (int kk = 0; kk < 8; kk++)
-        xa[kk] = ((ABL & 2) && kk) ? xa[0] : __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + (kk >> 1) * xstep + 32 * (kk & 1), 0, 0));
+        xa[kk] = ((ABL & 2) && kk) ? xa[0] : __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + kk * xstep, 0, 0));
     const half8 xu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, ((uint32_t) sb * (uint32_t) ncols + acol) * 32 + 16 * h, 0, 0));
     // da of prompt column c0 + r (lanes >= 32 duplicate), parked in this wave's LDS row: columns
     // past ncols read a clamped column's value (never stored)
@@ -787,33 +817,21 @@ __global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, 
         *(float4 *) (mine + 4 * g) = make_float4(term[0], term[1], term[2], term[3]);
     }
     mi_lds_barrier();
-    // wave 0 left-folds the terms in superblock order and stores; element el = prompt column
-    // c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
-    if (w != 0) return;
-    f32x16 y;
-    {
-        const float * src = red + (size_t) lane * 16;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const float4 t4 = *(const float4 *) (src + 4 * q);
-            y[4 * q] = t4.x; y[4 * q + 1] = t4.y; y[4 * q + 2] = t4.z; y[4 * q + 3] = t4.w;
-        }
-    }
-    for (int v = 1; v < ((ABL & 4) ? 1 : S); v++) {
-        const float * src = red + ((size_t) v * 64 + lane) * 16;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const float4 t4 = *(const float4 *) (src + 4 * q);
-            y[4 * q] = y[4 * q] + t4.x; y[4 * q + 1] = y[4 * q + 1] + t4.y;
-            y[4 * q + 2] = y[4 * q + 2] + t4.z; y[4 * q + 3] = y[4 * q + 3] + t4.w;
-        }
-    }
-    const int64_t n = n0 + r;
-    if (n >= N) return;
-#pragma unroll
-    for (int el = 0; el < 16; el++) {
-        const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * h;
-        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y[el];
+    // The 1024 outputs of the tile are folded by all S waves together: output o = 64 (w + S i) +
+    // lane is accumulator element el = o % 16 of lane lo = o / 16; its terms (one per superblock =
+    // per wave) are combined in the canonical order (cfold). Reads red[v][lo][el]: 64 consecutive
+    // floats per wave-load.
+    const int gs = cfold_gs(S);
+    for (int o = 64 * w + lane; o < 1024; o += 64 * S) {
+        const int lo = o >> 4, el = o & 15;
+        const float * src = red + (size_t) lo * 16 + el;
+        float y = 0.0f, gsum = 0.0f;
+        for (int v = 0; v < ((ABL & 4) ? 1 : S); v++) cfold(gsum, y, src[(size_t) v * 64 * 16], v, gs, S);
+        if (ABL & 4) y = gsum;
+        // element el of lane lo = prompt column c0 + (el & 3) + 8 (el >> 2) + 4 (lo >> 5), row n0 + lo % 32
+        const int64_t n = n0 + (lo & 31);
+        const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * (lo >> 5);
+        if (n < N && c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y;
     }
 }
 
@@ -826,8 +844,8 @@ __global__ __launch_bounds__(1024) void k_mmqd1(const uint8_t * __restrict__ W, 
 // accumulator element e of a lane is prompt column 4 g + e, weight row i. Same exact T / U and
 // the same fold as every kernel of this file: bit-identical.
 template <int TYPE>
-__global__ __launch_bounds__(1024) void k_mmqd16(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N, mi_act_mmx act,
-                                                float * __restrict__ dst, size_t ycol) {
+__global__ __launch_bounds__(1024) void k_mmqd16(mi_mmx_group grp) {
+    MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
     constexpr int NP = F::NP;
     extern __shared__ __attribute__((aligned(16))) float red[];  // [wave][lane][4] terms, then [wave][16] da
@@ -836,7 +854,7 @@ __global__ __launch_bounds__(1024) void k_mmqd16(const uint8_t * __restrict__ W,
     const int64_t ncols = act.ncols;
     const int S = (int) (K / 256);  // == waves of the workgroup
     const int64_t nrt = (N + 15) / 16;
-    const int64_t n0 = (blockIdx.x % nrt) * 16, c0 = (blockIdx.x / nrt) * 16;
+    const int64_t n0 = (mmx_tile % nrt) * 16, c0 = (mmx_tile / nrt) * 16;
     const int sb = w;
 
     const int nrows = (int) std::min<int64_t>(16, N - n0);
@@ -846,8 +864,9 @@ __global__ __launch_bounds__(1024) void k_mmqd16(const uint8_t * __restrict__ W,
     const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
     const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
     const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
-    const uint32_t xstep = (uint32_t) ncols * 64;
-    const uint32_t xcol = acol * 64 + 16 * g + (uint32_t) sb * 4 * xstep;
+    // 64-deep step t of this superblock = 32-deep steps 2 t (lanes g < 2) and 2 t + 1 (g >= 2)
+    const uint32_t xstep = (uint32_t) ncols * 32;
+    const uint32_t xcol = acol * 32 + 16 * (g & 1) + ((uint32_t) sb * 8 + (uint32_t) (g >> 1)) * xstep;
     constexpr uint32_t kQs = F::Q5 ? 48 : 16;
 
     auto ld_w = [&](uint32_t off) -> uint4 { return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wrow + off, 0, 0)); };
@@ -858,7 +877,7 @@ __global__ __launch_bounds__(1024) void k_mmqd16(const uint8_t * __restrict__ W,
     const uint4 qh = F::Q5 ? ld_w(16 + 16 * (g & 1)) : uint4{};
     i32x4 xa[4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) xa[t] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + t * xstep, 0, 0));
+    for (int t = 0; t < 4; t++) xa[t] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol + 2 * t * xstep, 0, 0));
     // U operand: sub-block halves of lanes g < 2 (g >= 2: zero K padding of the 16x16x32 MFMA)
     half8 xu = {};
     {
@@ -925,10 +944,14 @@ __global__ __launch_bounds__(1024) void k_mmqd16(const uint8_t * __restrict__ W,
     }
     mi_lds_barrier();
     if (w != 0) return;
-    float4 y = *(const float4 *) (red + (size_t) lane * 4);
-    for (int v = 1; v < S; v++) {
+    float4 y = {}, gsum = {};
+    const int gs = cfold_gs(S);
+    for (int v = 0; v < S; v++) {
         const float4 t4 = *(const float4 *) (red + ((size_t) v * 64 + lane) * 4);
-        y.x = y.x + t4.x; y.y = y.y + t4.y; y.z = y.z + t4.z; y.w = y.w + t4.w;
+        cfold(gsum.x, y.x, t4.x, v, gs, S);
+        cfold(gsum.y, y.y, t4.y, v, gs, S);
+        cfold(gsum.z, y.z, t4.z, v, gs, S);
+        cfold(gsum.w, y.w, t4.w, v, gs, S);
     }
     const int64_t n = n0 + i;
     if (n >= N) return;
@@ -948,102 +971,114 @@ bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t n
            (int64_t) nb01 * XBM < ((int64_t) 1 << 31);
 }
 
-void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_mmx & act, float * dst,
-                     size_t ycol, hipStream_t s) {
-    const uint8_t * w = (const uint8_t *) W;
-    // short prompts (<= 128 columns): 8 waves per 32 x 32 tile, superblocks round-robin (k_mmqd); long ones:
-    // 64 x 128 tiles with the weights dequantized once per workgroup into LDS (k_mmqx). Both
-    // follow the same canonical combine order, so a prompt's column shards give the whole
-    // prompt's bits whichever kernel runs them (variant bit 128 forces k_mmqx, 16 k_mmqd).
+// tiles of every member for a tile shape of tr rows x tc columns; returns the total
+static int64_t mmx_deal(mi_mmx_group & g, int64_t tr, int64_t tc) {
+    int64_t t = 0;
+    for (int i = 0; i < g.n; i++) {
+        g.m[i].tile_begin = t;
+        t += ((g.m[i].N + tr - 1) / tr) * ((g.m[i].act.ncols + tc - 1) / tc);
+    }
+    return t;
+}
+
+void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
+    if (g.n <= 0) return;
+    const int type = g.type;
+    const int64_t K = g.K;
+    const int64_t ncols = g.m[0].act.ncols;  // every member has the same column count
+    // short prompts (<= 128 columns): pipelined 32 x 32 tiles of 4 waves (k_mmqp; variant bit
+    // 2048: k_mmqd1, a wave per superblock) or, <= 16 columns, 16 x 16 tiles of a wave per
+    // superblock (k_mmqd16); long ones: 64 x 128 tiles with the weights dequantized once per
+    // workgroup into LDS (k_mmqx). All follow the same canonical combine order (cfold), so a
+    // prompt's column shards give the whole prompt's bits whichever kernel runs them (variant bit
+    // 128 forces k_mmqx, 16 the short-prompt kernels).
     const int var = g_mi_tuning.mmq_variant;
-    const bool direct = (var & 16) || (act.ncols <= 128 && !(var & 128));
+    const bool direct = (var & 16) || (ncols <= 128 && !(var & 128));
     if (direct) {
-        const int64_t nrt = (N + 31) / 32, nct = (act.ncols + 31) / 32;
         const int S = (int) (K / 256);
         const int64_t lim16 = (var & (1 << 22)) ? 128 : 16;  // bit 2^22: 16 x 16 tiles up to 128 columns
-        if (S <= 16 && act.ncols <= lim16 && !(var & (2048 | 4096 | (1 << 21)))) {  // 16 x 16 tiles (bit 2^21: k_mmqd1)
-            const dim3 grid16((unsigned) (((N + 15) / 16) * ((act.ncols + 15) / 16)));
+        if (S <= 16 && ncols <= lim16 && !(var & (2048 | 4096 | (1 << 21)))) {  // 16 x 16 tiles (bit 2^21: 32 x 32 tiles)
+            const dim3 grid16((unsigned) mmx_deal(g, 16, 16));
             const size_t lds16 = (size_t) S * 64 * 4 * sizeof(float) + (size_t) S * 16 * sizeof(float);
-            if (type == 12) hipLaunchKernelGGL((k_mmqd16<12>), grid16, dim3(64 * S), lds16, s, w, nb01, K, N, act, dst, ycol);
-            else hipLaunchKernelGGL((k_mmqd16<13>), grid16, dim3(64 * S), lds16, s, w, nb01, K, N, act, dst, ycol);
+            if (type == 12) hipLaunchKernelGGL((k_mmqd16<12>), grid16, dim3(64 * S), lds16, s, g);
+            else hipLaunchKernelGGL((k_mmqd16<13>), grid16, dim3(64 * S), lds16, s, g);
             return;
         }
-        if (S <= 16 && !(var & 2048)) {  // one round: a wave per superblock (variant bit 2048: k_mmqd)
-            const dim3 grid((unsigned) (nrt * nct));
+        const dim3 grid((unsigned) mmx_deal(g, 32, 32));
+        if (S <= 16 && (var & 2048)) {  // one round: a wave per superblock (variant bit 2048: k_mmqd1)
             const size_t lds = (size_t) S * 64 * 16 * sizeof(float) + (size_t) S * 32 * sizeof(float);
-            const int abl = (var >> 12) & 15;
+            // ABL bits 1..8 from variant bits 12..15, 16 from bit 23
+            const int abl = ((var >> 12) & 15) | (((var >> 23) & 1) << 4);
             if (abl && type == 12) {  // timing ablations (results invalid)
-#define MI_MMQD1A(A) hipLaunchKernelGGL((k_mmqd1<12, A>), grid, dim3(64 * S), lds, s, w, nb01, K, N, act, dst, ycol)
+#define MI_MMQD1A(A) hipLaunchKernelGGL((k_mmqd1<12, A>), grid, dim3(64 * S), lds, s, g)
                 switch (abl) {
                 case 1: MI_MMQD1A(1); break;
                 case 2: MI_MMQD1A(2); break;
                 case 4: MI_MMQD1A(4); break;
                 case 8: MI_MMQD1A(8); break;
                 case 10: MI_MMQD1A(10); break;
+                case 16: MI_MMQD1A(16); break;
                 default: MI_MMQD1A(15); break;
                 }
 #undef MI_MMQD1A
                 return;
             }
-            if (type == 12) hipLaunchKernelGGL((k_mmqd1<12>), grid, dim3(64 * S), lds, s, w, nb01, K, N, act, dst, ycol);
-            else hipLaunchKernelGGL((k_mmqd1<13>), grid, dim3(64 * S), lds, s, w, nb01, K, N, act, dst, ycol);
+            if (type == 12) hipLaunchKernelGGL((k_mmqd1<12>), grid, dim3(64 * S), lds, s, g);
+            else hipLaunchKernelGGL((k_mmqd1<13>), grid, dim3(64 * S), lds, s, g);
             return;
         }
-        const int nwv = std::min(S, 8);  // waves per tile (superblocks dealt round-robin)
-        const dim3 grid((unsigned) (nrt * nct));
-        const size_t lds = (size_t) nwv * 64 * 16 * sizeof(float);
-        const bool c4 = act.ncols % 4 == 0;
-        // weight ring depth (variant bit 256 -> two rounds of lead, default one); bit 512: two
-        // accumulator chains per plane
-#define MI_MMQD(TY, C, P, CHN) hipLaunchKernelGGL((k_mmqd<TY, C, P, 0, CHN>), grid, dim3(64 * nwv), lds, s, w, nb01, K, N, act, dst, ycol)
-#define MI_MMQDA(A) hipLaunchKernelGGL((k_mmqd<12, true, 1, A>), grid, dim3(64 * nwv), lds, s, w, nb01, K, N, act, dst, ycol)
-        if ((var >> 12) & 15) {  // timing ablations (results invalid): Q4_K, ncols % 4 == 0, PF 1
-            switch ((var >> 12) & 15) {
-            case 1: MI_MMQDA(1); break;
-            case 2: MI_MMQDA(2); break;
-            case 4: MI_MMQDA(4); break;
-            case 6: MI_MMQDA(6); break;
-            case 8: MI_MMQDA(8); break;
-            default: MI_MMQDA(15); break;
+        // pipelined 32 x 32 tiles, 4 waves each (k_mmqp): any K
+        bool c4 = true;
+        for (int i = 0; i < g.n; i++) c4 = c4 && g.m[i].act.ncols % 4 == 0;
+        const int pabl = (var >> 12) & 7;  // timing ablations (results invalid): Q4_K, ncols % 4 == 0
+        if (pabl && type == 12 && c4) {
+            switch (pabl) {
+            case 1: hipLaunchKernelGGL((k_mmqp<12, true, 1>), grid, dim3(256), 0, s, g); break;
+            case 2: hipLaunchKernelGGL((k_mmqp<12, true, 2>), grid, dim3(256), 0, s, g); break;
+            case 3: hipLaunchKernelGGL((k_mmqp<12, true, 3>), grid, dim3(256), 0, s, g); break;
+            case 4: hipLaunchKernelGGL((k_mmqp<12, true, 4>), grid, dim3(256), 0, s, g); break;
+            default: hipLaunchKernelGGL((k_mmqp<12, true, 7>), grid, dim3(256), 0, s, g); break;
             }
-        } else if (var & 256) {
-            if (type == 12) { if (c4) MI_MMQD(12, true, 2, 1); else MI_MMQD(12, false, 2, 1); }
-            else { if (c4) MI_MMQD(13, true, 2, 1); else MI_MMQD(13, false, 2, 1); }
-        } else if (var & 512) {
-            if (type == 12) { if (c4) MI_MMQD(12, true, 1, 2); else MI_MMQD(12, false, 1, 2); }
-            else { if (c4) MI_MMQD(13, true, 1, 2); else MI_MMQD(13, false, 1, 2); }
-        } else {
-            if (type == 12) { if (c4) MI_MMQD(12, true, 1, 1); else MI_MMQD(12, false, 1, 1); }
-            else { if (c4) MI_MMQD(13, true, 1, 1); else MI_MMQD(13, false, 1, 1); }
+            return;
         }
-#undef MI_MMQD
-#undef MI_MMQDA
+        if (type == 12) { if (c4) hipLaunchKernelGGL((k_mmqp<12, true>), grid, dim3(256), 0, s, g); else hipLaunchKernelGGL((k_mmqp<12, false>), grid, dim3(256), 0, s, g); }
+        else { if (c4) hipLaunchKernelGGL((k_mmqp<13, true>), grid, dim3(256), 0, s, g); else hipLaunchKernelGGL((k_mmqp<13, false>), grid, dim3(256), 0, s, g); }
         return;
     }
-    const int64_t nrt = (N + XBM - 1) / XBM;
     // half-width workgroups (two per CU) when full-width tiles would leave CUs idle: Q4_K B=256
     // 27.8 -> 26.4 us (B=512 41.7 vs 34.7 us: the per-workgroup dequantization then doubles)
-    const bool half = (var & 65536) || (type == 12 && nrt * ((act.ncols + XBN - 1) / XBN) < 256 && !(var & 131072));
+    int64_t full_tiles = 0;
+    for (int i = 0; i < g.n; i++) full_tiles += ((g.m[i].N + XBM - 1) / XBM) * ((g.m[i].act.ncols + XBN - 1) / XBN);
+    const bool half = (var & 65536) || (type == 12 && full_tiles < 256 && !(var & 131072));
     if (half) {
-        const dim3 grid4((unsigned) (nrt * ((act.ncols + 63) / 64)));
-        if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, w, nb01, K, N, act, dst, ycol);
-        else hipLaunchKernelGGL((k_mmqx<13, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, w, nb01, K, N, act, dst, ycol);
+        const dim3 grid4((unsigned) mmx_deal(g, XBM, 64));
+        if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, g);
+        else hipLaunchKernelGGL((k_mmqx<13, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, g);
         return;
     }
-    const int64_t nct = (act.ncols + XBN - 1) / XBN;
-    const dim3 grid((unsigned) (nrt * nct));
-    // weight ring depth LEAD (variant bits: 32 -> 2, 64 -> 1; default 4). (Fully unrolling the
-    // stage loop for K = 4096, SCT = 16, spills: the compiler hoists loads across stages.)
-#define MI_MMQX_T(TY, LD) hipLaunchKernelGGL((k_mmqx<TY, false, 0, LD, 0>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol)
-    const int lead = (var & 64) ? 1 : (var & 32) ? 2 : 4;
+    const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));
+    // weight ring depth LEAD (variant bits: 64 -> 1, default 4). (Fully unrolling the stage loop
+    // for K = 4096, SCT = 16, spills: the compiler hoists loads across stages.)
+#define MI_MMQX_T(TY, LD) hipLaunchKernelGGL((k_mmqx<TY, false, 0, LD, 0>), grid, dim3(512), 0, s, g)
+    const int lead = (var & 64) ? 1 : 4;
     if (var & 1024) {  // timing stamps (results invalid)
-        if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false, 8, 4, 0>), grid, dim3(512), 0, s, w, nb01, K, N, act, dst, ycol);
+        if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false, 8, 4, 0>), grid, dim3(512), 0, s, g);
         return;
     }
     if (type == 12) {
-        if (lead == 1) MI_MMQX_T(12, 1); else if (lead == 2) MI_MMQX_T(12, 2); else MI_MMQX_T(12, 4);
+        if (lead == 1) MI_MMQX_T(12, 1); else MI_MMQX_T(12, 4);
     } else {
-        if (lead == 1) MI_MMQX_T(13, 1); else if (lead == 2) MI_MMQX_T(13, 2); else MI_MMQX_T(13, 4);
+        if (lead == 1) MI_MMQX_T(13, 1); else MI_MMQX_T(13, 4);
     }
 #undef MI_MMQX_T
+}
+
+void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_mmx & act, float * dst,
+                     size_t ycol, hipStream_t s) {
+    mi_mmx_group g;
+    g.type = type;
+    g.n = 1;
+    g.K = K;
+    g.m[0] = mi_mmx_member{W, nb01, N, act, dst, ycol, 0};
+    mi_mul_mat_mmqx_group(g, s);
 }

@@ -1,0 +1,12 @@
+#!/bin/bash
+# k_mmqp ablations at B=64 (single and grouped), events then kernel trace
+set -eo pipefail
+TAG=${1:-r03f}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export PF_TYPES=q4_K PF_R=32 MMQ_VARIANTS=0,4096,8192,12288,16384,28672
+timeout -k 10 200 python3 -u tools/prefill_bench.py 64 2>&1 | grep -v amdgpu.ids | tee "$OUT/pf.txt"
+timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/pf" -o run --output-format csv -- python3 tools/prefill_bench.py 64 > "$OUT/pf_prof.txt" 2> "$OUT/pf_prof.err"
+find "$OUT/pf" -name '*kernel_trace.csv' -exec cp {} "$OUT/pf_kernel_trace.csv" \;
+python3 tools/ktrace.py "$OUT/pf_kernel_trace.csv"

@@ -19,14 +19,24 @@ for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
       for var in VARS:
         lib.ggml_backend_mi355x_set_tuning(b"mmq_variant", var)
         t = bench.TYPE_NAMES[tname]
-        wl = bench.MulMatWorkload(lib, be, t, 4096, 4096, B, 8)
+        R = int(os.environ.get("PF_R", "8"))  # weight copies per step (36 x 9.4 MB > the 256 MB Infinity Cache)
+        wl = bench.MulMatWorkload(lib, be, t, 4096, 4096, B, R)
         for _ in range(3):
             wl.step()
         ms = np.median([bench.event_time_per_step(torch, wl, sp, iters=5) for _ in range(3)])
         torch.cuda.synchronize()
+        # the same mul_mat, one per graph (R graphs round-robin: no grouping across mul_mats)
+        ms1 = float("nan")
+        if os.environ.get("PF_SINGLE", "1") != "0":
+            one = bench.RotatedSingle(lib, be, t, 4096, 4096, B, R)
+            for _ in range(R):
+                one.step()
+            ms1 = np.median([bench.event_time_per_step(torch, one, sp, iters=4 * R) for _ in range(3)])
+            one.free()
         y = G.tensor_get(lib, wl.y[0])
         ref = refs.setdefault((tname, B), y)
         same = "bit-equal to the first variant" if np.array_equal(y.view(np.uint32), ref.view(np.uint32)) else "DIFFERS from the first variant"
-        print(f"{tname:5s} B={B:4d} var={var:5d}: {ms * 1e3 / 8:8.2f} us/mul_mat  {2 * 4096 * 4096 * B * 8 / (ms / 1e3) / 1e12:7.1f} TFLOP/s  {same}")
+        print(f"{tname:5s} B={B:4d} var={var:5d} R={R}: {ms * 1e3 / R:8.2f} us/mul_mat in a graph of {R}  {2 * 4096 * 4096 * B * R / (ms / 1e3) / 1e12:7.1f} TFLOP/s  "
+              f"| one per graph {ms1 * 1e3:8.2f} us  {same}")
         wl.free()
 lib.ggml_backend_free(be)
