@@ -518,9 +518,10 @@ static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
             return true;
         case GGML_OP_MUL_MAT: {
             if (!mm_src0_supported(a->type)) return false;
-            if (b->type != GGML_TYPE_F32) return false;
-            if (a->nb[0] != ggml_type_size(a->type) || b->nb[0] != sizeof(float)) return false;
-            if (a->type == GGML_TYPE_F16 && (a->ne[0] % 8 != 0 || a->nb[1] % 16 != 0)) return false;
+            // src1 F32, or src1 already of the weight's vec_dot_type (the reference CPU's rule,
+            // ggml-backend.c:822-837: F16 x F16 reads src1 as it lies)
+            if (b->type != GGML_TYPE_F32 && !(b->type == GGML_TYPE_F16 && a->type == GGML_TYPE_F16)) return false;
+            if (a->nb[0] != ggml_type_size(a->type) || b->nb[0] != ggml_type_size(b->type)) return false;
             return true;
         }
         case GGML_OP_ADD:
@@ -640,7 +641,7 @@ static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, in
     if (kind == 8) {
         mi_quantize_q8_K_mmx(x, K, mi_act_mmx_carve(dev, K, ncols), ctx->stream);
     } else if (kind == 2 || kind == 5) {
-        mi_convert_f16(x, K, (uint16_t *) dev, ctx->stream, kind == 5);
+        mi_convert_f16(x, K, (uint16_t *) dev, ctx->stream, kind == 5, src1->type == GGML_TYPE_F16);
     } else if (kind >= 3) {
         mi_quantize_expand_f16(x, K, ncols, kind == 4 || kind == 7, (uint16_t *) dev, ctx->stream, kind >= 6);
     } else {
@@ -691,9 +692,9 @@ static int mm_act_kind(const mi_mm_desc & m, const ggml_tensor * src1) {
 // (op_mul_mat_split) each device's row slice.
 static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const void * W, int64_t N, const ggml_tensor * src1,
                         float * out, size_t nb1, size_t nb2, size_t nb3) {
-    MI_ASSERT(src1->type == GGML_TYPE_F32);
+    MI_ASSERT(src1->type == GGML_TYPE_F32 || (src1->type == GGML_TYPE_F16 && src0->type == GGML_TYPE_F16));
     MI_ASSERT(src0->nb[0] == ggml_type_size(src0->type));
-    MI_ASSERT(src1->nb[0] == sizeof(float));
+    MI_ASSERT(src1->nb[0] == ggml_type_size(src1->type));
     MI_ASSERT(src0->ne[0] == src1->ne[0]);
     MI_ASSERT(src1->ne[2] % src0->ne[2] == 0 && src1->ne[3] % src0->ne[3] == 0);
 

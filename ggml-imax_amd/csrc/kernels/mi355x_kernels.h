@@ -43,8 +43,9 @@ mi_act_q8 mi_act_q8_carve(void * base, int64_t K, int64_t ncols, bool is_q8K);
 
 void mi_quantize_q8_0(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s);
 void mi_quantize_q8_K(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s);
-// blocked: write the GEMM's K-blocked layout [K/16][ncols][16] instead of [ncols][K]
-void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s, bool blocked = false);
+// blocked: write the GEMM's K-blocked layout [K/16][ncols][16] instead of [ncols][K];
+// src_f16: the columns are f16 already (copied, not rounded)
+void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s, bool blocked = false, bool src_f16 = false);
 // quantize to q8_K / q8_0 exactly as above and store f16(d * q) as [ncols][K] (no q8 blocks):
 // the activation operand of mi_mul_mat_mmq for quantized weights
 void mi_quantize_expand_f16(const mi_src_cols & x, int64_t K, int64_t ncols, bool is_q8K, uint16_t * xh, hipStream_t s,

@@ -67,10 +67,12 @@ __device__ __forceinline__ float mmqx_term(int T, float U, float dw, float dm, f
 
 // The canonical combine order of an output's superblock terms, shared by every kernel of this
 // file (so any column shard of a prompt gives the same bits whichever kernel computes it): the S
-// superblocks form 4 contiguous groups of gs = ceil(S / 4) (the last ones shorter or empty), each
-// group's terms are left-folded (g = t_first; g = g + t; ...), then the group sums are
-// left-folded (y = g_0; y = y + g_1; ...). A pipelined kernel gives each group to one wave.
-__host__ __device__ constexpr int cfold_gs(int S) { return (S + 3) / 4; }
+// superblocks form kCfoldGroups contiguous groups of gs = ceil(S / kCfoldGroups) (the last ones
+// shorter or empty), each group's terms are left-folded (g = t_first; g = g + t; ...), then the
+// group sums are left-folded (y = g_0; y = y + g_1; ...). The pipelined kernel (k_mmqp) gives each
+// group to one of its waves.
+constexpr int kCfoldGroups = 8;
+__host__ __device__ constexpr int cfold_gs(int S) { return (S + kCfoldGroups - 1) / kCfoldGroups; }
 // term t of superblock sb (terms arrive in superblock order): g / y updated in place
 __device__ __forceinline__ void cfold(float & g, float & y, float t, int sb, int gs, int S) {
     const int pos = sb % gs;
@@ -540,167 +542,227 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
 }
 
 
-// ---- short prompts, pipelined: 4 waves per 32 x 32 tile, one superblock group each --------------
-// A workgroup computes one tile of 32 weight rows x 32 prompt columns; wave w computes the terms of
-// superblock group w of the canonical order (cfold: the S superblocks in 4 contiguous groups) one
-// superblock after the other and left-folds them in registers, with the next superblock's weights
-// and activation fragments requested before the current one's MFMAs (a register double buffer:
-// the load of superblock s + 1 streams under the MFMAs of s). The 4 group sums meet in LDS and
-// are folded by all 4 waves at once. Two workgroups per CU (<= 256 VGPRs: two waves per SIMD), so
-// one workgroup's loads also overlap the other's MFMAs / VALU, and a grouped launch (many members'
-// tiles in one grid) streams tile after tile through every CU.
-// MFMA orientation as k_mmqd1: A = activation fragment (accumulator row = prompt column), B =
-// the dequantized weight planes (accumulator column = the lane's own weight row r), so every lane
-// dequantizes its row from the 16-byte loads it issued and applies its row's d / dmin.
-// C4: every member has ncols % 4 == 0 (the four da of an accumulator row group: one 16-byte load)
-// ABL (timing ablations, results invalid): 1 weight loads addressed as a tile-major repacked
-// layout (a wave's superblocks of its 32 rows contiguous, [chunk][row] 16-byte chunks), 2 every
-// superblock reuses the activation bytes of the wave's first one (no further activation
-// traffic), 4 no MFMAs
-template <int TYPE, bool C4, int ABL = 0>
-__global__ __launch_bounds__(256, 2) void k_mmqp(mi_mmx_group grp) {
+// ---- short prompts, pipelined: 8 waves per tile, one superblock group each -----------------------
+// A workgroup computes one tile of 32 weight rows x 32 NC prompt columns; wave w computes the terms
+// of superblock group w of the canonical order (cfold: kCfoldGroups = 8 contiguous groups) one
+// superblock after the other and left-folds them in registers. The weights of the next superblock
+// are requested before the current one's MFMAs (register double buffer); each 32-deep activation
+// fragment of the next superblock is requested into the register its step has just consumed. The
+// 8 group sums meet in LDS and are folded by the whole workgroup. With NC = 2 a wave's dequantized
+// weight planes feed two column tiles (half the dequantization VALU per MFMA).
+// VALU economy: the plane factors of all 8 sub-blocks come from 2 SWAR extractions of the header's
+// scale bytes (one bit-field extract per factor), loads advance by a wave-uniform SGPR offset (no
+// per-load address VALU), and the activation scales travel as one float per lane through a
+// wave-private LDS row.
+// MFMA orientation as k_mmqd1: A = activation fragment (accumulator row = prompt column), B = the
+// dequantized weight planes (accumulator column = the lane's own weight row r).
+// NW = 4: two workgroups per CU (<= 256 VGPRs at two waves per SIMD), each wave computing groups
+// w and w + 4 one after the other (each group's sum goes to LDS when it ends).
+template <int TYPE, int NC, int NW, int ABL = 0>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
     constexpr int NP = F::NP;
-    __shared__ __attribute__((aligned(16))) float red[4 * 16 * 64];  // [wave][el][lane] group sums
+    constexpr int NE = 16 * NC;  // accumulator elements per lane
+    constexpr int NG = kCfoldGroups / NW;  // groups per wave
+    __shared__ __attribute__((aligned(16))) float red[kCfoldGroups * NE * 64];  // [group][el][lane] group sums
+    __shared__ __attribute__((aligned(16))) float dal[NW][32 * NC];              // per-wave da row
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
     const int64_t ncols = act.ncols;
     const int S = (int) (K / 256);
     const int gs = cfold_gs(S);
-    const int sb0 = w * gs, sb1 = min(S, sb0 + gs);  // this wave's superblock group (may be empty)
+    // this wave's superblocks: groups w, w + NW, ... -> the list [g gs, min(S, (g + 1) gs)) of each
+    auto gbeg = [&](int i) { return min(S, (w + NW * i) * gs); };
+    auto gend = [&](int i) { return min(S, (w + NW * i + 1) * gs); };
+    const int nsb = [&] { int n = 0; for (int i = 0; i < NG; i++) n += gend(i) - gbeg(i); return n; }();
+    // the wave's k-th superblock (clamped to its last one)
+    auto sb_at = [&](int k) {
+        k = min(k, nsb - 1);
+#pragma unroll
+        for (int i = 0; i < NG; i++) {
+            const int len = gend(i) - gbeg(i);
+            if (k < len) return gbeg(i) + k;
+            k -= len;
+        }
+        return S - 1;
+    };
     const int64_t nrt = (N + 31) / 32;
-    const int64_t n0 = (mmx_tile % nrt) * 32, c0 = (mmx_tile / nrt) * 32;
+    const int64_t n0 = (mmx_tile % nrt) * 32, c0 = (mmx_tile / nrt) * (32 * NC);
 
     const int nrows = (int) std::min<int64_t>(32, N - n0);
     const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
-    const uint32_t wrow = (uint32_t) (min(r, nrows - 1) * nb01);
-    const uint32_t acol = (uint32_t) std::min<int64_t>(c0 + r, ncols - 1);
     const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
     const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
     const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
-    const uint32_t xstep = (uint32_t) ncols * 32;
-    const uint32_t xcol = acol * 32 + 16 * h;
     constexpr uint32_t kQs = F::Q5 ? 48 : 16;
+    // lane-constant parts of every offset; the superblock / step advance is an SGPR
+    const uint32_t wv = (uint32_t) (min(r, nrows - 1) * nb01);
+    uint32_t acol[NC];
+#pragma unroll
+    for (int t = 0; t < NC; t++) acol[t] = (uint32_t) std::min<int64_t>(c0 + 32 * t + r, ncols - 1);
+    const uint32_t xstep = (uint32_t) ncols * 32;
 
-    struct Ops {
+    auto ld = [](__amdgpu_buffer_rsrc_t res, uint32_t voff, uint32_t soff) -> uint4 {
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(res, voff, soff, 0));
+    };
+    struct Wt {
         uint4 hdr, q4[4], qh;
-        i32x4 xa[8];
-        half8 xu;
-        float4 da[4];
     };
-    auto ld = [](__amdgpu_buffer_rsrc_t res, uint32_t off) -> uint4 { return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(res, off, 0, 0)); };
-    // weights first (HBM), then the activation fragments (L2)
-    auto load = [&](Ops & o, int sb) {
-        if constexpr ((ABL & 1) != 0) {
-            const uint32_t tb = (uint32_t) sb * 32 * F::BS;  // tile-major: [sb][chunk][row]
-            o.hdr = ld(wres, tb + (uint32_t) r * 16);
+    auto load_w = [&](Wt & o, int sb) {
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * F::BS);
+        o.hdr = ld(wres, wv, so);
 #pragma unroll
-            for (int p = 0; p < 4; p++) o.q4[p] = ld(wres, tb + (uint32_t) ((1 + 2 * p + h) * 32 + r) * 16);
-        } else {
-            const uint32_t wb = wrow + (uint32_t) sb * F::BS;
-            o.hdr = ld(wres, wb);
-#pragma unroll
-            for (int p = 0; p < 4; p++) o.q4[p] = ld(wres, wb + kQs + 32 * p + 16 * h);
-            if constexpr (F::Q5) o.qh = ld(wres, wb + 16 + 16 * h);
-        }
-        const int sbx = (ABL & 2) ? sb0 : sb;
-#pragma unroll
-        for (int kk = 0; kk < 8; kk++) o.xa[kk] = __builtin_bit_cast(i32x4, ld(xres, xcol + ((uint32_t) sbx * 8 + kk) * xstep));
-        o.xu = __builtin_bit_cast(half8, ld(ures, ((uint32_t) sb * (uint32_t) ncols + acol) * 32 + 16 * h));
-        // da of accumulator elements 4 g .. 4 g + 3: prompt columns c0 + 8 g + 4 h + 0..3 (columns
-        // past ncols read another superblock's scales or, past the buffer, zeros: never stored)
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const uint32_t off = (uint32_t) ((int64_t) sb * ncols + c0 + 8 * g + 4 * h) * 4;
-            if constexpr (C4) {
-                o.da[g] = __builtin_bit_cast(float4, ld(dres, off));
-            } else {
-                o.da[g] = make_float4(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off, 0, 0)),
-                                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 4, 0, 0)),
-                                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 8, 0, 0)),
-                                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, off + 12, 0, 0)));
-            }
-        }
+        for (int p = 0; p < 4; p++) o.q4[p] = ld(wres, wv + kQs + 32 * p + 16 * h, so);
+        if constexpr (F::Q5) o.qh = ld(wres, wv + 16 + 16 * h, so);
     };
-    f32x16 gsum = {};
-    // the superblock's exact T (plane MFMAs) and U (f16 MFMA), the canonical term, left-folded
-    auto compute = [&](const Ops & o, const bool first) {
-        const uint32_t w0 = o.hdr.y, w1 = o.hdr.z, w2 = o.hdr.w;
-        const float dw = mi_h2f((uint16_t) (o.hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (o.hdr.x >> 16));
-        i32x16 acc[NP];
-#pragma unroll
-        for (int kk = 0; kk < 8; kk++) {
-            const int jj = kk & 3;
-            const uint32_t sc = kk < 4 ? ((w0 >> (8 * jj)) & 63) : (((w2 >> (8 * jj)) & 0xF) | (((w0 >> (8 * jj + 6)) & 3) << 4));
-            const uint4 q = o.q4[kk >> 1];
-            uint32_t v[4] = {q.x, q.y, q.z, q.w};
-            const uint32_t hb[4] = {o.qh.x, o.qh.y, o.qh.z, o.qh.w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                v[e] = (kk & 1) ? (v[e] >> 4) & 0x0F0F0F0Fu : v[e] & 0x0F0F0F0Fu;
-                if constexpr (F::Q5) v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
-            }
-#pragma unroll
-            for (int p = 0; p < NP; p++) {
-                uint32_t f = F::factor((int) sc, p);
-                f |= f << 16;
-                const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
-                if constexpr ((ABL & 4) != 0) acc[p][kk] = (kk == 0 ? 0 : acc[p][kk]) + o.xa[kk][0] * b[0];
-                else acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.xa[kk], b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
-            }
-        }
-        half8 mu;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int j = 4 * h + q;  // this lane's k-halves of the U MFMA: sub-blocks 4h .. 4h + 3
-            const int jj = j & 3;
-            const uint32_t m = j < 4 ? ((w1 >> (8 * jj)) & 63) : (((w2 >> (8 * jj + 4)) & 0xF) | (((w1 >> (8 * jj + 6)) & 3) << 4));
-            mu[2 * q] = (_Float16) (float) m;
-            mu[2 * q + 1] = (_Float16) (float) (64 * m);
-        }
-        const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(o.xu, mu, f32x16{}, 0, 0, 0);
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const float dav[4] = {o.da[g].x, o.da[g].y, o.da[g].z, o.da[g].w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int el = 4 * g + e;
-                int T = acc[NP - 1][el];
-#pragma unroll
-                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
-                const float term = mmqx_term(T, Uv[el], dw, dm, dav[e]);
-                gsum[el] = first ? term : gsum[el] + term;
-            }
-        }
+    auto ld_x = [&](int sb, int kk, int t) -> i32x4 {
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((sb * 8 + kk) * (int) xstep);
+        return __builtin_bit_cast(i32x4, ld(xres, acol[t] * 32 + 16 * h, so));
     };
-    // superblocks sb0 .. sb1 - 1, two register sets alternating; every load unconditional (the
-    // superblock index clamped into the group: a past-the-end prefetch re-reads the last one)
-    if (sb0 < sb1) {
-        Ops a, b;
-        load(a, sb0);
-        for (int sb = sb0; sb < sb1; sb += 2) {
-            load(b, min(sb + 1, sb1 - 1));
-            compute(a, sb == sb0);
-            if (sb + 1 >= sb1) break;
-            load(a, min(sb + 2, sb1 - 1));
-            compute(b, false);
-        }
+    auto ld_u = [&](int sb, int t) -> half8 {
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * (int) ncols * 32);
+        return __builtin_bit_cast(half8, ld(ures, acol[t] * 32 + 16 * h, so));
+    };
+    auto ld_d = [&](int sb, int t) -> float {
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * (int) ncols * 4);
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, acol[t] * 4, so, 0));
+    };
+
+    f32x16 gsum[NC];
 #pragma unroll
-        for (int el = 0; el < 16; el++) red[(w * 16 + el) * 64 + lane] = gsum[el];
+    for (int t = 0; t < NC; t++) gsum[t] = f32x16{};
+    if (nsb > 0) {
+        Wt wt[2];
+        i32x4 xa[NC][8];
+        half8 xu[NC];
+        float da[NC];
+        const int sbf = sb_at(0);
+        load_w(wt[0], sbf);
+#pragma unroll
+        for (int t = 0; t < NC; t++) {
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) xa[t][kk] = ld_x(sbf, kk, t);
+            xu[t] = ld_u(sbf, t);
+            da[t] = ld_d(sbf, t);
+        }
+        // the wave's k-th superblock: `cur` holds its weights; the next one's loads are issued as
+        // the registers free up (weights into `nxt` first, activations step by step)
+        auto step = [&](const Wt & cur, Wt & nxt, const int k) {
+            const int sb = sb_at(k);
+            const int sn = sb_at(k + 1);  // clamped: a past-the-end prefetch re-reads the last one
+            const bool first = sb % gs == 0, last = sb % gs == gs - 1 || sb == S - 1;
+            load_w(nxt, sn);
+            const uint32_t w0 = cur.hdr.y, w1 = cur.hdr.z, w2 = cur.hdr.w;
+            // the 6-bit scales of sub-blocks 0..3 / 4..7 as bytes (get_scale_min_k4)
+            const uint32_t sca = w0 & 0x3F3F3F3Fu;
+            const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
+            const float dw = mi_h2f((uint16_t) (cur.hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (cur.hdr.x >> 16));
+            i32x16 acc[NC][NP];
+            uint32_t lo[4], hi[4];
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) {
+                if ((kk & 1) == 0) {
+                    const uint4 q = cur.q4[kk >> 1];
+                    const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        lo[e] = qv[e] & 0x0F0F0F0Fu;
+                        hi[e] = (qv[e] >> 4) & 0x0F0F0F0Fu;
+                    }
+                }
+                uint32_t v[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    v[e] = (kk & 1) ? hi[e] : lo[e];
+                    if constexpr (F::Q5) {
+                        const uint32_t hb[4] = {cur.qh.x, cur.qh.y, cur.qh.z, cur.qh.w};
+                        v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
+                    }
+                }
+                const uint32_t scw = kk < 4 ? sca : scb;
+#pragma unroll
+                for (int p = 0; p < NP; p++) {
+                    // plane factor: Q4_K sc = 8 hi3 + lo3; Q5_K sc = 16 f2 + 4 f1 + f0
+                    const uint32_t f = __builtin_amdgcn_ubfe(scw, 8 * (kk & 3) + (F::Q5 ? 2 * p : 3 * p), F::Q5 ? 2 : 3);
+                    const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+#pragma unroll
+                    for (int t = 0; t < NC; t++) {
+                        if constexpr ((ABL & 4) != 0) acc[t][p][kk] = (kk == 0 ? 0 : acc[t][p][kk]) + xa[t][kk][0] * b[0];
+                        else acc[t][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[t][kk], b, kk == 0 ? i32x16{} : acc[t][p], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < NC; t++) xa[t][kk] = ld_x(sn, kk, t);
+            }
+            // U on the f16 MFMA: A = [S & 63, S >> 6] of the lane's column, B = [m, 64 m] of its row
+            const uint32_t ma = w1 & 0x3F3F3F3Fu;
+            const uint32_t mb = ((w2 >> 4) & 0x0F0F0F0Fu) | ((w1 >> 2) & 0x30303030u);
+            const uint32_t mw = h ? mb : ma;  // this lane's k-halves: sub-blocks 4h .. 4h + 3
+            half8 mu;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t m = (mw >> (8 * q)) & 0xFF;
+                mu[2 * q] = (_Float16) (float) m;
+                mu[2 * q + 1] = (_Float16) (float) (64 * m);
+            }
+            // the activation scales of the tile's columns, redistributed through this wave's LDS row
+            if (h == 0) {
+#pragma unroll
+                for (int t = 0; t < NC; t++) dal[w][32 * t + r] = da[t];
+            }
+            __builtin_amdgcn_wave_barrier();
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+            for (int t = 0; t < NC; t++) {
+                const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu[t], mu, f32x16{}, 0, 0, 0);
+                xu[t] = ld_u(sn, t);
+                da[t] = ld_d(sn, t);
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const float4 d4 = *(const float4 *) &dal[w][32 * t + 8 * g + 4 * h];
+                    const float dav[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const int el = 4 * g + e;
+                        int T = acc[t][NP - 1][el];
+#pragma unroll
+                        for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[t][p][el];
+                        const float term = mmqx_term(T, Uv[el], dw, dm, dav[e]);
+                        gsum[t][el] = first ? term : gsum[t][el] + term;
+                    }
+                }
+            }
+            if (last) {  // the group's sum -> LDS slot of group sb / gs
+                const int grp_i = sb / gs;
+#pragma unroll
+                for (int t = 0; t < NC; t++)
+#pragma unroll
+                    for (int el = 0; el < 16; el++) red[(grp_i * NE + 16 * t + el) * 64 + lane] = gsum[t][el];
+            }
+            __builtin_amdgcn_wave_barrier();  // the LDS row is rewritten by the next superblock
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        };
+        for (int k = 0; k < nsb; k += 2) {
+            step(wt[0], wt[1], k);
+            if (k + 1 >= nsb) break;
+            step(wt[1], wt[0], k + 1);
+        }
     }
     mi_lds_barrier();
-    // the group sums left-folded (canonical order); wave w folds accumulator elements el = w,
-    // w + 4, w + 8, w + 12 of every lane: lanes 0..31 store 32 consecutive rows of one column
+    // the group sums left-folded (canonical order) by the whole workgroup: output o = el 64 + l
+    // (el: accumulator element of tile el / 16, l: lane) -- lanes 0..31 store 32 consecutive rows
     const int ngroups = (S + gs - 1) / gs;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int el = w + 4 * i;
-        float y = red[el * 64 + lane];
-        for (int v = 1; v < ngroups; v++) y = y + red[(v * 16 + el) * 64 + lane];
-        const int64_t n = n0 + r;
-        const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * h;
+    for (int i = 0; i < NE / NW; i++) {
+        const int o = (int) threadIdx.x + 64 * NW * i;
+        const int el = o >> 6, l = o & 63;
+        float y = red[el * 64 + l];
+        for (int v = 1; v < ngroups; v++) y = y + red[(v * NE + el) * 64 + l];
+        const int e = el & 15, t = el >> 4;
+        const int64_t n = n0 + (l & 31);
+        const int64_t c = c0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
         if (n < N && c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y;
     }
 }
@@ -1027,22 +1089,21 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
             else hipLaunchKernelGGL((k_mmqd1<13>), grid, dim3(64 * S), lds, s, g);
             return;
         }
-        // pipelined 32 x 32 tiles, 4 waves each (k_mmqp): any K
-        bool c4 = true;
-        for (int i = 0; i < g.n; i++) c4 = c4 && g.m[i].act.ncols % 4 == 0;
-        const int pabl = (var >> 12) & 7;  // timing ablations (results invalid): Q4_K, ncols % 4 == 0
-        if (pabl && type == 12 && c4) {
-            switch (pabl) {
-            case 1: hipLaunchKernelGGL((k_mmqp<12, true, 1>), grid, dim3(256), 0, s, g); break;
-            case 2: hipLaunchKernelGGL((k_mmqp<12, true, 2>), grid, dim3(256), 0, s, g); break;
-            case 3: hipLaunchKernelGGL((k_mmqp<12, true, 3>), grid, dim3(256), 0, s, g); break;
-            case 4: hipLaunchKernelGGL((k_mmqp<12, true, 4>), grid, dim3(256), 0, s, g); break;
-            default: hipLaunchKernelGGL((k_mmqp<12, true, 7>), grid, dim3(256), 0, s, g); break;
-            }
-            return;
+        // pipelined 32 x 32 tiles, 8 waves each (k_mmqp; variant bit 2^26: 32 x 64 tiles)
+        const int64_t t64 = mmx_deal(g, 32, 64);
+        const int nc = (var & (1 << 26)) ? 2 : 1;  // 64-column tiles spill at present: opt-in only
+        const dim3 gridp((unsigned) (nc == 2 ? t64 : mmx_deal(g, 32, 32)));
+        // 4 waves per tile (two workgroups per CU) unless variant bit 2^27 (8 waves, one per CU)
+        const bool w8 = (var & (1 << 27)) != 0;
+#define MI_MMQP(TY, NCC, NWW) hipLaunchKernelGGL((k_mmqp<TY, NCC, NWW>), gridp, dim3(64 * NWW), 0, s, g)
+        if (type == 12) {
+            if (nc == 2) { if (w8) MI_MMQP(12, 2, 8); else MI_MMQP(12, 2, 4); }
+            else { if (w8) MI_MMQP(12, 1, 8); else MI_MMQP(12, 1, 4); }
+        } else {
+            if (nc == 2) { if (w8) MI_MMQP(13, 2, 8); else MI_MMQP(13, 2, 4); }
+            else { if (w8) MI_MMQP(13, 1, 8); else MI_MMQP(13, 1, 4); }
         }
-        if (type == 12) { if (c4) hipLaunchKernelGGL((k_mmqp<12, true>), grid, dim3(256), 0, s, g); else hipLaunchKernelGGL((k_mmqp<12, false>), grid, dim3(256), 0, s, g); }
-        else { if (c4) hipLaunchKernelGGL((k_mmqp<13, true>), grid, dim3(256), 0, s, g); else hipLaunchKernelGGL((k_mmqp<13, false>), grid, dim3(256), 0, s, g); }
+#undef MI_MMQP
         return;
     }
     // half-width workgroups (two per CU) when full-width tiles would leave CUs idle: Q4_K B=256

@@ -57,9 +57,21 @@ struct ord_geom {
     int64_t col_chunks;
 };
 
+// 8 halves at p: one 16-byte load, or (ALIGNED false: rows of K % 8 != 0 halves, or a weight row
+// stride / base that is not a 16-byte multiple) eight 2-byte loads
+template <bool ALIGNED>
+__device__ __forceinline__ void ld_h8(const uint16_t * p, float (&f)[8]) {
+    if constexpr (ALIGNED) {
+        h8_to_f(*(const uint4 *) p, f);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) f[i] = mi_h2f(p[i]);
+    }
+}
+
 // F16 weights x f16 activation columns (xh: [ncols][K], the CPU's from_float rows).
 // One quad per (row, chunk of NC columns).
-template <int NC>
+template <int NC, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_mmv_f16_ord(const uint8_t * __restrict__ W, const uint16_t * __restrict__ xh,
                                                      float * __restrict__ dst, ord_geom g) {
     const int q = threadIdx.x & 3;
@@ -85,12 +97,12 @@ __global__ __launch_bounds__(256) void k_mmv_f16_ord(const uint8_t * __restrict_
     const int64_t np = g.K & ~(int64_t) 31;
     for (int64_t i = 8 * q; i < np; i += 32) {
         float w[8];
-        h8_to_f(*(const uint4 *) (wrow + i), w);
+        ld_h8<ALIGNED>(wrow + i, w);
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             if (c < nc) {
                 float x[8];
-                h8_to_f(*(const uint4 *) (xh + (col0 + c) * g.K + i), x);
+                ld_h8<ALIGNED>(xh + (col0 + c) * g.K + i, x);
 #pragma unroll
                 for (int l = 0; l < 8; l++) acc[c][l] = __fmaf_rn(w[l], x[l], acc[c][l]);
             }
@@ -829,7 +841,9 @@ ord_geom make_ord_geom(const mi_mm_desc & m, int NC) {
 template <int NC> void launch_f16(const mi_mm_desc & m, const uint16_t * xh, hipStream_t s) {
     const ord_geom g = make_ord_geom(m, NC);
     const dim3 grid((unsigned) ((m.N + kQuadsPerBlock - 1) / kQuadsPerBlock), (unsigned) (g.col_chunks * m.ne12 * m.ne13));
-    hipLaunchKernelGGL(k_mmv_f16_ord<NC>, grid, dim3(256), 0, s, (const uint8_t *) m.W, xh, m.dst, g);
+    const bool aligned = m.K % 8 == 0 && ((uintptr_t) m.W | m.nb01 | m.nb02 | m.nb03 | (uintptr_t) xh) % 16 == 0;
+    if (aligned) hipLaunchKernelGGL((k_mmv_f16_ord<NC, true>), grid, dim3(256), 0, s, (const uint8_t *) m.W, xh, m.dst, g);
+    else hipLaunchKernelGGL((k_mmv_f16_ord<NC, false>), grid, dim3(256), 0, s, (const uint8_t *) m.W, xh, m.dst, g);
 }
 
 } // namespace

@@ -152,11 +152,15 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K(mi_src_cols x, int64_t K,
 }
 
 // grid (column, group of 256 elements)
+// f32 columns rounded to f16 (the CPU's from_float for vec_dot_type F16), or (SRC_F16) f16 columns
+// copied as they are (src1 already of the vec_dot_type: the CPU reads it directly)
+template <bool SRC_F16>
 __global__ __launch_bounds__(256) void k_convert_f16(mi_src_cols x, int64_t K, uint16_t * out, int64_t xh_blk) {
     const int64_t k = (int64_t) blockIdx.y * 256 + threadIdx.x;
     if (k >= K) return;
     const int64_t c = blockIdx.x;
-    out[xh_index(c, k, K, xh_blk)] = mi_f2h(col_ptr(x, (uint32_t) c)[k]);
+    if constexpr (SRC_F16) out[xh_index(c, k, K, xh_blk)] = ((const uint16_t *) col_ptr(x, (uint32_t) c))[k];
+    else out[xh_index(c, k, K, xh_blk)] = mi_f2h(col_ptr(x, (uint32_t) c)[k]);
 }
 
 void mi_quantize_q8_0(const mi_src_cols & x, int64_t K, const mi_act_q8 & act, hipStream_t s) {
@@ -184,9 +188,10 @@ void mi_quantize_expand_f16(const mi_src_cols & x, int64_t K, int64_t ncols, boo
     }
 }
 
-void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s, bool blocked) {
+void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_t s, bool blocked, bool src_f16) {
     const int64_t ncols = x.ne1 * x.ne2 * x.ne3;
     const int64_t xb = blocked ? ncols : 0;
     if (ncols == 0 || K == 0) return;
-    hipLaunchKernelGGL(k_convert_f16, dim3((unsigned) ncols, (unsigned) ((K + 255) / 256)), dim3(256), 0, s, x, K, out, xb);
+    if (src_f16) hipLaunchKernelGGL(k_convert_f16<true>, dim3((unsigned) ncols, (unsigned) ((K + 255) / 256)), dim3(256), 0, s, x, K, out, xb);
+    else hipLaunchKernelGGL(k_convert_f16<false>, dim3((unsigned) ncols, (unsigned) ((K + 255) / 256)), dim3(256), 0, s, x, K, out, xb);
 }

@@ -148,7 +148,7 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
     w = synth.uniform(11, K * N)
     x = synth.uniform(12, K * B)
     wq = orc.quantize(t, w, K)
-    variants = [0, 2048, 128 | 131072, 128 | 65536] + ([1 << 21] if B <= 16 else [])
+    variants = [0, 2048, 1 << 27, 128 | 131072, 128 | 65536] + ([1 << 21] if B <= 16 else [])
     outs = {}
     try:
         for v in variants:

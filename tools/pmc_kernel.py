@@ -24,7 +24,7 @@ def main():
                 name = row.get("Kernel_Name", "")
                 if sub not in name:
                     continue
-                key = (name.split("(")[0][-60:], row["Counter_Name"])
+                key = (name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][-60:], row["Counter_Name"])
                 res.setdefault(key, []).append(float(row.get("Counter_Value", 0) or 0))
     for (k, c), v in sorted(res.items()):
         print(f"{k:60s} {c:32s} n={len(v):4d} mean={sum(v) / len(v):.4g}")
