@@ -590,10 +590,11 @@ static int act_kind(ggml_type wtype) {
 }
 
 // kinds: 0 q8_0, 1 q8_K, 2 f16, 3/4 q8_0/q8_K quants expanded to f16(d * q) (mmq.hip operand),
-// 5/6/7 = 2/3/4 in the GEMM's K-blocked layout [K/16][ncols][16], 8 q8_K in the int8-MFMA
-// layouts of the exact prefill GEMM (mmq_exact.hip)
+// 5/6/7 = 2/3/4 in the GEMM's K-blocked layout [K/16][ncols][16], 8 q8_K / 9 q8_0 in the int8-MFMA
+// layouts of the exact prefill GEMMs (mmq_exact.hip)
 static size_t act_bytes(int kind, int64_t K, int64_t ncols) {
     if (kind == 8) return mi_act_mmx_bytes(K, ncols);
+    if (kind == 9) return mi_act_mmx0_bytes(K, ncols);
     if (kind >= 2) return (size_t) K * ncols * 2;
     return mi_act_q8_bytes(K, ncols, kind == 1);
 }
@@ -638,8 +639,14 @@ static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, in
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
     void * dev = scratch_take(ctx, act_bytes(kind, K, ncols));
     const mi_src_cols x = src_cols(src1);
-    if (kind == 8) {
-        mi_quantize_q8_K_mmx(x, K, mi_act_mmx_carve(dev, K, ncols), ctx->stream);
+    if (kind == 8 || kind == 9) {
+        mi_mmx_qgroup q;
+        q.n = 1;
+        q.K = K;
+        q.m[0].x = x;
+        q.m[0].act = kind == 8 ? mi_act_mmx_carve(dev, K, ncols) : mi_act_mmx0_carve(dev, K, ncols);
+        if (kind == 8) mi_quantize_q8_K_mmx_group(q, ctx->stream);
+        else mi_quantize_q8_0_mmx_group(q, ctx->stream);
     } else if (kind == 2 || kind == 5) {
         mi_convert_f16(x, K, (uint16_t *) dev, ctx->stream, kind == 5, src1->type == GGML_TYPE_F16);
     } else if (kind >= 3) {
@@ -674,16 +681,16 @@ static bool mm_batched(const mi_mm_desc & m, const ggml_tensor * src1) {
 
 // The activation format mul_mat_run converts src1 to for this mul_mat (act_bytes kinds), or -1
 // (F32 weights: src1 is read as it lies). Q4_K / Q5_K prompts: the exact-integer int8 GEMM's
-// layouts (8); other batched types: f16 operands (2 / 3 / 4, K-blocked + 3); decode: q8 SoA
-// (0 / 1) or f16 (2).
+// q8_K layouts (8); Q4_0 / Q8_0 prompts: its q8_0 layouts (9); F16 prompts: f16 operands (2, or
+// K-blocked 5); decode: q8 SoA (0 / 1) or f16 (2).
 static int mm_act_kind(const mi_mm_desc & m, const ggml_tensor * src1) {
     const int kind = act_kind((ggml_type) m.type);
     if (kind < 0) return -1;
     if (!mm_batched(m, src1)) return kind;
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
-    // GGML_MI355X_MMQ_VARIANT bit 2^30 selects the f16 GEMM for K-quants too (A/B timing; the low
-    // bits are mmq_exact.hip's own kernel variants)
-    if (kind == 1 && (g_mi_tuning.mmq_variant & (1 << 30)) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01)) return 8;
+    // GGML_MI355X_MMQ_VARIANT bit 2^30 selects the f16 GEMM for the quantized types too (A/B
+    // timing; the low bits are mmq_exact.hip's own kernel variants)
+    if (kind <= 1 && (g_mi_tuning.mmq_variant & (1 << 30)) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01)) return kind == 1 ? 8 : 9;
     return (kind == 2 ? 2 : kind + 3) + (mi_mmq_wants_blocked() ? 3 : 0);
 }
 
@@ -723,9 +730,10 @@ static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const vo
     } else {
         const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
         void * xa = get_activations(ctx, src1, xkind, m.K);
-        if (xkind == 8) {
-            // Q4_K / Q5_K: the exact-integer int8 MFMA GEMM (mmq_exact.hip)
-            mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, mi_act_mmx_carve(xa, m.K, ncols), m.dst, m.nb1, ctx->stream);
+        if (xkind == 8 || xkind == 9) {
+            // Q4_K / Q5_K / Q4_0 / Q8_0: the exact-integer int8 MFMA GEMMs (mmq_exact.hip)
+            const mi_act_mmx act = xkind == 8 ? mi_act_mmx_carve(xa, m.K, ncols) : mi_act_mmx0_carve(xa, m.K, ncols);
+            mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, act, m.dst, m.nb1, ctx->stream);
         } else if (xkind >= 3 || (xkind == 2 && mm_batched(m, src1))) {
             // the GEMM's activation operand: f16 for F16 weights, else f16(d * q) of the q8 quants
             // written by the quantizer itself (kinds 3/4, K-blocked 5..7)
@@ -1149,7 +1157,8 @@ static size_t graph_scratch_bytes(const ggml_cgraph * cgraph) {
         // q8 blocks and/or their f16 expansion (batched) -- both counted, the choice is made at run time
         total += (act_bytes(kind, b->ne[0], ncols) + kBufferAlign - 1) & ~(kBufferAlign - 1);
         if (ncols > 8) {
-            const size_t big = std::max(act_bytes(kind + 3, b->ne[0], ncols), kind == 1 ? act_bytes(8, b->ne[0], ncols) : 0);
+            const size_t big = std::max(act_bytes(kind + 3, b->ne[0], ncols),
+                                        kind == 1 ? act_bytes(8, b->ne[0], ncols) : kind == 0 ? act_bytes(9, b->ne[0], ncols) : 0);
             total += (big + kBufferAlign - 1) & ~(kBufferAlign - 1);
         }
     }
@@ -1778,14 +1787,15 @@ static int try_fuse_attn_proj(mi_backend_ctx * ctx, ggml_cgraph * g, int i, cons
     return k2;
 }
 
-// a MUL_MAT node that runs on the exact int8 prefill GEMM (Q4_K / Q5_K weights, > 8 plain
-// columns; mm_act_kind 8)
-static bool prefill_mmx_eligible(const ggml_tensor * n) {
-    if (n->op != GGML_OP_MUL_MAT || is_split_tensor(n->src[0])) return false;
+// the activation kind of a MUL_MAT node that runs on an exact int8 prefill GEMM (Q4_K / Q5_K: 8,
+// Q4_0 / Q8_0: 9; > 8 plain columns), or -1
+static int prefill_mmx_kind(const ggml_tensor * n) {
+    if (n->op != GGML_OP_MUL_MAT || is_split_tensor(n->src[0])) return -1;
     const ggml_tensor * a = n->src[0], * b = n->src[1];
-    if (b->type != GGML_TYPE_F32 || a->nb[0] != ggml_type_size(a->type) || b->nb[0] != sizeof(float) || n->nb[0] != sizeof(float)) return false;
-    if (a->ne[0] != b->ne[0]) return false;
-    return mm_act_kind(mm_desc_of(n), b) == 8;
+    if (b->type != GGML_TYPE_F32 || a->nb[0] != ggml_type_size(a->type) || b->nb[0] != sizeof(float) || n->nb[0] != sizeof(float)) return -1;
+    if (a->ne[0] != b->ne[0]) return -1;
+    const int k = mm_act_kind(mm_desc_of(n), b);
+    return k == 8 || k == 9 ? k : -1;
 }
 
 // Batched (prompt) mul_mats that follow each other in the graph and are independent of each other
@@ -1798,7 +1808,8 @@ static bool prefill_mmx_eligible(const ggml_tensor * n) {
 static int run_prefill_group(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
     static const bool no_group = getenv("GGML_MI355X_NO_PREFILL_GROUP") != nullptr;
     ggml_tensor * first = g->nodes[i];
-    if (no_group || !prefill_mmx_eligible(first)) return -1;
+    const int kind = prefill_mmx_kind(first);
+    if (no_group || kind < 0) return -1;
     const ggml_type type = first->src[0]->type;
     const int64_t K = first->src[0]->ne[0];
     auto cols_of = [](const ggml_tensor * n) { return n->src[1]->ne[1] * n->src[1]->ne[2] * n->src[1]->ne[3]; };
@@ -1807,7 +1818,7 @@ static int run_prefill_group(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
     int last = i;
     for (int j = next_node(g, i); j >= 0 && (int) members.size() < kMiMaxPrefillMembers; j = next_node(g, j)) {
         ggml_tensor * n = g->nodes[j];
-        if (!prefill_mmx_eligible(n) || n->src[0]->type != type || n->src[0]->ne[0] != K || cols_of(n) != ncols) break;
+        if (prefill_mmx_kind(n) != kind || n->src[0]->type != type || n->src[0]->ne[0] != K || cols_of(n) != ncols) break;
         bool independent = true;
         for (ggml_tensor * m : members) {
             if (overlaps(n->src[1], m) || overlaps(n->src[0], m) || overlaps(n, m->src[0]) || overlaps(n, m->src[1]) || overlaps(n, m)) {
@@ -1826,17 +1837,18 @@ static int run_prefill_group(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
     std::vector<void *> xa(members.size(), nullptr);
     for (size_t k = 0; k < members.size(); k++) {
         const ggml_tensor * x = members[k]->src[1];
-        xa[k] = find_activations(ctx, x, 8);
+        xa[k] = find_activations(ctx, x, kind);
         if (xa[k]) continue;
-        void * dev = scratch_take(ctx, act_bytes(8, K, ncols));
+        void * dev = scratch_take(ctx, act_bytes(kind, K, ncols));
         q.m[q.n].x = src_cols(x);
-        q.m[q.n].act = mi_act_mmx_carve(dev, K, ncols);
+        q.m[q.n].act = kind == 8 ? mi_act_mmx_carve(dev, K, ncols) : mi_act_mmx0_carve(dev, K, ncols);
         q.n++;
-        cache_activations(ctx, x, 8, dev);
+        cache_activations(ctx, x, kind, dev);
         xa[k] = dev;
     }
     if (q.n > 0) {
-        mi_quantize_q8_K_mmx_group(q, ctx->stream);
+        if (kind == 8) mi_quantize_q8_K_mmx_group(q, ctx->stream);
+        else mi_quantize_q8_0_mmx_group(q, ctx->stream);
         ctx->last_launches++;
     }
     mi_mmx_group gg;
@@ -1845,8 +1857,8 @@ static int run_prefill_group(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
     gg.n = (int) members.size();
     for (size_t k = 0; k < members.size(); k++) {
         const ggml_tensor * n = members[k];
-        gg.m[k] = mi_mmx_member{n->src[0]->data, n->src[0]->nb[1], n->src[0]->ne[1], mi_act_mmx_carve(xa[k], K, ncols), (float *) n->data,
-                                n->nb[1], 0};
+        const mi_act_mmx act = kind == 8 ? mi_act_mmx_carve(xa[k], K, ncols) : mi_act_mmx0_carve(xa[k], K, ncols);
+        gg.m[k] = mi_mmx_member{n->src[0]->data, n->src[0]->nb[1], n->src[0]->ne[1], act, (float *) n->data, n->nb[1], 0};
     }
     mi_mul_mat_mmqx_group(gg, ctx->stream);
     ctx->last_launches++;

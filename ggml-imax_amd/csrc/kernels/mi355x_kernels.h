@@ -160,8 +160,14 @@ struct mi_mmx_qgroup {
     } m[kMiMaxPrefillMembers];
 };
 void mi_quantize_q8_K_mmx_group(mi_mmx_qgroup & q, hipStream_t s);
+// q8_0 activations (Q4_0 / Q8_0 weights) in the MFMA layout: xq [K/32][ncols][32] int8, xd
+// [K/32][ncols] f32 (xu unused) -- the bytes of the AVX2 quantize_row_q8_0, rearranged
+size_t mi_act_mmx0_bytes(int64_t K, int64_t ncols);
+mi_act_mmx mi_act_mmx0_carve(void * base, int64_t K, int64_t ncols);
+void mi_quantize_q8_0_mmx_group(mi_mmx_qgroup & q, hipStream_t s);
 bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t nb01);
-// Independent Q4_K / Q5_K mul_mats (same type, K and activation column count) in one launch:
+// Independent Q4_K / Q5_K (q8_K activations) or Q4_0 / Q8_0 (q8_0 activations, mi_act_mmx0_*)
+// mul_mats (same type, K and activation column count) in one launch:
 // member i = 2-D weights [K, N_i] x act_i.ncols columns -> dst_i (column stride ycol_i bytes)
 struct mi_mmx_member {
     const void * W;

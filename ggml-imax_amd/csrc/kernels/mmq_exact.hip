@@ -165,6 +165,67 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K_mmx(mi_mmx_qgroup q) {
     if (lane == 0) act.xd[b * ncols + c] = d;
 }
 
+// q8_0 activations (Q4_0 / Q8_0 weights) in the same MFMA layout: xq [K/32][ncols][32] int8, xd
+// [K/32][ncols] f32 (the fp16-rounded d). quantize_row_q8_0 as the reference's AVX2 build computes
+// it (src/ggml-quants.c:535-618: amax, d = amax / 127 -> fp16, id = 127 / amax, round-half-even
+// of x * id); one 32-block per half-wave, grid (column, group of 8 blocks).
+__global__ __launch_bounds__(256) void k_quantize_q8_0_mmx(mi_mmx_qgroup q) {
+    const int64_t K = q.K;
+    const int64_t nb_per_col = K / 32;
+    const int64_t b = (int64_t) blockIdx.y * 8 + (threadIdx.x >> 5);
+    const int l = threadIdx.x & 31;
+    if (b >= nb_per_col) return;  // whole half-waves exit together
+    int mi = 0;
+    while (mi + 1 < q.n && (int64_t) blockIdx.x >= q.m[mi + 1].col_begin) mi++;
+    const mi_src_cols x = q.m[mi].x;
+    const mi_act_mmx act = q.m[mi].act;
+    const uint32_t c = (uint32_t) ((int64_t) blockIdx.x - q.m[mi].col_begin);
+    const char * cbase;
+    if (x.ne2 == 1 && x.ne3 == 1) {
+        cbase = x.base + (size_t) c * x.nb1;
+    } else {
+        const uint32_t ne1 = (uint32_t) x.ne1, ne2 = (uint32_t) x.ne2;
+        const uint32_t i1 = c % ne1, i2 = (c / ne1) % ne2, i3 = c / (ne1 * ne2);
+        cbase = x.base + (size_t) i1 * x.nb1 + (size_t) i2 * x.nb2 + (size_t) i3 * x.nb3;
+    }
+    const float v = ((const float *) cbase)[b * 32 + l];
+    float amax = fabsf(v);
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 32));
+    const float d = amax / 127.f;
+    const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+    const float qv = __builtin_rintf(__fmul_rn(v, id));
+    act.xq[(b * act.ncols + c) * 32 + l] = (int8_t) (int) qv;
+    if (l == 0) act.xd[b * act.ncols + c] = mi_h2f(mi_f2h(d));
+}
+
+size_t mi_act_mmx0_bytes(int64_t K, int64_t ncols) {
+    auto al = [](size_t v) { return (v + 255) & ~(size_t) 255; };
+    return al((size_t) K * ncols) + al((size_t) (K / 32) * ncols * 4);
+}
+
+mi_act_mmx mi_act_mmx0_carve(void * base, int64_t K, int64_t ncols) {
+    auto al = [](size_t v) { return (v + 255) & ~(size_t) 255; };
+    char * p = (char *) base;
+    mi_act_mmx a;
+    a.K = K;
+    a.ncols = ncols;
+    a.xq = (int8_t *) p;
+    a.xd = (float *) (p + al((size_t) K * ncols));
+    a.xu = nullptr;
+    return a;
+}
+
+void mi_quantize_q8_0_mmx_group(mi_mmx_qgroup & q, hipStream_t s) {
+    int64_t cols = 0;
+    for (int i = 0; i < q.n; i++) {
+        q.m[i].col_begin = cols;
+        cols += q.m[i].act.ncols;
+    }
+    if (cols == 0 || q.K < 32) return;
+    hipLaunchKernelGGL(k_quantize_q8_0_mmx, dim3((unsigned) cols, (unsigned) ((q.K / 32 + 7) / 8)), dim3(256), 0, s, q);
+}
+
 size_t mi_act_mmx_bytes(int64_t K, int64_t ncols) {
     auto al = [](size_t v) { return (v + 255) & ~(size_t) 255; };
     return al((size_t) K * ncols) + al((size_t) (K / 256) * ncols * 4) + al((size_t) (K / 256) * ncols * 32);
@@ -767,6 +828,393 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
     }
 }
 
+// ---- Q4_0 / Q8_0 prefill: the reference's exact int32 block sums on the int8 matrix cores --------
+// The reference dots (vec_dot_q4_0_q8_0, src/ggml-quants.c:3469-3874, AVX2 :3600-3623;
+// vec_dot_q8_0_q8_0, :4819, AVX2 :4925+) compute, per 32-block b, the exact int32
+// T_b = sum (q_w - 8 | q_w) q_a and combine in f32: acc = fma(fp16(d_w) fp16(d_a), (float) T_b, acc).
+// Here T_b is ONE v_mfma_i32_32x32x32_i8 (the instruction's K is exactly one block) on the weight
+// quants -- Q4_0: the nibble minus 8, by the byte-wise bias trick (q + 0x78) ^ 0x80 (no carry
+// between bytes for q <= 15); Q8_0: the bytes -- and the q8_0 activation quants; per block
+// f = d_w d_a and g = fma(f, T, g). Canonical order of this family: blocks in kCfoldGroups groups of
+// whole 8-block units (gs = ceil(K / 256 / kCfoldGroups) units each), fma-chained in block order
+// from +0 inside a group, the group sums left-folded. Against the reference only that order differs.
+// Workgroup: 4 waves on a tile of 32 weight rows x 32 prompt columns, two per CU; wave w computes
+// groups w and w + 4, unit after unit, the next unit's weight bytes and scales requested into a
+// second register set before the current unit's blocks are processed (Q4_0: the 144-byte unit of
+// the lane's row, nine 16-byte loads, 16-byte aligned at K % 256 == 0; Q8_0: per block the five
+// dwords covering the lane's 16 quant bytes and the scale -- blocks are 2-byte aligned). A block's
+// operand is extracted with v_alignbyte right before its MFMA. Accumulator element el: prompt
+// column c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r (as k_mmqp); the activation scales
+// reach that layout through a wave-private LDS row per block.
+template <bool Q8>
+struct Q0Raw {
+    // Q4_0: the unit's 144 bytes; Q8_0: per block 5 dwords from byte 34 j + 16 h (4-aligned down)
+    uint32_t v[Q8 ? 40 : 36];
+    float da[8];  // this lane's column's activation scales of the unit's 8 blocks
+};
+
+template <bool Q8>
+__global__ __launch_bounds__(256, 2) void k_mmq0p(mi_mmx_group grp) {
+    MI_MMX_MEMBER(grp);
+    constexpr int NW = 4;
+    constexpr int BS = Q8 ? 34 : 18;
+    constexpr int UB = 8 * BS;  // bytes of a row's 8-block unit: 144 / 272
+    constexpr int NG = kCfoldGroups / NW;
+    __shared__ __attribute__((aligned(16))) float red[kCfoldGroups * 16 * 64];  // [group][el][lane]
+    __shared__ __attribute__((aligned(16))) float dal[NW][8][32];                // per-wave da rows
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t ncols = act.ncols;
+    const int S = (int) (K / 256);  // 8-block units
+    const int gs = cfold_gs(S);
+    auto gbeg = [&](int i) { return min(S, (w + NW * i) * gs); };
+    auto gend = [&](int i) { return min(S, (w + NW * i + 1) * gs); };
+    const int nsb = [&] { int n = 0; for (int i = 0; i < NG; i++) n += gend(i) - gbeg(i); return n; }();
+    auto sb_at = [&](int k) {
+        k = min(k, nsb - 1);
+#pragma unroll
+        for (int i = 0; i < NG; i++) {
+            const int len = gend(i) - gbeg(i);
+            if (k < len) return gbeg(i) + k;
+            k -= len;
+        }
+        return S - 1;
+    };
+    const int64_t nrt = (N + 31) / 32;
+    const int64_t n0 = (mmx_tile % nrt) * 32, c0 = (mmx_tile / nrt) * 32;
+    const int nrows = (int) std::min<int64_t>(32, N - n0);
+    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) ((K / 32) * ncols * 4), 0x00020000);
+    const uint32_t wv = (uint32_t) (min(r, nrows - 1) * nb01);
+    const uint32_t acol = (uint32_t) std::min<int64_t>(c0 + r, ncols - 1);
+    const uint32_t xstep = (uint32_t) ncols * 32;
+
+    auto load_unit = [&](Q0Raw<Q8> & o, int u) {
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(u * UB);
+        if constexpr (Q8) {
+            // block j: quants at 34 j + 2 + 16 h .. + 15, scale at 34 j; dwords from 4-aligned 34 j + 16 h - 2 (j odd)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t b0 = (uint32_t) ((BS * j) & ~3);  // 4-aligned start of block j
+                const uint32_t q0 = b0 + 16 * h;                 // this half's first covering dword
+#pragma unroll
+                for (int i = 0; i < 5; i++) o.v[5 * j + i] = __builtin_amdgcn_raw_buffer_load_b32(wres, wv + q0 + 4 * i, so, 0);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 9; i++) {
+                const uint4 x = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wv + 16 * i, so, 0));
+                o.v[4 * i] = x.x; o.v[4 * i + 1] = x.y; o.v[4 * i + 2] = x.z; o.v[4 * i + 3] = x.w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t sd = (uint32_t) __builtin_amdgcn_readfirstlane((u * 8 + j) * (int) ncols * 4);
+            o.da[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, acol * 4, sd, 0));
+        }
+    };
+    // block j's 16 quant bytes (and its scale) from the unit registers
+    auto operand = [&](const Q0Raw<Q8> & o, const int j, i32x4 & b, float & dw) {
+        uint32_t t[4];
+        if constexpr (Q8) {
+            const int base = (BS * j) & 3;    // 0 (j even) or 2 (j odd): block start within its first dword
+            const int qo = base + 2;          // quant byte offset within this half's covering dwords
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int ob = qo + 4 * e;
+                t[e] = (ob & 3) == 0 ? o.v[5 * j + (ob >> 2)] : __builtin_amdgcn_alignbyte(o.v[5 * j + (ob >> 2) + 1], o.v[5 * j + (ob >> 2)], ob & 3);
+            }
+            // scale: half 0 holds it at byte `base` of its first dword; half 1 takes it from half 0
+            const uint32_t d0w = o.v[5 * j] >> (8 * base);
+            const uint32_t dsh = (uint32_t) __shfl_xor((int) d0w, 32, 64);
+            dw = mi_h2f((uint16_t) ((h ? dsh : d0w) & 0xFFFF));
+        } else {
+            const int oq = BS * j + 2;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int ob = oq + 4 * e;
+                const uint32_t x = (ob & 3) == 0 ? o.v[ob >> 2] : __builtin_amdgcn_alignbyte(o.v[(ob >> 2) + 1], o.v[ob >> 2], ob & 3);
+                t[e] = (((x >> (4 * h)) & 0x0F0F0F0Fu) + 0x78787878u) ^ 0x80808080u;
+            }
+            const int od = BS * j;
+            const uint32_t x = (od & 3) == 0 ? o.v[od >> 2] : __builtin_amdgcn_alignbyte(o.v[(od >> 2) + 1], o.v[od >> 2], od & 3);
+            dw = mi_h2f((uint16_t) (x & 0xFFFF));
+        }
+        b = i32x4{(int) t[0], (int) t[1], (int) t[2], (int) t[3]};
+    };
+    auto ld_x = [&](int u, int j) -> i32x4 {
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((u * 8 + j) * (int) xstep);
+        return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, acol * 32 + 16 * h, so, 0));
+    };
+
+    f32x16 gsum = {};
+    if (nsb > 0) {
+        Q0Raw<Q8> ru[2];
+        i32x4 xa[8];
+        const int uf = sb_at(0);
+        load_unit(ru[0], uf);
+#pragma unroll
+        for (int j = 0; j < 8; j++) xa[j] = ld_x(uf, j);
+        auto unit = [&](const Q0Raw<Q8> & cur, Q0Raw<Q8> & nxt, const int k) {
+            const int u = sb_at(k);
+            const int un = sb_at(k + 1);  // clamped: a past-the-end prefetch re-reads the last one
+            const bool last = u % gs == gs - 1 || u == S - 1;
+            if (u % gs == 0) gsum = f32x16{};
+            load_unit(nxt, un);
+            if (h == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) dal[w][j][r] = cur.da[j];
+            }
+            __builtin_amdgcn_wave_barrier();
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                i32x4 bq;
+                float dw;
+                operand(cur, j, bq, dw);
+                const i32x16 T = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[j], bq, i32x16{}, 0, 0, 0);
+                xa[j] = ld_x(un, j);
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const float4 d4 = *(const float4 *) &dal[w][j][8 * g + 4 * h];
+                    const float dav[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const int el = 4 * g + e;
+                        gsum[el] = __builtin_fmaf(dw * dav[e], (float) T[el], gsum[el]);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);  // one block's accumulator at a time
+            }
+            __builtin_amdgcn_wave_barrier();  // the LDS rows are rewritten by the next unit
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (last) {
+                const int gi = u / gs;
+#pragma unroll
+                for (int el = 0; el < 16; el++) red[(gi * 16 + el) * 64 + lane] = gsum[el];
+            }
+        };
+        for (int k = 0; k < nsb; k += 2) {
+            unit(ru[0], ru[1], k);
+            if (k + 1 >= nsb) break;
+            unit(ru[1], ru[0], k + 1);
+        }
+    }
+    mi_lds_barrier();
+    const int ngroups = (S + gs - 1) / gs;
+#pragma unroll
+    for (int i = 0; i < 16 / NW; i++) {
+        const int o = (int) threadIdx.x + 64 * NW * i;
+        const int el = o >> 6, l = o & 63;
+        float y = red[el * 64 + l];
+        for (int v = 1; v < ngroups; v++) y = y + red[(v * 16 + el) * 64 + l];
+        const int64_t n = n0 + (l & 31);
+        const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * (l >> 5);
+        if (n < N && c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y;
+    }
+}
+
+// ---- Q4_0 / Q8_0, long prompts: weights staged once per workgroup ---------------------------------
+// k_mmqx's structure for the one-MFMA-per-block family: a workgroup of NWV waves computes 64 weight
+// rows x 16 NWV prompt columns, wave (rw, cw) one 32 x 32 tile. A stage is one 8-block unit (256
+// K): its threads turn the next unit's 64 rows into MFMA operands in the other LDS buffer (thread =
+// (row, block): the block's dwords, 8 lanes per row contiguous -- coalesced -- re-aligned with
+// v_alignbyte; Q4_0 nibbles biased to q - 8), plus the rows' d_w; the raw weights were requested
+// LEAD stages earlier. Per block: one v_mfma_i32_32x32x32_i8 whose accumulator input is the
+// constant 0x4B400000, so the int32 result's bits are the float 1.5 * 2^23 + T (|T| < 2^22): one
+// subtraction gives (float) T exactly; then f = d_w d_a (exact: two fp16 values) and
+// g = fma(f, T, g). The MFMA of block j + 1 is issued before block j's combine (two accumulators).
+// Combine order: the family's canonical one (k_mmq0p): bit-identical to it.
+template <bool Q8, int NWV, int LEAD>
+__global__ __launch_bounds__(64 * NWV) void k_mmq0x(mi_mmx_group grp) {
+    MI_MMX_MEMBER(grp);
+    constexpr int BS = Q8 ? 34 : 18;
+    constexpr int UB = 8 * BS;                // bytes of a row's unit
+    constexpr int ND = Q8 ? 9 : 5;            // dwords covering a block (2-byte aligned)
+    constexpr int XR = 256 + 16;              // LDS row stride of the operand plane
+    constexpr int kPlane = XBM * XR;
+    constexpr int kBuf = kPlane + 8 * XBM * 4;  // + d_w [block][row]
+    constexpr int XBN_ = 16 * NWV;
+    constexpr int ROWP = 8 / NWV;             // staging passes (rows per thread)
+    constexpr int RSTEP = 8 * NWV;
+    __shared__ __attribute__((aligned(16))) char lds[2 * kBuf];
+
+    const int tid = (int) threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int rw = wave & 1, cw = wave >> 1;
+    const int64_t ncols = act.ncols;
+    const int64_t nrt = (N + XBM - 1) / XBM;
+    const int64_t n0 = (mmx_tile % nrt) * XBM, b0 = (mmx_tile / nrt) * XBN_;
+    const int S = (int) (K / 256);
+    const int gs = cfold_gs(S);
+
+    // staging role: row ar (+ RSTEP per pass), block j of the unit
+    const int ar = tid >> 3, j = tid & 7;
+    const int nrows = (int) std::min<int64_t>(XBM, N - n0);
+    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
+    const uint32_t boff = (uint32_t) (BS * j);
+    const uint32_t bal = boff & 3;  // 0 or 2: the block's offset in its first dword
+    uint32_t wrow[ROWP];
+#pragma unroll
+    for (int pr = 0; pr < ROWP; pr++) wrow[pr] = (uint32_t) (std::min(ar + pr * RSTEP, nrows - 1) * nb01) + (boff & ~3u);
+
+    // activation fragments: column b0 + 32 cw + (lane & 31), 16 bytes at 16 (lane >> 5)
+    const int r = lane & 31, h = lane >> 5;
+    const uint32_t bcol = (uint32_t) std::min<int64_t>(b0 + 32 * cw + r, ncols - 1);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) ((K / 32) * ncols * 4), 0x00020000);
+    const uint32_t xcol = bcol * 32 + 16 * h;
+    const uint32_t xstep = (uint32_t) ncols * 32;
+
+    struct Raw {
+        uint32_t w[ND];
+    };
+    auto load_raw = [&](Raw & raw, int u, int pr) {
+        u = u < S ? u : S - 1;
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(u * UB);
+#pragma unroll
+        for (int i = 0; i < ND; i++) raw.w[i] = __builtin_amdgcn_raw_buffer_load_b32(wres, wrow[pr] + 4 * i, so, 0);
+    };
+    struct Xs {
+        i32x4 q[8];
+        float da[8];
+    };
+    auto load_x = [&](Xs & xs, int u) {
+        u = u < S ? u : S - 1;
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((u * 8 + kk) * (int) xstep);
+            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol, so, 0));
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((u * 8 + kk) * (int) ncols * 4);
+            xs.da[kk] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, bcol * 4, so, 0));
+        }
+    };
+    // one thread's block into LDS buffer `buf`: 32 operand bytes at [row][32 j] and d_w
+    auto store_block = [&](int buf, const Raw & raw, int pr) {
+        const int row = ar + pr * RSTEP;
+        char * pl = lds + buf * kBuf + row * XR + 32 * j;
+        float * dwv = (float *) (lds + buf * kBuf + kPlane);
+        const uint32_t dbits = (bal ? raw.w[0] >> 16 : raw.w[0]) & 0xFFFF;
+        dwv[j * XBM + row] = mi_h2f((uint16_t) dbits);
+        // quants start at byte bal + 2 of w[0]: 2 -> alignbyte, 4 -> whole dwords from w[1]
+        if constexpr (Q8) {
+            uint32_t t[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) t[i] = bal ? raw.w[i + 1] : __builtin_amdgcn_alignbyte(raw.w[i + 1], raw.w[i], 2);
+            *(uint4 *) pl = make_uint4(t[0], t[1], t[2], t[3]);
+            *(uint4 *) (pl + 16) = make_uint4(t[4], t[5], t[6], t[7]);
+        } else {
+            uint32_t t[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) t[i] = bal ? raw.w[i + 1] : __builtin_amdgcn_alignbyte(raw.w[i + 1], raw.w[i], 2);
+            uint32_t lo[4], hi[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                lo[i] = ((t[i] & 0x0F0F0F0Fu) + 0x78787878u) ^ 0x80808080u;          // elements 4i..: q - 8
+                hi[i] = (((t[i] >> 4) & 0x0F0F0F0Fu) + 0x78787878u) ^ 0x80808080u;   // elements 16 + 4i..
+            }
+            *(uint4 *) pl = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+            *(uint4 *) (pl + 16) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+        }
+    };
+
+    f32x16 y = {}, gsum = {};
+    Raw raw[LEAD][ROWP];
+    Xs xs;
+#pragma unroll
+    for (int pr = 0; pr < ROWP; pr++) {
+        Raw r0;
+        load_raw(r0, 0, pr);
+        store_block(0, r0, pr);
+    }
+    load_x(xs, 0);
+#pragma unroll
+    for (int u = 0; u < LEAD; u++)
+#pragma unroll
+        for (int pr = 0; pr < ROWP; pr++) load_raw(raw[u][pr], 1 + u, pr);
+    mi_lds_barrier();
+
+    const i32x16 kBias = {0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000,
+                          0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000};
+    auto stage = [&](const int u, Raw (&rslot)[ROWP]) {
+        const int cur = u & 1;
+        const char * base = lds + cur * kBuf;
+        const char * arow_p = base + (32 * rw + r) * XR + 16 * h;
+        const float * dwv = (const float *) (base + kPlane);
+        const int un = u + 1 < S ? u + 1 : S - 1;
+        if (u % gs == 0) gsum = f32x16{};
+        float da[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) da[kk] = xs.da[kk];
+        i32x16 acc[2];
+        auto combine = [&](int kk, const i32x16 & T) {
+            const f32x16 tv = __builtin_bit_cast(f32x16, T) - 12582912.0f;  // exact (float) T
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const float4 d4 = *(const float4 *) (dwv + kk * XBM + 32 * rw + 8 * g + 4 * h);
+                const float dw[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int i = 4 * g + e;
+                    gsum[i] = __builtin_fmaf(dw[e] * da[kk], tv[i], gsum[i]);
+                }
+            }
+        };
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const i32x4 a = *(const i32x4 *) (arow_p + 32 * kk);
+            acc[kk & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, xs.q[kk], kBias, 0, 0, 0);
+            // step kk of the next unit into the register just consumed
+            const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((un * 8 + kk) * (int) xstep);
+            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol, so, 0));
+            if (kk > 0) combine(kk - 1, acc[(kk - 1) & 1]);
+#pragma unroll
+            for (int pr = 0; pr < ROWP; pr++) {
+                if (kk == 2 * pr + 1) store_block(cur ^ 1, rslot[pr], pr);
+                if (kk == 2 * pr + 2) load_raw(rslot[pr], u + 1 + LEAD, pr);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((un * 8 + kk) * (int) ncols * 4);
+            xs.da[kk] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, bcol * 4, so, 0));
+        }
+        combine(7, acc[1]);
+        if (u % gs == gs - 1 || u == S - 1) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) y[i] = u < gs ? gsum[i] : y[i] + gsum[i];
+        }
+        mi_lds_barrier();
+    };
+    for (int u0 = 0; u0 < S; u0 += LEAD) {
+#pragma unroll
+        for (int v = 0; v < LEAD; v++) {
+            if (u0 + v < S) stage(u0 + v, raw[v]);
+        }
+    }
+
+    // D[n][b]: column b = lane & 31 of this wave's 32, rows n = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+    const int64_t b = b0 + 32 * cw + r;
+    if (b >= ncols) return;
+    float * out = (float *) ((char *) dst + b * ycol);
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const int64_t n = n0 + 32 * rw + 8 * g + 4 * h;
+        if (n + 3 < N) {
+            *(float4 *) (out + n) = make_float4(y[4 * g], y[4 * g + 1], y[4 * g + 2], y[4 * g + 3]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[4 * g + e];
+        }
+    }
+}
+
 // ---- short prompts, K <= 4096: one round -------------------------------------------------------
 // A workgroup of S waves (one superblock each) per 32 x 32 tile, so every load of the tile is
 // requested at once and no wave runs a second round (k_mmqd's rounds each wait a full memory
@@ -1029,6 +1477,10 @@ __global__ __launch_bounds__(1024) void k_mmqd16(mi_mmx_group grp) {
 
 bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t nb01) {
     // buffer descriptors address < 2 GiB: activations K * ncols bytes, a 64-row weight block;
+    // Q4_0 / Q8_0: 16-byte aligned 8-block units (K % 256 == 0, rows of 16-byte multiples)
+    if (type == 2 || type == 8) {
+        return K % 256 == 0 && K >= 256 && nb01 % 16 == 0 && K * ncols < ((int64_t) 1 << 31) && (int64_t) nb01 * 32 < ((int64_t) 1 << 31);
+    }
     return (type == 12 || type == 13) && K % 256 == 0 && K >= 256 && ycol % 16 == 0 && K * ncols < ((int64_t) 1 << 31) &&
            (int64_t) nb01 * XBM < ((int64_t) 1 << 31);
 }
@@ -1048,6 +1500,28 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     const int type = g.type;
     const int64_t K = g.K;
     const int64_t ncols = g.m[0].act.ncols;  // every member has the same column count
+    if (type == 2 || type == 8) {  // Q4_0 / Q8_0: q8_0 activations (mi_act_mmx0_*), every column count
+        // <= 64 columns (or variant bit 16): 32 x 32 tiles, 4 waves on a tile (k_mmq0p); more:
+        // 64 x 128 tiles with the weights staged once per workgroup (k_mmq0x; variant bit 65536:
+        // 64 x 64 tiles of 4 waves). Same canonical combine: the same bits either way.
+        const int var = g_mi_tuning.mmq_variant;
+        if ((var & 16) || (ncols <= 64 && !(var & 128))) {
+            const dim3 grid((unsigned) mmx_deal(g, 32, 32));
+            if (type == 2) hipLaunchKernelGGL((k_mmq0p<false>), grid, dim3(256), 0, s, g);
+            else hipLaunchKernelGGL((k_mmq0p<true>), grid, dim3(256), 0, s, g);
+            return;
+        }
+        if (var & 65536) {
+            const dim3 grid4((unsigned) mmx_deal(g, XBM, 64));
+            if (type == 2) hipLaunchKernelGGL((k_mmq0x<false, 4, 2>), grid4, dim3(256), 0, s, g);
+            else hipLaunchKernelGGL((k_mmq0x<true, 4, 2>), grid4, dim3(256), 0, s, g);
+            return;
+        }
+        const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));
+        if (type == 2) hipLaunchKernelGGL((k_mmq0x<false, 8, 4>), grid, dim3(512), 0, s, g);
+        else hipLaunchKernelGGL((k_mmq0x<true, 8, 4>), grid, dim3(512), 0, s, g);
+        return;
+    }
     // short prompts (<= 128 columns): pipelined 32 x 32 tiles of 4 waves (k_mmqp; variant bit
     // 2048: k_mmqd1, a wave per superblock) or, <= 16 columns, 16 x 16 tiles of a wave per
     // superblock (k_mmqd16); long ones: 64 x 128 tiles with the weights dequantized once per

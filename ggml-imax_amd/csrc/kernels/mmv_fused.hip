@@ -416,6 +416,53 @@ struct FmtQ0 {
     }
 };
 
+// Q4_0 in pairs of blocks (tree order only): an item is 2 blocks = 36 B, 4-byte aligned, so 9
+// dword loads cover it with no slack, the second block's quants are whole dwords (only the
+// first's need v_alignbyte), and a K = 4096 row is one item per lane.
+struct FmtQ0Pair {
+    static constexpr int QKA = 32;
+    static constexpr int ITEM = 64;
+    struct Regs {
+        uint32_t w[9];
+    };
+    __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item) {
+        const uint32_t * p = (const uint32_t *) (row + (uint32_t) item * 36);
+#pragma unroll
+        for (int i = 0; i < 9; i++) r.w[i] = p[i];
+    }
+    template <int NC>
+    __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
+        // block 0: d = bytes 0..1, quants bytes 2..17; block 1: d = bytes 18..19, quants 20..35
+        uint32_t t0[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) t0[i] = __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], 2);
+        const float dw0 = mi_h2f((uint16_t) (r.w[0] & 0xFFFF));
+        const float dw1 = mi_h2f((uint16_t) (r.w[4] >> 16));
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 64);
+            const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            const int av0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const int av1[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            int s0 = 0, s1 = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                s0 = mi_dot4((int) (t0[i] & 0x0F0F0F0Fu), av0[i], s0);
+                s0 = mi_dot4((int) ((t0[i] >> 4) & 0x0F0F0F0Fu), av0[i + 4], s0);
+                s1 = mi_dot4((int) (r.w[i + 5] & 0x0F0F0F0Fu), av1[i], s1);
+                s1 = mi_dot4((int) ((r.w[i + 5] >> 4) & 0x0F0F0F0Fu), av1[i + 4], s1);
+            }
+            const uint32_t ss = *(const uint32_t *) (a.s32 + c * (K / 32) + 2 * item);  // both blocks' sums
+            s0 -= 8 * (int) (int16_t) (ss & 0xFFFF);
+            s1 -= 8 * (int) (int16_t) (ss >> 16);
+            const float2 da = *(const float2 *) (a.d + c * (K / 32) + 2 * item);
+            acc[c] += (float) s0 * (dw0 * da.x);
+            acc[c] += (float) s1 * (dw1 * da.y);
+        }
+    }
+};
+
 // ------------------------------------------------------------------ the streaming kernel
 
 // IPL = items per lane held in the prefetch ring (further items of long rows are loaded
@@ -731,7 +778,7 @@ template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO = fals
 void launch_one(mi_mmv_group g, hipStream_t s) {
     const size_t act = lds_bytes<F::QKA>(NC, g.K);
     size_t lds = act;
-    if (ORD) {
+    if constexpr (ORD) {
         // whole rows in the scratch when R >= 1 rows per wave fit a 36 KB budget (the kernel is
         // VGPR-limited to ~4 workgroups per CU anyway), else one chunk of 64 items per wave
         const int nitems = (int) (g.K / F::ITEM);
@@ -871,7 +918,11 @@ static void mi_mul_mat_q_fused_launch(mi_mmv_group & g, hipStream_t s) {
     switch (g.type) {
         case 12: launch_stream_ord<FmtKQ<false>>(g, variant, s); break;
         case 13: launch_stream_ord<FmtKQ<true>>(g, variant, s); break;
-        case 2: launch_stream_ord<FmtQ0<false>>(g, variant, s); break;
+        case 2:
+            // tree order: pairs of blocks per item (variant % 10 == 1: single blocks)
+            if (!g_mi_tuning.mmv_order && variant % 10 != 1) launch_stream_nc<FmtQ0Pair, false>(g, variant, s);
+            else launch_stream_ord<FmtQ0<false>>(g, variant, s);
+            break;
         case 8: launch_stream_ord<FmtQ0<true>>(g, variant, s); break;
         default: break;
     }

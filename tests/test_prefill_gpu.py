@@ -100,11 +100,12 @@ def test_prompt_sharded_prefill_equals_whole(rt, backend, world):
     assert np.array_equal(sharded.view(np.uint32), whole.view(np.uint32)), rel_err(sharded, whole)
 
 
-@pytest.mark.parametrize("tname", ["q4_K", "q5_K"])
+@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q4_0", "q8_0"])
 @pytest.mark.parametrize("K,N,B", [(256, 64, 9), (512, 100, 130), (768, 2304, 24), (3072, 768, 40), (1280, 96, 257)])
 def test_prefill_exact_gemm_shapes_vs_oracle(rt, backend, tname, K, N, B):
     """Ragged tiles (N, B not multiples of 64 / 128), odd superblock counts (the canonical chain
-    split puts the extra superblock in the second half), one-superblock rows."""
+    split puts the extra superblock in the second half), one-superblock rows. Q4_0 / Q8_0 run the
+    same exact-integer scheme on k_mmq0p (one i8 MFMA per 32-block, q8_0 activations)."""
     t = orc.TYPES_BY_NAME[tname]
     w = synth.uniform(K * 7 + N, K * N)
     x = synth.uniform(K * 3 + B, K * B)
@@ -135,20 +136,24 @@ def test_prefill_edge_values(rt, backend):
     assert rel_err(y, ref) <= EXACT_TOL
 
 
-@pytest.mark.parametrize("tname", ["q4_K", "q5_K"])
+@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q4_0", "q8_0"])
 @pytest.mark.parametrize("B", [72, 13])
 def test_prefill_kernels_bit_equal(rt, backend, tname, B):
     """Every prefill kernel shares the canonical combine (exact T and U per superblock, terms
     combined in the cfold order: 4 contiguous superblock groups, each left-folded, then the group
     sums left-folded), so any kernel choice gives the same bits: k_mmqp (the default for <= 128
     columns), k_mmqd1 (variant bit 2048), k_mmqx (full- and half-width workgroups) and, for <= 16
-    columns, k_mmqd16 (the default there; 16 x 16 tiles on the 16x16x64 MFMA)."""
+    columns, k_mmqd16 (the default there; 16 x 16 tiles on the 16x16x64 MFMA). Q4_0 / Q8_0:
+    k_mmq0p (32 x 32 tiles, <= 64 columns) and k_mmq0x (weights staged per 64 x 128 workgroup)."""
     t = orc.TYPES_BY_NAME[tname]
     K, N = 4096, 320
     w = synth.uniform(11, K * N)
     x = synth.uniform(12, K * B)
     wq = orc.quantize(t, w, K)
-    variants = [0, 2048, 1 << 27, 128 | 131072, 128 | 65536] + ([1 << 21] if B <= 16 else [])
+    if tname in ("q4_0", "q8_0"):  # k_mmq0p (16), k_mmq0x full / half width (128, 128 | 65536)
+        variants = [0, 16, 128, 128 | 65536]
+    else:
+        variants = [0, 2048, 1 << 27, 128 | 131072, 128 | 65536] + ([1 << 21] if B <= 16 else [])
     outs = {}
     try:
         for v in variants:
@@ -162,7 +167,7 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
         assert np.array_equal(outs[v].view(np.uint32), outs[0].view(np.uint32)), (v, rel_err(outs[v], outs[0]))
 
 
-@pytest.mark.parametrize("tname", ["q4_K", "q5_K"])
+@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q4_0", "q8_0"])
 @pytest.mark.parametrize("B", [64, 13, 300])
 def test_grouped_prefill_equals_single(rt, backend, tname, B):
     """Independent batched mul_mats of one graph (five members: two share one src1, weights of
