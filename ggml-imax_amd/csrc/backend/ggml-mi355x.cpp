@@ -506,6 +506,15 @@ static bool mm_src0_supported(ggml_type t) {
 static bool is_f32(const ggml_tensor * t) { return t && t->type == GGML_TYPE_F32; }
 static bool is_f16_or_f32(const ggml_tensor * t) { return t && (t->type == GGML_TYPE_F32 || t->type == GGML_TYPE_F16); }
 
+// the quantized vec_dot_type a src1 may already have for weight type t (GGML_TYPE_COUNT: none)
+static ggml_type q8_src1_type(ggml_type t) {
+    switch (t) {
+        case GGML_TYPE_Q4_K: case GGML_TYPE_Q5_K: return GGML_TYPE_Q8_K;
+        case GGML_TYPE_Q4_0: case GGML_TYPE_Q8_0: return GGML_TYPE_Q8_0;
+        default: return GGML_TYPE_COUNT;
+    }
+}
+
 static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
     const ggml_tensor * a = op->src[0];
     const ggml_tensor * b = op->src[1];
@@ -518,11 +527,12 @@ static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
             return true;
         case GGML_OP_MUL_MAT: {
             if (!mm_src0_supported(a->type)) return false;
-            // src1 F32, or src1 already of the weight's vec_dot_type (the reference CPU's rule,
-            // ggml-backend.c:822-837: F16 x F16 reads src1 as it lies)
-            if (b->type != GGML_TYPE_F32 && !(b->type == GGML_TYPE_F16 && a->type == GGML_TYPE_F16)) return false;
             if (a->nb[0] != ggml_type_size(a->type) || b->nb[0] != ggml_type_size(b->type)) return false;
-            return true;
+            // src1 F32, or src1 already of the weight's vec_dot_type, which the reference CPU reads as
+            // it lies (ggml.c:11952; F16 x F16, Q4_K/Q5_K x Q8_K, Q4_0/Q8_0 x Q8_0): the quantized
+            // ones with whole superblocks, on the device's own weights
+            if (b->type == GGML_TYPE_F32 || (b->type == GGML_TYPE_F16 && a->type == GGML_TYPE_F16)) return true;
+            return b->type == q8_src1_type(a->type) && a->ne[0] % 256 == 0 && !is_split_tensor(a);
         }
         case GGML_OP_ADD:
         case GGML_OP_SUB:
@@ -558,6 +568,10 @@ static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
         case GGML_OP_CPY:
         case GGML_OP_DUP:
         case GGML_OP_CONT:
+            // F32 -> Q8_K / Q8_0 (from_float = quantize_row_q8_K / _q8_0): whole rows of blocks
+            if (is_f32(a) && (op->type == GGML_TYPE_Q8_K || op->type == GGML_TYPE_Q8_0))
+                return ggml_are_same_shape(a, op) && a->nb[0] == sizeof(float) && op->nb[0] == ggml_type_size(op->type) &&
+                       op->ne[0] % (op->type == GGML_TYPE_Q8_K ? 256 : 32) == 0;
             return is_f16_or_f32(a) && is_f16_or_f32(op);
         case GGML_OP_ROPE: {
             const int32_t * pp = (const int32_t *) op->op_params;
@@ -639,7 +653,19 @@ static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, in
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
     void * dev = scratch_take(ctx, act_bytes(kind, K, ncols));
     const mi_src_cols x = src_cols(src1);
-    if (kind == 8 || kind == 9) {
+    if (src1->type == GGML_TYPE_Q8_K || src1->type == GGML_TYPE_Q8_0) {
+        // already quantized by the reference's rules (e.g. a CPY F32 -> Q8_K): re-laid out only
+        MI_ASSERT(kind == 0 || kind == 1 || kind == 8 || kind == 9);
+        const bool q8K = src1->type == GGML_TYPE_Q8_K;
+        MI_ASSERT(q8K == (kind == 1 || kind == 8));
+        if (kind >= 8) {
+            const mi_act_mmx mx = q8K ? mi_act_mmx_carve(dev, K, ncols) : mi_act_mmx0_carve(dev, K, ncols);
+            mi_q8_rows_to_act(x, K, q8K, nullptr, &mx, ctx->stream);
+        } else {
+            const mi_act_q8 act = mi_act_q8_carve(dev, K, ncols, q8K);
+            mi_q8_rows_to_act(x, K, q8K, &act, nullptr, ctx->stream);
+        }
+    } else if (kind == 8 || kind == 9) {
         mi_mmx_qgroup q;
         q.n = 1;
         q.K = K;
@@ -686,8 +712,12 @@ static bool mm_batched(const mi_mm_desc & m, const ggml_tensor * src1) {
 static int mm_act_kind(const mi_mm_desc & m, const ggml_tensor * src1) {
     const int kind = act_kind((ggml_type) m.type);
     if (kind < 0) return -1;
-    if (!mm_batched(m, src1)) return kind;
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
+    if (src1->type != GGML_TYPE_F32 && src1->type != GGML_TYPE_F16) {
+        // pre-quantized src1 (Q8_K / Q8_0 rows): the exact GEMMs' layouts, else the GEMV's
+        return mm_batched(m, src1) && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01) ? (kind == 1 ? 8 : 9) : kind;
+    }
+    if (!mm_batched(m, src1)) return kind;
     // GGML_MI355X_MMQ_VARIANT bit 2^30 selects the f16 GEMM for the quantized types too (A/B
     // timing; the low bits are mmq_exact.hip's own kernel variants)
     if (kind <= 1 && (g_mi_tuning.mmq_variant & (1 << 30)) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01)) return kind == 1 ? 8 : 9;
@@ -699,7 +729,8 @@ static int mm_act_kind(const mi_mm_desc & m, const ggml_tensor * src1) {
 // (op_mul_mat_split) each device's row slice.
 static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const void * W, int64_t N, const ggml_tensor * src1,
                         float * out, size_t nb1, size_t nb2, size_t nb3) {
-    MI_ASSERT(src1->type == GGML_TYPE_F32 || (src1->type == GGML_TYPE_F16 && src0->type == GGML_TYPE_F16));
+    MI_ASSERT(src1->type == GGML_TYPE_F32 || (src1->type == GGML_TYPE_F16 && src0->type == GGML_TYPE_F16) ||
+              src1->type == q8_src1_type(src0->type));
     MI_ASSERT(src0->nb[0] == ggml_type_size(src0->type));
     MI_ASSERT(src1->nb[0] == ggml_type_size(src1->type));
     MI_ASSERT(src0->ne[0] == src1->ne[0]);
@@ -1108,6 +1139,10 @@ static void op_companion(mi_backend_ctx * ctx, ggml_tensor * node) {
         case GGML_OP_DUP:
         case GGML_OP_CONT:
             MI_ASSERT(ggml_nelements(node) == ggml_nelements(a));
+            if (node->type == GGML_TYPE_Q8_K || node->type == GGML_TYPE_Q8_0) {
+                mi_quantize_rows_q8(src_cols(a), a->ne[0], node->type == GGML_TYPE_Q8_K, src_cols(node), st);
+                break;
+            }
             mi_op_cpy(desc(node), desc(a), st);
             break;
         case GGML_OP_ROPE: {
@@ -1198,7 +1233,10 @@ static int run_fused_group(mi_backend_ctx * ctx, ggml_cgraph * cgraph, int i) {
     ggml_tensor * first = cgraph->nodes[i];
     std::vector<ggml_tensor *> members = {first};
     int last = i;
-    for (int j = i + 1; j < cgraph->n_nodes && (int) members.size() < kMiMaxMembers; j++) {
+    std::vector<int> at = {i};
+    // scan up to 4 launches' worth, then split the run evenly (36 -> 18 + 18, not 32 + 4: a
+    // launch of few members is all prologue)
+    for (int j = i + 1; j < cgraph->n_nodes && (int) members.size() < 4 * kMiMaxMembers; j++) {
         ggml_tensor * n = cgraph->nodes[j];
         if (is_noop(n)) continue;
         if (!fused_mv_eligible(n) || !same_group_shape(first, n)) break;
@@ -1211,7 +1249,13 @@ static int run_fused_group(mi_backend_ctx * ctx, ggml_cgraph * cgraph, int i) {
         }
         if (!independent) break;
         members.push_back(n);
-        last = j;
+        at.push_back(j);
+    }
+    {
+        const int runs = ((int) members.size() + kMiMaxMembers - 1) / kMiMaxMembers;
+        const int take = ((int) members.size() + runs - 1) / runs;
+        members.resize(take);
+        last = at[take - 1];
     }
     mi_mmv_group g;
     g.type = first->src[0]->type;
@@ -1816,7 +1860,8 @@ static int run_prefill_group(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
     const int64_t ncols = cols_of(first);
     std::vector<ggml_tensor *> members = {first};
     int last = i;
-    for (int j = next_node(g, i); j >= 0 && (int) members.size() < kMiMaxPrefillMembers; j = next_node(g, j)) {
+    std::vector<int> at = {i};
+    for (int j = next_node(g, i); j >= 0 && (int) members.size() < 4 * kMiMaxPrefillMembers; j = next_node(g, j)) {
         ggml_tensor * n = g->nodes[j];
         if (prefill_mmx_kind(n) != kind || n->src[0]->type != type || n->src[0]->ne[0] != K || cols_of(n) != ncols) break;
         bool independent = true;
@@ -1828,7 +1873,14 @@ static int run_prefill_group(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
         }
         if (!independent) break;
         members.push_back(n);
-        last = j;
+        at.push_back(j);
+    }
+    {
+        // split a long run evenly over its launches (as run_fused_group)
+        const int runs = ((int) members.size() + kMiMaxPrefillMembers - 1) / kMiMaxPrefillMembers;
+        const int take = ((int) members.size() + runs - 1) / runs;
+        members.resize(take);
+        last = at[take - 1];
     }
     if (members.size() < 2) return -1;
     // activations: cached conversions are reused; the missing distinct src1s in one quantizer launch

@@ -59,7 +59,7 @@ void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s);
 // Decode-regime mul_mat with the activation quantizer fused in; one launch serves up to
 // kMiMaxMembers independent mul_mats of identical weight type / shape (2-D weights, 2-D f32 src1
 // with 16-byte aligned columns, contiguous f32 dst columns).
-constexpr int kMiMaxMembers = 32;
+constexpr int kMiMaxMembers = 64;
 struct mi_mmv_member {
     const void * W;
     const char * X;
@@ -165,6 +165,11 @@ void mi_quantize_q8_K_mmx_group(mi_mmx_qgroup & q, hipStream_t s);
 size_t mi_act_mmx0_bytes(int64_t K, int64_t ncols);
 mi_act_mmx mi_act_mmx0_carve(void * base, int64_t K, int64_t ncols);
 void mi_quantize_q8_0_mmx_group(mi_mmx_qgroup & q, hipStream_t s);
+// src1 of the weight's vec_dot type (quantize.hip): GGML_OP_CPY F32 -> Q8_K / Q8_0 rows in the
+// reference block layouts (dst columns addressed like src1's), and such rows -> the GEMV's q8 SoA
+// (act) or the prefill GEMMs' MFMA layout (mx); exactly one of act / mx non-null
+void mi_quantize_rows_q8(const mi_src_cols & x, int64_t K, bool is_q8K, const mi_src_cols & dst, hipStream_t s);
+void mi_q8_rows_to_act(const mi_src_cols & xs, int64_t K, bool is_q8K, const mi_act_q8 * act, const mi_act_mmx * mx, hipStream_t s);
 bool mi_mmqx_supported(int type, int64_t K, size_t ycol, int64_t ncols, size_t nb01);
 // Independent Q4_K / Q5_K (q8_K activations) or Q4_0 / Q8_0 (q8_0 activations, mi_act_mmx0_*)
 // mul_mats (same type, K and activation column count) in one launch:

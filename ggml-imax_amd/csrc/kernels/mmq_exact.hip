@@ -1027,8 +1027,11 @@ __global__ __launch_bounds__(256, 2) void k_mmq0p(mi_mmx_group grp) {
 // subtraction gives (float) T exactly; then f = d_w d_a (exact: two fp16 values) and
 // g = fma(f, T, g). The MFMA of block j + 1 is issued before block j's combine (two accumulators).
 // Combine order: the family's canonical one (k_mmq0p): bit-identical to it.
-template <bool Q8, int NWV, int LEAD>
-__global__ __launch_bounds__(64 * NWV) void k_mmq0x(mi_mmx_group grp) {
+// NR = 2: each wave computes both 32-row halves of its 32 columns (64 x 32: every activation
+// fragment feeds two MFMAs, half the activation traffic per MFMA); the workgroup's NWV waves then
+// cover 32 NWV columns.
+template <bool Q8, int NWV, int LEAD, int NR = 1>
+__global__ __launch_bounds__(64 * NWV, NR == 2 ? 2 : 1) void k_mmq0x(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     constexpr int BS = Q8 ? 34 : 18;
     constexpr int UB = 8 * BS;                // bytes of a row's unit
@@ -1036,14 +1039,14 @@ __global__ __launch_bounds__(64 * NWV) void k_mmq0x(mi_mmx_group grp) {
     constexpr int XR = 256 + 16;              // LDS row stride of the operand plane
     constexpr int kPlane = XBM * XR;
     constexpr int kBuf = kPlane + 8 * XBM * 4;  // + d_w [block][row]
-    constexpr int XBN_ = 16 * NWV;
+    constexpr int XBN_ = NR == 2 ? 32 * NWV : 16 * NWV;
     constexpr int ROWP = 8 / NWV;             // staging passes (rows per thread)
     constexpr int RSTEP = 8 * NWV;
     __shared__ __attribute__((aligned(16))) char lds[2 * kBuf];
 
     const int tid = (int) threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const int rw = wave & 1, cw = wave >> 1;
+    const int rw = NR == 2 ? 0 : (wave & 1), cw = NR == 2 ? wave : (wave >> 1);
     const int64_t ncols = act.ncols;
     const int64_t nrt = (N + XBM - 1) / XBM;
     const int64_t n0 = (mmx_tile % nrt) * XBM, b0 = (mmx_tile / nrt) * XBN_;
@@ -1123,7 +1126,7 @@ __global__ __launch_bounds__(64 * NWV) void k_mmq0x(mi_mmx_group grp) {
         }
     };
 
-    f32x16 y = {}, gsum = {};
+    f32x16 y[NR] = {}, gsum[NR] = {};
     Raw raw[LEAD][ROWP];
     Xs xs;
 #pragma unroll
@@ -1147,32 +1150,50 @@ __global__ __launch_bounds__(64 * NWV) void k_mmq0x(mi_mmx_group grp) {
         const char * arow_p = base + (32 * rw + r) * XR + 16 * h;
         const float * dwv = (const float *) (base + kPlane);
         const int un = u + 1 < S ? u + 1 : S - 1;
-        if (u % gs == 0) gsum = f32x16{};
+        if (u % gs == 0) {
+#pragma unroll
+            for (int ri = 0; ri < NR; ri++) gsum[ri] = f32x16{};
+        }
         float da[8];
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) da[kk] = xs.da[kk];
-        i32x16 acc[2];
-        auto combine = [&](int kk, const i32x16 & T) {
+        // NR = 1: two accumulators, block kk + 1's MFMA issued before block kk's combine; NR = 2:
+        // one per row half, in the order M0(kk) C1(kk-1) M1(kk) C0(kk)
+        i32x16 acc[NR == 1 ? 2 : NR];
+        auto combine = [&](int kk, int ri, const i32x16 & T) {
             const f32x16 tv = __builtin_bit_cast(f32x16, T) - 12582912.0f;  // exact (float) T
 #pragma unroll
             for (int g = 0; g < 4; g++) {
-                const float4 d4 = *(const float4 *) (dwv + kk * XBM + 32 * rw + 8 * g + 4 * h);
+                const float4 d4 = *(const float4 *) (dwv + kk * XBM + 32 * (rw + ri) + 8 * g + 4 * h);
                 const float dw[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     const int i = 4 * g + e;
-                    gsum[i] = __builtin_fmaf(dw[e] * da[kk], tv[i], gsum[i]);
+                    gsum[ri][i] = __builtin_fmaf(dw[e] * da[kk], tv[i], gsum[ri][i]);
                 }
             }
         };
+        auto mfma = [&](int kk, int ri) {
+            const i32x4 a = *(const i32x4 *) (arow_p + ri * 32 * XR + 32 * kk);
+            return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, xs.q[kk], kBias, 0, 0, 0);
+        };
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) {
-            const i32x4 a = *(const i32x4 *) (arow_p + 32 * kk);
-            acc[kk & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, xs.q[kk], kBias, 0, 0, 0);
+            if constexpr (NR == 1) {
+                acc[kk & 1] = mfma(kk, 0);
+            } else {
+                acc[0] = mfma(kk, 0);
+                if (kk > 0) combine(kk - 1, 1, acc[1]);
+                acc[1] = mfma(kk, 1);
+            }
             // step kk of the next unit into the register just consumed
             const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((un * 8 + kk) * (int) xstep);
             xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol, so, 0));
-            if (kk > 0) combine(kk - 1, acc[(kk - 1) & 1]);
+            if constexpr (NR == 1) {
+                if (kk > 0) combine(kk - 1, 0, acc[(kk - 1) & 1]);
+            } else {
+                combine(kk, 0, acc[0]);
+            }
 #pragma unroll
             for (int pr = 0; pr < ROWP; pr++) {
                 if (kk == 2 * pr + 1) store_block(cur ^ 1, rslot[pr], pr);
@@ -1185,10 +1206,12 @@ __global__ __launch_bounds__(64 * NWV) void k_mmq0x(mi_mmx_group grp) {
             const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((un * 8 + kk) * (int) ncols * 4);
             xs.da[kk] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, bcol * 4, so, 0));
         }
-        combine(7, acc[1]);
+        combine(7, NR - 1, acc[1]);
         if (u % gs == gs - 1 || u == S - 1) {
 #pragma unroll
-            for (int i = 0; i < 16; i++) y[i] = u < gs ? gsum[i] : y[i] + gsum[i];
+            for (int ri = 0; ri < NR; ri++)
+#pragma unroll
+                for (int i = 0; i < 16; i++) y[ri][i] = u < gs ? gsum[ri][i] : y[ri][i] + gsum[ri][i];
         }
         mi_lds_barrier();
     };
@@ -1204,13 +1227,15 @@ __global__ __launch_bounds__(64 * NWV) void k_mmq0x(mi_mmx_group grp) {
     if (b >= ncols) return;
     float * out = (float *) ((char *) dst + b * ycol);
 #pragma unroll
+    for (int ri = 0; ri < NR; ri++)
+#pragma unroll
     for (int g = 0; g < 4; g++) {
-        const int64_t n = n0 + 32 * rw + 8 * g + 4 * h;
+        const int64_t n = n0 + 32 * (rw + ri) + 8 * g + 4 * h;
         if (n + 3 < N) {
-            *(float4 *) (out + n) = make_float4(y[4 * g], y[4 * g + 1], y[4 * g + 2], y[4 * g + 3]);
+            *(float4 *) (out + n) = make_float4(y[ri][4 * g], y[ri][4 * g + 1], y[ri][4 * g + 2], y[ri][4 * g + 3]);
         } else {
 #pragma unroll
-            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[4 * g + e];
+            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[ri][4 * g + e];
         }
     }
 }
@@ -1501,26 +1526,59 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     const int64_t K = g.K;
     const int64_t ncols = g.m[0].act.ncols;  // every member has the same column count
     if (type == 2 || type == 8) {  // Q4_0 / Q8_0: q8_0 activations (mi_act_mmx0_*), every column count
-        // <= 64 columns (or variant bit 16): 32 x 32 tiles, 4 waves on a tile (k_mmq0p); more:
-        // 64 x 128 tiles with the weights staged once per workgroup (k_mmq0x; variant bit 65536:
-        // 64 x 64 tiles of 4 waves). Same canonical combine: the same bits either way.
+        // By workgroup count: 64 x 128 tiles of 4 waves, each 64 rows x 32 columns (k_mmq0x NR = 2)
+        // when there are >= 256 of them; else 64 x 64 tiles of 4 waves (k_mmq0x half width) when
+        // >= 256 (Q8_0: 128); else 32 x 32 tiles of 4 waves on one tile (k_mmq0p). Variant bits force one: 16 k_mmq0p, 128 k_mmq0x (8 waves, 64 x 128), 128 |
+        // 65536 half width, 128 | 2^24 NR = 2, 128 | 2^25 NR = 2 with 8 waves (64 x 256). Every one
+        // keeps the family's canonical combine: the same bits.
         const int var = g_mi_tuning.mmq_variant;
-        if ((var & 16) || (ncols <= 64 && !(var & 128))) {
-            const dim3 grid((unsigned) mmx_deal(g, 32, 32));
-            if (type == 2) hipLaunchKernelGGL((k_mmq0p<false>), grid, dim3(256), 0, s, g);
-            else hipLaunchKernelGGL((k_mmq0p<true>), grid, dim3(256), 0, s, g);
-            return;
+        int pick;
+        if (var & 16) pick = 0;
+        else if (var & 128) pick = (var & (1 << 25)) ? 4 : (var & (1 << 24)) ? 3 : (var & 65536) ? 2 : 1;
+        else {
+            int64_t t2 = 0, th = 0;
+            for (int i = 0; i < g.n; i++) {
+                const int64_t rt = (g.m[i].N + XBM - 1) / XBM, nc = g.m[i].act.ncols;
+                t2 += rt * ((nc + 127) / 128);
+                th += rt * ((nc + 63) / 64);
+            }
+            // (k_mmq0p's Q8_0 operands -- five dword loads per block and lane -- make it the
+            // slower one for Q8_0 from 128 half-width tiles on)
+            pick = t2 >= 256 && ncols > 64 ? 3 : th >= (type == 8 ? 128 : 256) ? 2 : 0;
         }
-        if (var & 65536) {
-            const dim3 grid4((unsigned) mmx_deal(g, XBM, 64));
-            if (type == 2) hipLaunchKernelGGL((k_mmq0x<false, 4, 2>), grid4, dim3(256), 0, s, g);
-            else hipLaunchKernelGGL((k_mmq0x<true, 4, 2>), grid4, dim3(256), 0, s, g);
-            return;
+        const bool q8 = type == 8;
+        switch (pick) {
+            case 0: {
+                const dim3 grid((unsigned) mmx_deal(g, 32, 32));
+                if (!q8) hipLaunchKernelGGL((k_mmq0p<false>), grid, dim3(256), 0, s, g);
+                else hipLaunchKernelGGL((k_mmq0p<true>), grid, dim3(256), 0, s, g);
+                return;
+            }
+            case 1: {
+                const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));
+                if (!q8) hipLaunchKernelGGL((k_mmq0x<false, 8, 4>), grid, dim3(512), 0, s, g);
+                else hipLaunchKernelGGL((k_mmq0x<true, 8, 4>), grid, dim3(512), 0, s, g);
+                return;
+            }
+            case 2: {
+                const dim3 grid((unsigned) mmx_deal(g, XBM, 64));
+                if (!q8) hipLaunchKernelGGL((k_mmq0x<false, 4, 2>), grid, dim3(256), 0, s, g);
+                else hipLaunchKernelGGL((k_mmq0x<true, 4, 2>), grid, dim3(256), 0, s, g);
+                return;
+            }
+            case 3: {
+                const dim3 grid((unsigned) mmx_deal(g, XBM, 128));
+                if (!q8) hipLaunchKernelGGL((k_mmq0x<false, 4, 2, 2>), grid, dim3(256), 0, s, g);
+                else hipLaunchKernelGGL((k_mmq0x<true, 4, 2, 2>), grid, dim3(256), 0, s, g);
+                return;
+            }
+            default: {
+                const dim3 grid((unsigned) mmx_deal(g, XBM, 256));
+                if (!q8) hipLaunchKernelGGL((k_mmq0x<false, 8, 2, 2>), grid, dim3(512), 0, s, g);
+                else hipLaunchKernelGGL((k_mmq0x<true, 8, 2, 2>), grid, dim3(512), 0, s, g);
+                return;
+            }
         }
-        const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));
-        if (type == 2) hipLaunchKernelGGL((k_mmq0x<false, 8, 4>), grid, dim3(512), 0, s, g);
-        else hipLaunchKernelGGL((k_mmq0x<true, 8, 4>), grid, dim3(512), 0, s, g);
-        return;
     }
     // short prompts (<= 128 columns): pipelined 32 x 32 tiles of 4 waves (k_mmqp; variant bit
     // 2048: k_mmqd1, a wave per superblock) or, <= 16 columns, 16 x 16 tiles of a wave per

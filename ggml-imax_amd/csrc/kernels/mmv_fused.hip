@@ -912,9 +912,10 @@ void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s) {
 
 static void mi_mul_mat_q_fused_launch(mi_mmv_group & g, hipStream_t s) {
     // variant 0 = per-type default, from interleaved A/B runs on MI355X (tools/mmv_tune.py):
-    // prefetch depth 2 for Q4_K / Q8_0, depth 1 for Q5_K / Q4_0 (fewer VGPRs, more waves)
+    // prefetch depth 2 for Q4_K / Q8_0 / Q4_0 (Q4_0 in block pairs: 4096 x 11008 5.34 -> 5.58
+    // TB/s), depth 1 for Q5_K (fewer VGPRs, more waves)
     int variant = g_mi_tuning.mmv_variant;
-    if (variant == 0) variant = (g.type == 12 || g.type == 8) ? 21 : 11;
+    if (variant == 0) variant = (g.type == 12 || g.type == 8) ? 21 : (g.type == 2 ? 22 : 11);
     switch (g.type) {
         case 12: launch_stream_ord<FmtKQ<false>>(g, variant, s); break;
         case 13: launch_stream_ord<FmtKQ<true>>(g, variant, s); break;

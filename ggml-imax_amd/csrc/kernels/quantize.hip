@@ -195,3 +195,142 @@ void mi_convert_f16(const mi_src_cols & x, int64_t K, uint16_t * out, hipStream_
     if (src_f16) hipLaunchKernelGGL(k_convert_f16<true>, dim3((unsigned) ncols, (unsigned) ((K + 255) / 256)), dim3(256), 0, s, x, K, out, xb);
     else hipLaunchKernelGGL(k_convert_f16<false>, dim3((unsigned) ncols, (unsigned) ((K + 255) / 256)), dim3(256), 0, s, x, K, out, xb);
 }
+
+// ---- src1 already of the vec_dot type (Q8_K / Q8_0 rows) -------------------------------------
+// The reference CPU mul_mat reads such a src1 as it lies (ggml.c:11952: no conversion when
+// src1->type == vec_dot_type); GGML_OP_CPY F32 -> Q8_K / Q8_0 writes it (ggml_compute_forward_dup
+// -> from_float = quantize_row_q8_K / quantize_row_q8_0). Reference block layouts:
+//   block_q8_K (292 B): float d | int8 qs[256] | int16 bsums[16] (sums of 16 quants)
+//   block_q8_0 (34 B):  fp16 d  | int8 qs[32]
+static __device__ __forceinline__ const char * col_base(const mi_src_cols & x, uint32_t c) {
+    if (x.ne2 == 1 && x.ne3 == 1) return x.base + (size_t) c * x.nb1;
+    const uint32_t ne1 = (uint32_t) x.ne1, ne2 = (uint32_t) x.ne2;
+    const uint32_t i1 = c % ne1, i2 = (c / ne1) % ne2, i3 = c / (ne1 * ne2);
+    return x.base + (size_t) i1 * x.nb1 + (size_t) i2 * x.nb2 + (size_t) i3 * x.nb3;
+}
+
+// CPY F32 -> Q8_K: one superblock per wave, grid (column, group of 4 superblocks); the rounding of
+// k_quantize_q8_K (quantize_row_q8_K_reference, src/ggml-quants.c:3370-3407). An all-zero
+// superblock gets d = 0, zero quants and zero bsums (the reference leaves its bsums untouched;
+// every dot product multiplies them by d = 0).
+__global__ __launch_bounds__(256) void k_quantize_rows_q8_K(mi_src_cols x, int64_t K, char * dst, mi_src_cols dl) {
+    const int wave = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t) blockIdx.y * 4 + wave;
+    if (b >= K / 256) return;
+    const uint32_t c = blockIdx.x;
+    const float4 v4 = *(const float4 *) ((const float *) col_base(x, c) + b * 256 + lane * 4);
+    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+    uint32_t packed;
+    int sum32;
+    float d;
+    mi_q8K_superblock(v, lane, packed, sum32, d);
+    (void) sum32;
+    char * blk = (char *) col_base(dl, c) + (size_t) b * 292;
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) s += (int) (int8_t) (packed >> (8 * i));
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);  // sum of the 16 quants of lanes 4j..4j+3
+    *(uint32_t *) (blk + 4 + lane * 4) = packed;
+    if ((lane & 3) == 0) *(int16_t *) (blk + 260 + 2 * (lane >> 2)) = (int16_t) s;
+    if (lane == 0) *(float *) blk = d;
+    (void) dst;
+}
+
+// CPY F32 -> Q8_0: one block per half-wave (k_quantize_q8_0's rounding, the AVX2 branch of
+// quantize_row_q8_0, src/ggml-quants.c:535-618); grid (column, group of 8 blocks). Blocks are
+// 2-byte aligned: the quants go out as bytes.
+__global__ __launch_bounds__(256) void k_quantize_rows_q8_0(mi_src_cols x, int64_t K, mi_src_cols dl) {
+    const int64_t b = (int64_t) blockIdx.y * 8 + (threadIdx.x >> 5);
+    const int l = threadIdx.x & 31;
+    if (b >= K / 32) return;
+    const uint32_t c = blockIdx.x;
+    const float v = ((const float *) col_base(x, c))[b * 32 + l];
+    float amax = fabsf(v);
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 32));
+    const float d = amax / 127.f;
+    const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+    const float q = __builtin_rintf(__fmul_rn(v, id));
+    char * blk = (char *) col_base(dl, c) + (size_t) b * 34;
+    blk[2 + l] = (char) (int8_t) (int) q;
+    if (l == 0) *(uint16_t *) blk = mi_f2h(d);
+}
+
+void mi_quantize_rows_q8(const mi_src_cols & x, int64_t K, bool is_q8K, const mi_src_cols & dst, hipStream_t s) {
+    const int64_t ncols = x.ne1 * x.ne2 * x.ne3;
+    if (ncols == 0) return;
+    if (is_q8K) hipLaunchKernelGGL(k_quantize_rows_q8_K, dim3((unsigned) ncols, (unsigned) ((K / 256 + 3) / 4)), dim3(256), 0, s, x, K, nullptr, dst);
+    else hipLaunchKernelGGL(k_quantize_rows_q8_0, dim3((unsigned) ncols, (unsigned) ((K / 32 + 7) / 8)), dim3(256), 0, s, x, K, dst);
+}
+
+// Q8_K rows -> the kernels' activation layouts. One superblock per wave (four quant bytes per lane),
+// grid (column, group of 4 superblocks). MMX: the prefill GEMMs' [K/32][ncols][32] quants, d and the
+// f16 halves of the sums of 32 (k_quantize_q8_K_mmx's layout); else the GEMV's q8 SoA (mi_act_q8).
+// The sums of 32 are recomputed from the quants (equal to bsums[2j] + bsums[2j+1] whenever d != 0).
+template <bool MMX>
+__global__ __launch_bounds__(256) void k_q8K_rows_to_act(mi_src_cols xs, int64_t K, mi_act_q8 act, mi_act_mmx mx) {
+    const int wave = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t) blockIdx.y * 4 + wave;
+    if (b >= K / 256) return;
+    const uint32_t c = blockIdx.x;
+    const char * blk = col_base(xs, c) + (size_t) b * 292;
+    const uint32_t packed = *(const uint32_t *) (blk + 4 + lane * 4);
+    const float d = *(const float *) blk;
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) s += (int) (int8_t) (packed >> (8 * i));
+    s = s + __shfl_xor(s, 1, 64);
+    s = s + __shfl_xor(s, 2, 64);
+    s = s + __shfl_xor(s, 4, 64);  // sum of the 32 quants of lanes 8j..8j+7
+    if constexpr (MMX) {
+        const int64_t ncols = mx.ncols;
+        *(uint32_t *) (mx.xq + ((b * 8 + (lane >> 3)) * ncols + c) * 32 + (lane & 7) * 4) = packed;
+        if ((lane & 7) == 0) {
+            const uint32_t lo = mi_f2h((float) (s & 63)), hi = mi_f2h((float) (s >> 6));
+            *(uint32_t *) (mx.xu + (b * ncols + c) * 16 + 2 * (lane >> 3)) = lo | (hi << 16);
+        }
+        if (lane == 0) mx.xd[b * ncols + c] = d;
+    } else {
+        *(uint32_t *) (act.qs + (int64_t) c * K + b * 256 + lane * 4) = packed;
+        if ((lane & 7) == 0) act.s32[(int64_t) c * (K / 32) + b * 8 + (lane >> 3)] = (int16_t) s;
+        if (lane == 0) act.d[(int64_t) c * (K / 256) + b] = d;
+    }
+}
+
+// Q8_0 rows -> activation layouts: one block per half-wave, one quant per lane; d as f32
+template <bool MMX>
+__global__ __launch_bounds__(256) void k_q8_0_rows_to_act(mi_src_cols xs, int64_t K, mi_act_q8 act, mi_act_mmx mx) {
+    const int64_t b = (int64_t) blockIdx.y * 8 + (threadIdx.x >> 5);
+    const int l = threadIdx.x & 31;
+    if (b >= K / 32) return;
+    const uint32_t c = blockIdx.x;
+    const char * blk = col_base(xs, c) + (size_t) b * 34;
+    const int8_t q = (int8_t) blk[2 + l];
+    const float d = mi_h2f(*(const uint16_t *) blk);
+    if constexpr (MMX) {
+        mx.xq[(b * mx.ncols + c) * 32 + l] = q;
+        if (l == 0) mx.xd[b * mx.ncols + c] = d;
+    } else {
+        act.qs[(int64_t) c * K + b * 32 + l] = q;
+        if (l == 0) act.d[(int64_t) c * (K / 32) + b] = d;
+    }
+}
+
+void mi_q8_rows_to_act(const mi_src_cols & xs, int64_t K, bool is_q8K, const mi_act_q8 * act, const mi_act_mmx * mx, hipStream_t s) {
+    const int64_t ncols = xs.ne1 * xs.ne2 * xs.ne3;
+    if (ncols == 0) return;
+    const mi_act_q8 a = act ? *act : mi_act_q8{};
+    const mi_act_mmx m = mx ? *mx : mi_act_mmx{};
+    if (is_q8K) {
+        const dim3 grid((unsigned) ncols, (unsigned) ((K / 256 + 3) / 4));
+        if (mx) hipLaunchKernelGGL(k_q8K_rows_to_act<true>, grid, dim3(256), 0, s, xs, K, a, m);
+        else hipLaunchKernelGGL(k_q8K_rows_to_act<false>, grid, dim3(256), 0, s, xs, K, a, m);
+    } else {
+        const dim3 grid((unsigned) ncols, (unsigned) ((K / 32 + 7) / 8));
+        if (mx) hipLaunchKernelGGL(k_q8_0_rows_to_act<true>, grid, dim3(256), 0, s, xs, K, a, m);
+        else hipLaunchKernelGGL(k_q8_0_rows_to_act<false>, grid, dim3(256), 0, s, xs, K, a, m);
+    }
+}
