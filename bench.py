@@ -279,8 +279,8 @@ def reassemble_rows(y_all: np.ndarray, N: int, world: int, B: int) -> np.ndarray
 class _DevArray:
     """__cuda_array_interface__ over a device pointer (ggml device buffer memory -> torch view)."""
 
-    def __init__(self, ptr: int, n: int):
-        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (ptr, False), "version": 2, "strides": None}
+    def __init__(self, ptr: int, n: int, typestr: str = "<f4"):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False), "version": 2, "strides": None}
 
 
 def torch_view(torch, lib, t, device):
@@ -289,21 +289,32 @@ def torch_view(torch, lib, t, device):
     return torch.as_tensor(_DevArray(G.tensor_data_ptr(lib, t), n), device=device)
 
 
+def torch_bytes(torch, lib, t, device):
+    """A torch uint8 view of ggml tensor `t`'s device bytes (quantized tensors)."""
+    return torch.as_tensor(_DevArray(G.tensor_data_ptr(lib, t), int(lib.ggml_nbytes(t)), "|u1"), device=device)
+
+
 def rowsplit_prefill(lib, backend, dist, world, rank, device, torch, steps=5, K=4096, N=4096, B=512, return_y=False):
     """Optional tensor-split row path over RCCL (north_star "RCCL only for
     the optional tensor-split row path"): rank r holds rows row_shard(N) of one Q4_K weight; per
-    step rank 0's prompt activations X (f32 [K, B]) are broadcast to every rank (RCCL over xGMI),
-    each rank computes its Y rows on its GPU, and the row slices are all-gathered (RCCL)."""
+    step rank 0 quantizes its prompt activations X (f32 [K, B]) ONCE on its GPU to Q8_K rows (the
+    weight's vec_dot type: a GGML_OP_CPY F32 -> Q8_K graph) and broadcasts those bytes to every rank
+    (RCCL over xGMI; 292 B per 256 values instead of 1 KB -- as the reference ships src1 quantized
+    once, ggml-cuda.cu:1551-1565); each rank computes its Y rows from them (MUL_MAT with a Q8_K
+    src1, read as it lies) and the row slices are all-gathered (RCCL)."""
     r0, r1 = row_shard(N, world, rank)
     rows = r1 - r0
     rows_max = max(row_shard(N, world, r)[1] - row_shard(N, world, r)[0] for r in range(world))
-    ovh = lib.ggml_tensor_overhead() * 8 + lib.ggml_graph_overhead()
+    ovh = lib.ggml_tensor_overhead() * 8 + 2 * lib.ggml_graph_overhead()
     ctx = G.Context(lib, ovh, no_alloc=True)
     c = ctx.ctx
     w = lib.ggml_new_tensor_2d(c, 12, K, rows)
     x = lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F32, K, B)
-    y = lib.ggml_mul_mat(c, w, x)
+    xq = lib.ggml_new_tensor_2d(c, 15, K, B)  # GGML_TYPE_Q8_K
+    y = lib.ggml_mul_mat(c, w, xq)
     ypad = lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F32, rows_max, B)  # all_gather needs equal slices
+    gq = lib.ggml_new_graph(c)
+    lib.ggml_build_forward_expand(gq, lib.ggml_cpy(c, x, xq))
     g = lib.ggml_new_graph(c)
     lib.ggml_build_forward_expand(g, y)
     buf = lib.ggml_backend_alloc_ctx_tensors(c, backend)
@@ -313,14 +324,17 @@ def rowsplit_prefill(lib, backend, dist, world, rank, device, torch, steps=5, K=
     G.tensor_set(lib, w, wq)
     if rank == 0:
         G.tensor_set(lib, x, synth.uniform(43, K * B))
-    x_t = torch_view(torch, lib, x, device)
+    xq_t = torch_bytes(torch, lib, xq, device)
     y_t = torch_view(torch, lib, y, device).view(B, rows)
     ypad_t = torch_view(torch, lib, ypad, device).view(B, rows_max)
     y_all = torch.empty(world * B * rows_max, dtype=torch.float32, device=device)
 
     def step():
-        dist.broadcast(x_t, src=0)
-        torch.cuda.current_stream().synchronize()  # X landed before the backend stream reads it
+        if rank == 0:
+            lib.ggml_backend_graph_compute(backend, gq)
+            lib.ggml_backend_synchronize(backend)  # the quants are written before RCCL reads them
+        dist.broadcast(xq_t, src=0)
+        torch.cuda.current_stream().synchronize()  # Xq landed before the backend stream reads it
         lib.ggml_backend_graph_compute(backend, g)
         if rows != rows_max:
             ypad_t[:, :rows].copy_(y_t)
@@ -340,7 +354,8 @@ def rowsplit_prefill(lib, backend, dist, world, rank, device, torch, steps=5, K=
 
     dt = timed_region(run, sync, dist, device)
     y_full = reassemble_rows(y_all.cpu().numpy(), N, world, B)
-    res = {"workload": f"Q4_K {K}x{N} x B={B}, rows split over {world} ranks: RCCL broadcast of X, local GEMM, RCCL all-gather of Y",
+    res = {"workload": f"Q4_K {K}x{N} x B={B}, rows split over {world} ranks: X quantized to Q8_K once on rank 0, RCCL broadcast "
+                       f"of the {int(lib.ggml_nbytes(xq))} quant bytes, local GEMM, RCCL all-gather of Y",
            "rows_per_rank": rows, "TFLOP/s": round(2.0 * K * N * B * steps / dt / 1e12, 2),
            "us_per_step": round(dt / steps * 1e6, 2)}
     res.update(rowsplit_parity(y_full, K, N, B))
@@ -553,22 +568,34 @@ def main():
             "note": "one mul_mat per graph_compute, 32 weight copies round-robin; HIP events over 256 graphs"}
         w1.free()
         # configs[4]: batched prefill Q4_K 4096x4096 on MFMA tiles (per GPU; the 8-GPU run shards
-        # the 512 prompt columns, 64 per GPU), plus the mid-batch sizes
+        # the 512 prompt columns, 64 per GPU), plus the mid-batch sizes. 32 rotated weight copies
+        # (288 MiB, more than the 256 MB Infinity Cache): R independent mul_mats per graph (grouped
+        # launches), and the same mul_mat alone in its own graph (a dependent layer's shape)
+        RP = 32
         for bb in (512, 64, 32, 16):
-            w3 = MulMatWorkload(lib, backend, 12, 4096, 4096, bb, 8)
+            w3 = MulMatWorkload(lib, backend, 12, 4096, 4096, bb, RP)
             for _ in range(3):
                 w3.step()
             lib.ggml_backend_synchronize(backend)
             ms = event_time_per_step(torch, w3, stream_ptr, iters=10)
-            flops = 2.0 * 4096 * 4096 * bb * 8
-            us = ms * 1e3 / 8
+            flops = 2.0 * 4096 * 4096 * bb * RP
+            us = ms * 1e3 / RP
+            flops_per = flops / RP
             e = {"TFLOP/s": round(flops / (ms / 1e3) / 1e12, 2), "us_per_mul_mat": round(us, 2),
                  "GB/s_effective": round(unit_bytes(12, 4096, 4096, bb) / (us / 1e6) / 1e9, 1),
-                 "launches_per_mul_mat": lib.ggml_backend_mi355x_last_launch_count(backend) / 8}
+                 "launches_per_mul_mat": lib.ggml_backend_mi355x_last_launch_count(backend) / RP, "rotated_copies": RP}
+            w3.free()
+            w4 = RotatedSingle(lib, backend, 12, 4096, 4096, bb, RP)
+            for _ in range(2 * RP):
+                w4.step()
+            lib.ggml_backend_synchronize(backend)
+            ms1 = event_time_per_step(torch, w4, stream_ptr, iters=4 * RP)
+            e["us_per_mul_mat_one_per_graph"] = round(ms1 * 1e3, 2)
+            w4.free()
             if bb == 512:
                 peak = I8_PEAK_TOPS / 2  # Q4_K: two int8 weight planes per weight (mmq_exact.hip)
-                e["roofline"] = {"bound": "mfma", "achieved": round(flops / 8 / (us / 1e6) / 1e12, 2), "peak": peak,
-                                 "unit": "TFLOP/s", "frac": round(flops / 8 / (us / 1e6) / 1e12 / peak, 4),
+                e["roofline"] = {"bound": "mfma", "achieved": round(flops_per / (us / 1e6) / 1e12, 2), "peak": peak,
+                                 "unit": "TFLOP/s", "frac": round(flops_per / (us / 1e6) / 1e12 / peak, 4),
                                  "note": "useful 2*N*K*B / HIP-event time of the whole mul_mat (activation quantizer + GEMM) vs "
                                          "the dense I8 MFMA peak (5 POP/s) / 2: the exact block sums run as two "
                                          "v_mfma_i32_32x32x32_i8 per 32-deep K step (Q4_K weight planes q*(sc bit field))"}
@@ -578,7 +605,6 @@ def main():
                                  "note": "algorithmic bytes (weights + f32 activations + f32 outputs) / HIP-event time of the "
                                          "whole mul_mat (activation quantizer + GEMM)"}
             sweep[f"q4_K_4096x4096_b{bb}_prefill"] = e
-            w3.free()
         result["sweep"] = sweep
 
     if world > 1 and not args.no_sweep:

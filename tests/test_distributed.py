@@ -104,28 +104,50 @@ def test_row_shard_covers_exactly():
 
 
 def _rowsplit_worker(rank, world, port, K, N, B, out_dir):
-    """bench.rowsplit_prefill's exchange on gloo: broadcast X from rank 0, each rank computes its
-    rows of W.X with the reference CPU backend, all-gather the padded row slices, reassemble."""
+    """bench.rowsplit_prefill's exchange on gloo: rank 0 quantizes X to Q8_K rows (the weight's
+    vec_dot type) and broadcasts the bytes, each rank computes its rows of W.Xq with the reference
+    CPU backend (MUL_MAT reads a Q8_K src1 as it lies), all-gather the padded row slices,
+    reassemble."""
+    from ggml_mi355x import synth
+    Q8_K = 15
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ref = G.Lib([REF_LIB], isolated=True)
         cpu = ref.ggml_backend_cpu_init()
         ref.ggml_backend_cpu_set_n_threads(cpu, 2)
+        with G.Context(ref, 1024, no_alloc=True):
+            pass  # ggml_init: the fp16 tables ggml_quantize_chunk's rounding reads
         r0, r1 = bench.row_shard(N, world, rank)
         rows = r1 - r0
         rows_max = max(bench.row_shard(N, world, r)[1] - bench.row_shard(N, world, r)[0] for r in range(world))
-        from ggml_mi355x import synth
-        x = torch.from_numpy(synth.uniform(43, K * B)) if rank == 0 else torch.zeros(K * B)
-        dist.broadcast(x, src=0)
+        x = synth.uniform(43, K * B)
+        nq = K // 256 * 292 * B
+        if rank == 0:  # X -> Q8_K rows on the reference CPU (GGML_OP_CPY: quantize_row_q8_K)
+            ovh = ref.ggml_tensor_overhead() * 4 + ref.ggml_graph_overhead()
+            with G.Context(ref, ovh, no_alloc=True) as c:
+                xt = ref.ggml_new_tensor_2d(c.ctx, G.GGML_TYPE_F32, K, B)
+                q = ref.ggml_cpy(c.ctx, xt, ref.ggml_new_tensor_2d(c.ctx, Q8_K, K, B))
+                g = ref.ggml_new_graph(c.ctx)
+                ref.ggml_build_forward_expand(g, q)
+                buf = ref.ggml_backend_alloc_ctx_tensors(c.ctx, cpu)
+                G.tensor_set(ref, xt, x)
+                ref.ggml_backend_graph_compute(cpu, g)
+                xq = torch.from_numpy(G.tensor_get(ref, q, np.uint8).copy())
+                ref.ggml_backend_buffer_free(buf)
+        else:
+            xq = torch.zeros(nq, dtype=torch.uint8)
+        dist.broadcast(xq, src=0)
         wf = synth.uniform(42, K * N)
-        mine = bench.MulMatWorkload(ref, cpu, 12, K, rows, B, 1, seed=5)
         wq = np.empty(G.row_size(12, K) * rows, np.uint8)
         ref.ggml_quantize_chunk(12, wf[r0 * K:r1 * K].ctypes.data, wq.ctypes.data, 0, rows, K, None)
-        G.tensor_set(ref, mine.w[0], wq)
-        G.tensor_set(ref, mine.x[0], x.numpy())
-        ref.ggml_backend_graph_compute(cpu, mine.graph)
-        y = G.tensor_get(ref, mine.y[0]).reshape(B, rows)
+
+        def build(c):
+            wt = ref.ggml_new_tensor_2d(c, 12, K, rows)
+            xt = ref.ggml_new_tensor_2d(c, Q8_K, K, B)
+            return [(wt, wq), (xt, xq.numpy())], ref.ggml_mul_mat(c, wt, xt)
+
+        y = G.graph_once(ref, cpu, build).reshape(B, rows)
         ypad = np.zeros((B, rows_max), np.float32)
         ypad[:, :rows] = y
         y_all = torch.empty(world * B * rows_max)
@@ -136,11 +158,10 @@ def _rowsplit_worker(rank, world, port, K, N, B, out_dir):
             wq_full = np.empty(G.row_size(12, K) * N, np.uint8)
             ref.ggml_quantize_chunk(12, wf.ctypes.data, wq_full.ctypes.data, 0, N, K, None)
             G.tensor_set(ref, full.w[0], wq_full)
-            G.tensor_set(ref, full.x[0], x.numpy())
+            G.tensor_set(ref, full.x[0], x)
             ref.ggml_backend_graph_compute(cpu, full.graph)
             np.save(os.path.join(out_dir, "full.npy"), G.tensor_get(ref, full.y[0]).reshape(B, N))
             full.free()
-        mine.free()
         ref.ggml_backend_free(cpu)
     finally:
         dist.destroy_process_group()
