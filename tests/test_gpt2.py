@@ -274,14 +274,18 @@ def test_gpt2_decode_launches_per_token(model_path, quantized_paths, qtype, orde
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
-def test_quantized_gpt2_default_order_close_to_reference_cpu(quantized_paths):
-    """Default (fast) order on the q4_k model: per-op error is f32 summation order only (<= 1e-5,
-    test_mul_mat_gpu), amplified by the model's activation re-quantization to at most the
-    reference's own 1-ulp sensitivity."""
+@pytest.mark.parametrize("qtype", QTYPES)
+def test_quantized_gpt2_default_order_close_to_reference_cpu(quantized_paths, qtype):
+    """Default (fast) order on the quantized models: per-op error is f32 summation order only (<= 1e-5,
+    test_mul_mat_gpu), amplified by the model's activation re-quantization to the reference's own
+    1-ulp sensitivity (1.7e-2, test_reference_quantized_gpt2_is_ulp_sensitive). Measured on MI355X
+    (profiles/r03o_gpt2_default_order.txt): q4_0 1.4e-2, q8_0 1.6e-2, q4_k 2.1e-2, q5_k 2.1e-2 of
+    max|logit|; bound 3e-2. Bit identity: mmv_order=1 (test above)."""
     def check(ours, rm):
         errs, _ = _teacher_forced_both(ours, rm, n_decode=12)
-        assert max(errs) <= 5e-2, errs
-    _gpu_vs_ref(quantized_paths["q4_k"], check)
+        print(f"{qtype}: default order max rel logit error {max(errs):.3e}")
+        assert max(errs) <= 3e-2, errs
+    _gpu_vs_ref(quantized_paths[qtype], check)
 
 
 @pytest.mark.gpu
