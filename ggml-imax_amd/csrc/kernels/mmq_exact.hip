@@ -79,6 +79,22 @@ __device__ __forceinline__ void cfold(float & g, float & y, float t, int sb, int
     g = pos == 0 ? t : g + t;
     if (pos == gs - 1 || sb == S - 1) y = sb < gs ? g : y + g;
 }
+// the same for a whole accumulator (sb wave-uniform) without per-element selects: a group sum
+// starts at -0 (-0 + t == t for every float t, signed zeros and NaNs included), y starts at -0 too
+// (callers initialize it so); the resets are uniform branches kept as branches (the empty asm
+// stops their if-conversion into 16 v_cndmask per superblock)
+__device__ __forceinline__ void cfold_vec(f32x16 & g, f32x16 & y, const f32x16 & t, int sb, int gs, int S) {
+    const int pos = sb % gs;
+    if (pos == 0) {
+        asm volatile("" ::: "memory");
+        g = f32x16(-0.0f);
+    }
+    g = g + t;
+    if (pos == gs - 1 || sb == S - 1) {
+        asm volatile("" ::: "memory");
+        y = y + g;
+    }
+}
 
 template <int TYPE>
 struct XFmt {
@@ -443,7 +459,7 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
         dq_rows(buf, raw, pr);
     };
 
-    f32x16 y = {}, gsum = {};
+    f32x16 y = f32x16(-0.0f), gsum = {};  // y = -0: cfold_vec's first group sum lands exactly
     const int gs = cfold_gs(S);
     // The raw weights of superblock sb + 1 are dequantized into LDS at the end of stage sb; they
     // were requested LEAD stages earlier (a ring of LEAD raw slots: HBM latency is several stage
@@ -540,6 +556,7 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
                 xs.bu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, sc * 32 + 16 * h, 0, 0));
                 xs.da = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, sc * 4, 0, 0));
             }
+            f32x16 tv;
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const float4 dw4 = *(const float4 *) (dwv + 32 * rw + 8 * g + 4 * h);
@@ -552,13 +569,10 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
                     int T = acc[NP - 1][i];
 #pragma unroll
                     for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][i];
-                    const float term = mmqx_term(T, Uv[i], dw[e], dm[e], da);
-                    float gg = gsum[i], yy = y[i];
-                    cfold(gg, yy, term, sb, gs, S);
-                    gsum[i] = gg;
-                    y[i] = yy;
+                    tv[i] = mmqx_term(T, Uv[i], dw[e], dm[e], da);
                 }
             }
+            cfold_vec(gsum, y, tv, sb, gs, S);
         }
         stamp(4 + 4 * sb);
         mi_lds_barrier();
@@ -775,6 +789,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
             }
             __builtin_amdgcn_wave_barrier();
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (first) {  // uniform: a group starts at -0 (-0 + t == t), kept a branch (no selects)
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int t = 0; t < NC; t++) gsum[t] = f32x16(-0.0f);
+            }
 #pragma unroll
             for (int t = 0; t < NC; t++) {
                 const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu[t], mu, f32x16{}, 0, 0, 0);
@@ -791,7 +810,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
 #pragma unroll
                         for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[t][p][el];
                         const float term = mmqx_term(T, Uv[el], dw, dm, dav[e]);
-                        gsum[t][el] = first ? term : gsum[t][el] + term;
+                        gsum[t][el] = gsum[t][el] + term;
                     }
                 }
             }
