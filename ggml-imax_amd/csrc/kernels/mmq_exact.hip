@@ -1057,7 +1057,8 @@ __global__ __launch_bounds__(64 * NWV, NR == 2 ? 2 : 1) void k_mmq0x(mi_mmx_grou
     constexpr int ND = Q8 ? 9 : 5;            // dwords covering a block (2-byte aligned)
     constexpr int XR = 256 + 16;              // LDS row stride of the operand plane
     constexpr int kPlane = XBM * XR;
-    constexpr int kBuf = kPlane + 8 * XBM * 4;  // + d_w [block][row]
+    constexpr int DWS = XBM + 4;              // d_w row stride: a row's 8 blocks on 8 distinct banks
+    constexpr int kBuf = kPlane + 8 * DWS * 4;  // + d_w [block][row]
     constexpr int XBN_ = NR == 2 ? 32 * NWV : 16 * NWV;
     constexpr int ROWP = 8 / NWV;             // staging passes (rows per thread)
     constexpr int RSTEP = 8 * NWV;
@@ -1122,7 +1123,7 @@ __global__ __launch_bounds__(64 * NWV, NR == 2 ? 2 : 1) void k_mmq0x(mi_mmx_grou
         char * pl = lds + buf * kBuf + row * XR + 32 * j;
         float * dwv = (float *) (lds + buf * kBuf + kPlane);
         const uint32_t dbits = (bal ? raw.w[0] >> 16 : raw.w[0]) & 0xFFFF;
-        dwv[j * XBM + row] = mi_h2f((uint16_t) dbits);
+        dwv[j * DWS + row] = mi_h2f((uint16_t) dbits);
         // quants start at byte bal + 2 of w[0]: 2 -> alignbyte, 4 -> whole dwords from w[1]
         if constexpr (Q8) {
             uint32_t t[8];
@@ -1145,7 +1146,12 @@ __global__ __launch_bounds__(64 * NWV, NR == 2 ? 2 : 1) void k_mmq0x(mi_mmx_grou
         }
     };
 
-    f32x16 y[NR] = {}, gsum[NR] = {};
+    f32x16 y[NR], gsum[NR];
+#pragma unroll
+    for (int ri = 0; ri < NR; ri++) {
+        y[ri] = f32x16(-0.0f);
+        gsum[ri] = f32x16{};
+    }
     Raw raw[LEAD][ROWP];
     Xs xs;
 #pragma unroll
@@ -1169,7 +1175,8 @@ __global__ __launch_bounds__(64 * NWV, NR == 2 ? 2 : 1) void k_mmq0x(mi_mmx_grou
         const char * arow_p = base + (32 * rw + r) * XR + 16 * h;
         const float * dwv = (const float *) (base + kPlane);
         const int un = u + 1 < S ? u + 1 : S - 1;
-        if (u % gs == 0) {
+        if (u % gs == 0) {  // uniform; kept a branch (no per-element selects)
+            asm volatile("" ::: "memory");
 #pragma unroll
             for (int ri = 0; ri < NR; ri++) gsum[ri] = f32x16{};
         }
@@ -1183,7 +1190,7 @@ __global__ __launch_bounds__(64 * NWV, NR == 2 ? 2 : 1) void k_mmq0x(mi_mmx_grou
             const f32x16 tv = __builtin_bit_cast(f32x16, T) - 12582912.0f;  // exact (float) T
 #pragma unroll
             for (int g = 0; g < 4; g++) {
-                const float4 d4 = *(const float4 *) (dwv + kk * XBM + 32 * (rw + ri) + 8 * g + 4 * h);
+                const float4 d4 = *(const float4 *) (dwv + kk * DWS + 32 * (rw + ri) + 8 * g + 4 * h);
                 const float dw[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
@@ -1226,11 +1233,10 @@ __global__ __launch_bounds__(64 * NWV, NR == 2 ? 2 : 1) void k_mmq0x(mi_mmx_grou
             xs.da[kk] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, bcol * 4, so, 0));
         }
         combine(7, NR - 1, acc[1]);
-        if (u % gs == gs - 1 || u == S - 1) {
+        if (u % gs == gs - 1 || u == S - 1) {  // y starts at -0: -0 + g0 == g0 exactly
+            asm volatile("" ::: "memory");
 #pragma unroll
-            for (int ri = 0; ri < NR; ri++)
-#pragma unroll
-                for (int i = 0; i < 16; i++) y[ri][i] = u < gs ? gsum[ri][i] : y[ri][i] + gsum[ri][i];
+            for (int ri = 0; ri < NR; ri++) y[ri] = y[ri] + gsum[ri];
         }
         mi_lds_barrier();
     };

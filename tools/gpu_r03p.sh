@@ -7,5 +7,5 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 python -u -m pytest tests/test_prefill_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
-export PF_TYPES=q4_K,q5_K PF_R=32 MMQ_VARIANTS=0
+export PF_TYPES=q4_0,q8_0 PF_R=32 MMQ_VARIANTS=0
 timeout -k 10 300 python3 -u tools/prefill_bench.py 512 256 64 32 2>&1 | grep --line-buffered -v amdgpu.ids | tee "$OUT/pf.txt"
