@@ -617,6 +617,236 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
 }
 
 
+// ---- long prompts, warp-specialized: loader waves stage, MFMA waves compute ----------------------
+// k_mmqx's tile (64 weight rows x 128 columns) and stage structure, with the roles split: 8 MFMA
+// waves (rw, cw) compute their 32 x 32 tiles from the LDS planes of superblock sb while 4 loader
+// waves turn superblock sb + 1 (requested LEAD stages earlier) into the other LDS buffer's planes
+// and row operands. Every wave passes the same one barrier per stage. In k_mmqx each wave does its
+// MFMA steps, its share of the dequantization and the combine, and the barrier then waits for the
+// slowest; here the MFMA waves' stage is only MFMAs + combine. Same operands, same canonical combine
+// (mmqx_term, cfold_vec): bit-identical to k_mmqx.
+template <int TYPE, int LEAD>
+__global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
+    MI_MMX_MEMBER(g);
+    using F = XFmt<TYPE>;
+    constexpr int NP = F::NP;
+    constexpr int XR = 256 + 16;
+    constexpr int kPlane = XBM * XR;
+    constexpr int kRow = XBM * 32 + XBM * 8;
+    constexpr int kBuf = NP * kPlane + kRow;
+    constexpr int NCW = 8;       // MFMA waves
+    constexpr int ROWP = 2;      // loader threads (256) x 2 rows = 64 rows
+    constexpr int RSTEP = 32;
+    __shared__ __attribute__((aligned(16))) char lds[2 * kBuf];
+
+    const int tid = (int) threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const bool loader = wave >= NCW;  // wave-uniform role
+    const int rw = wave & 1, cw = (wave >> 1) & 3;
+    const int64_t ncols = act.ncols;
+    const int64_t nrt = (N + XBM - 1) / XBM;
+    const int64_t n0 = (mmx_tile % nrt) * XBM, b0 = (mmx_tile / nrt) * XBN;
+    const int S = (int) (K / 256);
+    const int gs = cfold_gs(S);
+
+    // loader role: thread lt = tid - 512, row ar (+ 32), 16-byte quant chunk c8 of the superblock
+    const int lt = tid - 64 * NCW;
+    const int ar = (lt >> 3) & 31, c8 = lt & 7;
+    const int nrows = (int) std::min<int64_t>(XBM, N - n0);
+    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
+    uint32_t wrow[ROWP];
+#pragma unroll
+    for (int pr = 0; pr < ROWP; pr++) wrow[pr] = (uint32_t) (std::min(ar + pr * RSTEP, nrows - 1) * nb01);
+    const uint32_t qoff = (F::Q5 ? 48 : 16) + 16 * c8;
+    const int j0 = 2 * (c8 >> 1), hf = c8 & 1;
+
+    // MFMA role: column b0 + 32 cw + (lane & 31), 16 bytes at 16 (lane >> 5)
+    const int r = lane & 31, h = lane >> 5;
+    const uint32_t bcol = (uint32_t) std::min<int64_t>(b0 + 32 * cw + r, ncols - 1);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
+    const uint32_t xcol = bcol * 32 + 16 * h;
+    const uint32_t xstep = (uint32_t) ncols * 32;
+
+    struct Raw {
+        uint4 hdr, qs, qh;
+    };
+    auto load_raw = [&](Raw & raw, int sb, int pr) {
+        sb = sb < S ? sb : S - 1;
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * F::BS);
+        raw.hdr = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wrow[pr], so, 0));
+        raw.qs = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wrow[pr] + qoff, so, 0));
+        if constexpr (F::Q5) raw.qh = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wres, wrow[pr] + 16 + 16 * hf, so, 0));
+    };
+    struct Xs {
+        i32x4 q[8];
+        half8 bu;
+        float da;
+    };
+    auto load_x = [&](Xs & xs, int sb) {
+        sb = sb < S ? sb : S - 1;
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((sb * 8 + kk) * (int) xstep);
+            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol, so, 0));
+        }
+        const uint32_t sc = (uint32_t) sb * (uint32_t) ncols + bcol;
+        xs.bu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, sc * 32 + 16 * h, 0, 0));
+        xs.da = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, sc * 4, 0, 0));
+    };
+    struct KSel {
+        bool hi;
+        uint32_t sh, w, shh, wh;
+    };
+    auto ksel = [](int j) { const int jj = j & 3; const bool hi = j >= 4; return KSel{hi, (uint32_t) (8 * jj), hi ? 4u : 6u, (uint32_t) (8 * jj + 6), hi ? 2u : 0u}; };
+    const KSel k0 = ksel(j0), k1 = ksel(j0 + 1), kc = ksel(c8);
+    auto kscale = [](const KSel & k, uint32_t w0, uint32_t w2) {
+        return __builtin_amdgcn_ubfe(k.hi ? w2 : w0, k.sh, k.w) | (__builtin_amdgcn_ubfe(w0, k.shh, k.wh) << 4);
+    };
+    auto kmin = [](const KSel & k, uint32_t w1, uint32_t w2) {
+        return __builtin_amdgcn_ubfe(k.hi ? w2 : w1, k.hi ? k.sh + 4 : k.sh, k.w) | (__builtin_amdgcn_ubfe(w1, k.shh, k.wh) << 4);
+    };
+    // one loader thread's share of a superblock (rows ar, ar + 32) into LDS buffer `buf`
+    auto store_stage = [&](int buf, const Raw & raw, int pr) {
+        const int row = ar + pr * RSTEP;
+        const uint32_t sc0 = kscale(k0, raw.hdr.y, raw.hdr.w), sc1 = kscale(k1, raw.hdr.y, raw.hdr.w);
+        const uint32_t q[4] = {raw.qs.x, raw.qs.y, raw.qs.z, raw.qs.w};
+        const uint32_t qh[4] = {raw.qh.x, raw.qh.y, raw.qh.z, raw.qh.w};
+        uint32_t lo[4], hi[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            lo[i] = q[i] & 0x0F0F0F0Fu;
+            hi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
+            if constexpr (F::Q5) {
+                lo[i] |= ((qh[i] >> j0) & 0x01010101u) << 4;
+                hi[i] |= ((qh[i] >> (j0 + 1)) & 0x01010101u) << 4;
+            }
+        }
+        char * pl0 = lds + buf * kBuf + row * XR + 32 * j0 + 16 * hf;
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            const uint32_t f0 = F::factor((int) sc0, p), f1 = F::factor((int) sc1, p);
+            *(uint4 *) (pl0 + p * kPlane) = make_uint4(mulb(lo[0], f0), mulb(lo[1], f0), mulb(lo[2], f0), mulb(lo[3], f0));
+            *(uint4 *) (pl0 + p * kPlane + 32) = make_uint4(mulb(hi[0], f1), mulb(hi[1], f1), mulb(hi[2], f1), mulb(hi[3], f1));
+        }
+        char * ro = lds + buf * kBuf + NP * kPlane;
+        const uint32_t mc = kmin(kc, raw.hdr.z, raw.hdr.w);
+        *(uint32_t *) (ro + row * 32 + 4 * c8) = (uint32_t) mi_f2h((float) mc) | ((uint32_t) mi_f2h((float) (64 * mc)) << 16);
+        if (c8 < 2) ((float *) (ro + XBM * 32))[c8 * XBM + row] = mi_h2f((uint16_t) (c8 == 0 ? (raw.hdr.x & 0xFFFF) : (raw.hdr.x >> 16)));
+    };
+
+    // The roles run separate loops (so their registers are not live at once), each passing the
+    // same 1 + S barriers.
+    if (loader) {
+        Raw raw[LEAD][ROWP];
+#pragma unroll
+        for (int pr = 0; pr < ROWP; pr++) {
+            Raw r0;
+            load_raw(r0, 0, pr);
+            store_stage(0, r0, pr);
+        }
+#pragma unroll
+        for (int u = 0; u < LEAD; u++)
+#pragma unroll
+            for (int pr = 0; pr < ROWP; pr++) load_raw(raw[u][pr], 1 + u, pr);
+        mi_lds_barrier();
+        // S % LEAD == 0 (host-checked) and no branch in the body, so the waits are exact (vmcnt
+        // retires in order: a slot's loads wait only for themselves). Past the end the loads are
+        // clamped re-reads and the last store fills the buffer nobody reads any more.
+        for (int sb0 = 0; sb0 < S; sb0 += LEAD) {
+#pragma unroll
+            for (int u = 0; u < LEAD; u++) {
+                const int sb = sb0 + u;
+                // superblock sb + 1 into the other buffer (its readers passed the last barrier),
+                // then the slot's next request
+#pragma unroll
+                for (int pr = 0; pr < ROWP; pr++) store_stage((sb + 1) & 1, raw[u][pr], pr);
+#pragma unroll
+                for (int pr = 0; pr < ROWP; pr++) load_raw(raw[u][pr], sb + 1 + LEAD, pr);
+                mi_lds_barrier();
+            }
+        }
+        return;
+    }
+
+    f32x16 y = f32x16(-0.0f), gsum = {};
+    Xs xs;
+    load_x(xs, 0);
+    mi_lds_barrier();
+    for (int sb = 0; sb < S; sb++) {
+        const char * base = lds + (sb & 1) * kBuf;
+        const char * arow_p = base + (32 * rw + r) * XR + 16 * h;
+        const int nx = sb + 1 < S ? sb + 1 : S - 1;
+        const uint32_t kbn = (uint32_t) nx * 8;
+        i32x16 acc[NP];
+        i32x4 an[2][NP];
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            an[0][p] = *(const i32x4 *) (arow_p + p * kPlane);
+            an[1][p] = *(const i32x4 *) (arow_p + p * kPlane + 32);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            i32x4 a[NP];
+#pragma unroll
+            for (int p = 0; p < NP; p++) a[p] = an[kk & 1][p];
+            if (kk < 6) {
+#pragma unroll
+                for (int p = 0; p < NP; p++) an[kk & 1][p] = *(const i32x4 *) (arow_p + p * kPlane + 32 * (kk + 2));
+            }
+#pragma unroll
+            for (int p = 0; p < NP; p++)
+                acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], xs.q[kk], kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
+            const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((int) (kbn + kk) * (int) xstep);
+            xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol, so, 0));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const char * ro = base + NP * kPlane;
+        const float * dwv = (const float *) (ro + XBM * 32);
+        const half8 au = *(const half8 *) (ro + (32 * rw + r) * 32 + 16 * h);
+        const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(au, xs.bu, f32x16{}, 0, 0, 0);
+        const float da = xs.da;
+        {
+            const uint32_t sc = (uint32_t) nx * (uint32_t) ncols + bcol;
+            xs.bu = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(ures, sc * 32 + 16 * h, 0, 0));
+            xs.da = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, sc * 4, 0, 0));
+        }
+        f32x16 tv;
+#pragma unroll
+        for (int gq = 0; gq < 4; gq++) {
+            const float4 dw4 = *(const float4 *) (dwv + 32 * rw + 8 * gq + 4 * h);
+            const float4 dm4 = *(const float4 *) (dwv + XBM + 32 * rw + 8 * gq + 4 * h);
+            const float dw[4] = {dw4.x, dw4.y, dw4.z, dw4.w};
+            const float dm[4] = {dm4.x, dm4.y, dm4.z, dm4.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int i2 = 4 * gq + e;
+                int T = acc[NP - 1][i2];
+#pragma unroll
+                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][i2];
+                tv[i2] = mmqx_term(T, Uv[i2], dw[e], dm[e], da);
+            }
+        }
+        cfold_vec(gsum, y, tv, sb, gs, S);
+        mi_lds_barrier();
+    }
+
+    const int64_t b = b0 + 32 * cw + r;
+    if (b >= ncols) return;
+    float * out = (float *) ((char *) dst + b * ycol);
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) {
+        const int64_t n = n0 + 32 * rw + 8 * gq + 4 * h;
+        if (n + 3 < N) {
+            *(float4 *) (out + n) = make_float4(y[4 * gq], y[4 * gq + 1], y[4 * gq + 2], y[4 * gq + 3]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[4 * gq + e];
+        }
+    }
+}
+
 // ---- short prompts, pipelined: 8 waves per tile, one superblock group each -----------------------
 // A workgroup computes one tile of 32 weight rows x 32 NC prompt columns; wave w computes the terms
 // of superblock group w of the canonical order (cfold: kCfoldGroups = 8 contiguous groups) one
@@ -1675,6 +1905,13 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         return;
     }
     const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));
+    // warp-specialized k_mmqw (4 loader + 8 MFMA waves; Q4_K B=512 32.1 -> 31.2 us, Q5_K 46.2 ->
+    // 43.8 us grouped, profiles/r03r_prefill_mmqw.txt) unless variant bit 2^28 asks for k_mmqx
+    if (!(var & ((1 << 28) | 64 | 1024)) && (K / 256) % 4 == 0) {
+        if (type == 12) hipLaunchKernelGGL((k_mmqw<12, 4>), grid, dim3(768), 0, s, g);
+        else hipLaunchKernelGGL((k_mmqw<13, 4>), grid, dim3(768), 0, s, g);
+        return;
+    }
     // weight ring depth LEAD (variant bits: 64 -> 1, default 4). (Fully unrolling the stage loop
     // for K = 4096, SCT = 16, spills: the compiler hoists loads across stages.)
 #define MI_MMQX_T(TY, LD) hipLaunchKernelGGL((k_mmqx<TY, false, 0, LD, 0>), grid, dim3(512), 0, s, g)

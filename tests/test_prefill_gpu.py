@@ -153,7 +153,7 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
     if tname in ("q4_0", "q8_0"):  # k_mmq0p (16), k_mmq0x full / half width (128, 128 | 65536)
         variants = [0, 16, 128, 128 | 65536, 128 | (1 << 24), 128 | (1 << 25)]
     else:
-        variants = [0, 2048, 1 << 27, 128 | 131072, 128 | 65536] + ([1 << 21] if B <= 16 else [])
+        variants = [0, 2048, 1 << 27, 128 | 131072, 128 | 65536, 128 | 131072 | (1 << 28)] + ([1 << 21] if B <= 16 else [])
     outs = {}
     try:
         for v in variants:
