@@ -625,7 +625,8 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
 // MFMA steps, its share of the dequantization and the combine, and the barrier then waits for the
 // slowest; here the MFMA waves' stage is only MFMAs + combine. Same operands, same canonical combine
 // (mmqx_term, cfold_vec): bit-identical to k_mmqx.
-template <int TYPE, int LEAD>
+// ABL 8: timing stamps of MFMA wave 0 (workgroups 0 and 97) into dst, as k_mmqx (results invalid)
+template <int TYPE, int LEAD, int ABL = 0>
 __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
     MI_MMX_MEMBER(g);
     using F = XFmt<TYPE>;
@@ -770,11 +771,26 @@ __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
         return;
     }
 
+    auto stamp = [&](int slot) {
+        if constexpr ((ABL & 8) != 0) {
+            const int wsel = blockIdx.x == 0 ? 0 : blockIdx.x == 97 ? 1 : -1;
+            if (wsel >= 0 && wave == 0 && lane == 0 && slot < 80) ((uint64_t *) dst)[wsel * 80 + slot] = __builtin_amdgcn_s_memtime();
+        }
+    };
+    auto rstamp = [&](int e) {
+        if constexpr ((ABL & 8) != 0) {
+            if (threadIdx.x == 0) ((uint64_t *) dst)[160 + 2 * blockIdx.x + e] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
+    rstamp(0);
+    stamp(0);
     f32x16 y = f32x16(-0.0f), gsum = {};
     Xs xs;
     load_x(xs, 0);
     mi_lds_barrier();
+    stamp(1);
     for (int sb = 0; sb < S; sb++) {
+        stamp(2 + 4 * sb);
         const char * base = lds + (sb & 1) * kBuf;
         const char * arow_p = base + (32 * rw + r) * XR + 16 * h;
         const int nx = sb + 1 < S ? sb + 1 : S - 1;
@@ -802,6 +818,7 @@ __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
             xs.q[kk] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, xcol, so, 0));
             __builtin_amdgcn_sched_barrier(0);
         }
+        stamp(3 + 4 * sb);
         const char * ro = base + NP * kPlane;
         const float * dwv = (const float *) (ro + XBM * 32);
         const half8 au = *(const half8 *) (ro + (32 * rw + r) * 32 + 16 * h);
@@ -829,7 +846,17 @@ __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
             }
         }
         cfold_vec(gsum, y, tv, sb, gs, S);
+        stamp(4 + 4 * sb);
         mi_lds_barrier();
+        stamp(5 + 4 * sb);
+    }
+    rstamp(1);
+    if constexpr ((ABL & 8) != 0) {
+        float t = 0.0f;
+#pragma unroll
+        for (int i2 = 0; i2 < 16; i2++) t += y[i2];
+        if (t == 1.2345e-30f) dst[4096 + threadIdx.x] = t;
+        return;
     }
 
     const int64_t b = b0 + 32 * cw + r;
@@ -1907,6 +1934,10 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));
     // warp-specialized k_mmqw (4 loader + 8 MFMA waves; Q4_K B=512 32.1 -> 31.2 us, Q5_K 46.2 ->
     // 43.8 us grouped, profiles/r03r_prefill_mmqw.txt) unless variant bit 2^28 asks for k_mmqx
+    if ((var & 1024) && (var & (1 << 29)) && type == 12) {  // k_mmqw timing stamps (results invalid)
+        hipLaunchKernelGGL((k_mmqw<12, 4, 8>), grid, dim3(768), 0, s, g);
+        return;
+    }
     if (!(var & ((1 << 28) | 64 | 1024)) && (K / 256) % 4 == 0) {
         if (type == 12) hipLaunchKernelGGL((k_mmqw<12, 4>), grid, dim3(768), 0, s, g);
         else hipLaunchKernelGGL((k_mmqw<13, 4>), grid, dim3(768), 0, s, g);
