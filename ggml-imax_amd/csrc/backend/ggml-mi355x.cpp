@@ -1475,7 +1475,7 @@ static int try_fuse_f16_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const
     if (pro && (overlaps(out, x) || (x->nb[1] % sizeof(float)) != 0)) return -1;
     if (pro && pro->parts) {
         // only the tree-order kernel sums partials
-        if (g_mi_tuning.mmv_order != 0 || !mi_mul_mat_f16_fast_supported(w->ne[0], x->ne[1], src_cols(x), nullptr, *pro)) return -1;
+        if (mi_mmv_order() != 0 || !mi_mul_mat_f16_fast_supported(w->ne[0], x->ne[1], src_cols(x), nullptr, *pro)) return -1;
         // x (stored by the first workgroup) must not be read by the others through the epilogue
         if ((bias_t && overlaps(x, bias_t)) || (res_t && overlaps(x, res_t))) return -1;
         mi_mul_mat_f16_fast(w->data, w->nb[1], w->ne[0], N, src_cols(x), nullptr, x->ne[1], (float *) out->data, out->nb[1], e, *pro,
@@ -1792,7 +1792,7 @@ static void plan_attention(const ggml_cgraph * g, const mi_uses & u, std::vector
 // as one k_attn_proj launch, whose result stays as per-head partial sums (ctx->pend) until its
 // consumer adds them (tree-order decode mode only). Returns the last node covered, or -1.
 static int try_fuse_attn_proj(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const mi_attn_plan & pl, const mi_uses & u) {
-    if (g_mi_tuning.mmv_order != 0 || g_mi_tuning.attn_variant != 0 || pl.d.N != 1) return -1;
+    if (mi_mmv_order() != 0 || g_mi_tuning.attn_variant != 0 || pl.d.N != 1) return -1;
     const int j = next_node(g, i);
     if (j < 0) return -1;
     ggml_tensor * mm = g->nodes[j];
@@ -2249,7 +2249,28 @@ static enum ggml_status mi_graph_plan_compute(ggml_backend_t backend, ggml_backe
     return GGML_STATUS_SUCCESS;
 }
 
+// mmv_order -1: the decode summation order of a graph. A quantized MUL_MAT whose src1 is computed
+// in the graph re-quantizes it (quantize_row_q8_*: round(x / d)), so a 1-ulp difference upstream can
+// move a quant by a whole step and the logits of a quantized model by ~1e-2
+// (tests/test_gpt2.py::test_reference_quantized_gpt2_is_ulp_sensitive): such graphs run every decode
+// reduction in the reference CPU's order (bit-identical). Any other graph (F16 models, a mul_mat of
+// input data) keeps the tree order, within 1e-5 of the reference per op.
+static int graph_decode_order(const ggml_cgraph * g) {
+    for (int i = 0; i < g->n_nodes; i++) {
+        const ggml_tensor * n = g->nodes[i];
+        if (n->op != GGML_OP_MUL_MAT || !ggml_is_quantized(n->src[0]->type)) continue;
+        const ggml_tensor * x = n->src[1];
+        while (x->view_src || x->op == GGML_OP_RESHAPE || x->op == GGML_OP_VIEW || x->op == GGML_OP_PERMUTE ||
+               x->op == GGML_OP_TRANSPOSE) {
+            x = x->view_src ? x->view_src : x->src[0];
+        }
+        if (x->op != GGML_OP_NONE) return 1;
+    }
+    return 0;
+}
+
 static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
+    tl_mi_graph_order = graph_decode_order(cgraph);
     {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         MI_CHECK(hipStreamIsCapturing(ctx->stream, &cs));
@@ -2661,7 +2682,7 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.mmq_variant = value;
         return true;
     }
-    if (strcmp(name, "mmv_order") == 0 && (value == 0 || value == 1)) {
+    if (strcmp(name, "mmv_order") == 0 && value >= -1 && value <= 1) {
         g_mi_tuning.mmv_order = value;
         return true;
     }

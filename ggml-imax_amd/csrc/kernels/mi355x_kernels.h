@@ -115,12 +115,17 @@ struct mi_tuning {
     int mmq_variant;  // prefill GEMM: 0 = k_mmq3 (activations in registers), 1 = k_mmq2 (activations via LDS)
     int attn_variant; // attention block: 0 = k_attn_fast where it fits, 1 = k_attn_ordered
     int attn_abl;     // timing ablations of k_attn_fast (0 = none; results invalid otherwise)
-    int mmv_order;    // decode GEMVs (quantized and F16): 1 = the reference CPU's summation order (bit-identical, slower), 0 = tree sums
+    int mmv_order;    // decode GEMVs (quantized and F16) and attention: 1 = the reference CPU's summation order (bit-identical,
+                      // slower), 0 = tree sums, -1 (default) = per graph: 1 where a quantized MUL_MAT consumes a value the
+                      // graph computes (its activation re-quantization would carry order differences forward), else 0
     int f16_waves;    // fast F16 decode GEMV: target waves on the chip (0 = automatic)
     int f16_rgs;      // fast F16 decode GEMV: row groups (4 rows) per workgroup (0 = automatic)
     int f16_ps_waves; // k_gemv_f16_ps (GEMV over summed partials): waves per workgroup, 2 / 4 / 8 (0 = automatic)
 };
 extern mi_tuning g_mi_tuning;
+// the order of the graph being launched when mmv_order is -1 (set by the backend per graph)
+extern thread_local int tl_mi_graph_order;
+inline int mi_mmv_order() { return g_mi_tuning.mmv_order >= 0 ? g_mi_tuning.mmv_order : tl_mi_graph_order; }
 size_t mi_mmv_fused_lds_bytes(int type, int64_t K, int64_t ncols);
 void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s);
 // Batched (prefill) mul_mat on MFMA: 2-D weights [K, N] of type Q4_0/Q8_0/Q4_K/Q5_K/F16,

@@ -37,7 +37,8 @@ static int env_int(const char * name, int def) {
 }
 
 // mmv_blocks == 0: size the grid from the kernel's residency (hipOccupancy...) per instance
-mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 0), env_int("GGML_MI355X_MMV_VARIANT", 0), env_int("GGML_MI355X_F16_VARIANT", 0), 0, env_int("GGML_MI355X_MMQ_VARIANT", 0), env_int("GGML_MI355X_ATTN_VARIANT", 0), env_int("GGML_MI355X_ATTN_ABL", 0), env_int("GGML_MI355X_MMV_ORDER", 0), env_int("GGML_MI355X_F16_WAVES", 0), env_int("GGML_MI355X_F16_RGS", 0), env_int("GGML_MI355X_F16_PS_WAVES", 0)};
+mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 0), env_int("GGML_MI355X_MMV_VARIANT", 0), env_int("GGML_MI355X_F16_VARIANT", 0), 0, env_int("GGML_MI355X_MMQ_VARIANT", 0), env_int("GGML_MI355X_ATTN_VARIANT", 0), env_int("GGML_MI355X_ATTN_ABL", 0), env_int("GGML_MI355X_MMV_ORDER", -1), env_int("GGML_MI355X_F16_WAVES", 0), env_int("GGML_MI355X_F16_RGS", 0), env_int("GGML_MI355X_F16_PS_WAVES", 0)};
+thread_local int tl_mi_graph_order = 0;
 
 namespace {
 
@@ -863,9 +864,9 @@ void launch_stream_nc(const mi_mmv_group & g, int variant, hipStream_t s) {
 
 template <class F>
 void launch_stream_ord(const mi_mmv_group & g, int variant, hipStream_t s) {
-    if (g_mi_tuning.mmv_order) {
+    if (mi_mmv_order()) {
         mi_mmv_group h = g;
-        h.abl = g_mi_tuning.mmv_order == 2;
+        h.abl = mi_mmv_order() == 2;
         launch_stream_nc<F, true>(h, variant, s);
     } else
         launch_stream_nc<F, false>(g, variant, s);
@@ -921,7 +922,7 @@ static void mi_mul_mat_q_fused_launch(mi_mmv_group & g, hipStream_t s) {
         case 13: launch_stream_ord<FmtKQ<true>>(g, variant, s); break;
         case 2:
             // tree order: pairs of blocks per item (variant % 10 == 1: single blocks)
-            if (!g_mi_tuning.mmv_order && variant % 10 != 1) launch_stream_nc<FmtQ0Pair, false>(g, variant, s);
+            if (!mi_mmv_order() && variant % 10 != 1) launch_stream_nc<FmtQ0Pair, false>(g, variant, s);
             else launch_stream_ord<FmtQ0<false>>(g, variant, s);
             break;
         case 8: launch_stream_ord<FmtQ0<true>>(g, variant, s); break;

@@ -868,7 +868,7 @@ bool mi_mul_mat_f16_fused_supported(int64_t K, int64_t ncols) { return ncols >= 
 void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh,
                           int64_t ncols, float * dst, size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro,
                           hipStream_t s) {
-    if (g_mi_tuning.mmv_order == 0 && mi_mul_mat_f16_fast_supported(K, ncols, x, xh, pro)) {
+    if (mi_mmv_order() == 0 && mi_mul_mat_f16_fast_supported(K, ncols, x, xh, pro)) {
         mi_mul_mat_f16_fast(W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s);
         return;
     }
@@ -886,7 +886,7 @@ void mi_mul_mat_f16_fused(const void * W, size_t nb01, int64_t K, int64_t N, con
 bool mi_attn_supported(int D, int n_kv) { return D >= 1 && D <= 256 && n_kv >= 1 && (size_t) (D + n_kv) * 4 <= 60 * 1024; }
 
 void mi_attn_ordered(const mi_attn_desc & a, const uint16_t * exp_table, hipStream_t s) {
-    if (g_mi_tuning.mmv_order == 0 && g_mi_tuning.attn_variant == 0 && mi_attn_tree_supported(a)) {
+    if (mi_mmv_order() == 0 && g_mi_tuning.attn_variant == 0 && mi_attn_tree_supported(a)) {
         mi_attn_tree(a, s);  // attn_fast.hip: tree order (the default decode mode)
         return;
     }

@@ -285,7 +285,7 @@ def test_gpt2_attention_block_exact(libs, n_past, N, order):
     try:
         a = run(rt, be)
     finally:
-        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
+        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", -1)
     b = run(ref, cpu)
     if order:
         assert_exact(a, b, "attention block")
@@ -414,7 +414,7 @@ def test_attention_projection_fused(libs, consumer, n_past):
     try:
         (y_1, o_1), n_ord = graph_outputs(rt, be, lambda c: build(rt, c))
     finally:
-        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
+        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", -1)
     (y_r, o_r), _ = graph_outputs(ref, cpu, lambda c: build(ref, c))
     eo = float(np.max(np.abs(o_a - o_r)) / np.max(np.abs(o_r)))
     ey = float(np.max(np.abs(y_a - y_r)) / np.max(np.abs(y_r)))

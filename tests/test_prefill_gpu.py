@@ -61,7 +61,7 @@ def _reference_y_by_gemv(rt, backend, t, wq, K, N, x, B):
         cols = [G.mul_mat_once(rt, backend, t, wq, K, N, np.ascontiguousarray(xs[c0:c0 + 8]).ravel(), min(8, B - c0))
                 for c0 in range(0, B, 8)]
     finally:
-        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
+        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", -1)
     return np.concatenate(cols).reshape(B, N)
 
 
