@@ -721,6 +721,7 @@ static int mm_act_kind(const mi_mm_desc & m, const ggml_tensor * src1) {
     // GGML_MI355X_MMQ_VARIANT bit 2^30 selects the f16 GEMM for the quantized types too (A/B
     // timing; the low bits are mmq_exact.hip's own kernel variants)
     if (kind <= 1 && (g_mi_tuning.mmq_variant & (1 << 30)) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01)) return kind == 1 ? 8 : 9;
+    if (kind == 2 && mi_mmf16p_supported(m.K, m.N, m.nb01, ncols, m.nb1)) return 2;  // k_mmf16p: plain f16 columns
     return (kind == 2 ? 2 : kind + 3) + (mi_mmq_wants_blocked() ? 3 : 0);
 }
 
@@ -765,6 +766,9 @@ static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const vo
             // Q4_K / Q5_K / Q4_0 / Q8_0: the exact-integer int8 MFMA GEMMs (mmq_exact.hip)
             const mi_act_mmx act = xkind == 8 ? mi_act_mmx_carve(xa, m.K, ncols) : mi_act_mmx0_carve(xa, m.K, ncols);
             mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, act, m.dst, m.nb1, ctx->stream);
+        } else if (xkind == 2 && mm_batched(m, src1) && mi_mmf16p_supported(m.K, m.N, m.nb01, ncols, m.nb1)) {
+            // F16 weights, a short prompt: 32 x 32 tiles with the K split over each tile's 4 waves
+            mi_mul_mat_f16p(m.W, m.nb01, m.K, m.N, (const uint16_t *) xa, ncols, m.dst, m.nb1, ctx->stream);
         } else if (xkind >= 3 || (xkind == 2 && mm_batched(m, src1))) {
             // the GEMM's activation operand: f16 for F16 weights, else f16(d * q) of the q8 quants
             // written by the quantizer itself (kinds 3/4, K-blocked 5..7)
@@ -1419,9 +1423,10 @@ static int collect_epilogue(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const 
         ggml_tensor * cp = g->nodes[j];
         if (cp->op != GGML_OP_CPY) break;
         const ggml_tensor * v = cp->src[0];
-        if (v->view_src != out || v->type != GGML_TYPE_F32 || v->nb[0] != sizeof(float) || v->view_offs % sizeof(float)) break;
+        // a row view of `out`, or `out` itself (e.g. the logits copied into a host staging tensor)
+        if ((v->view_src != out && v != out) || v->type != GGML_TYPE_F32 || v->nb[0] != sizeof(float) || v->view_offs % sizeof(float)) break;
         if (v->ne[2] != 1 || v->ne[3] != 1 || v->ne[1] != out->ne[1] || (v->ne[1] > 1 && v->nb[1] != out->nb[1])) break;
-        const int64_t r0 = (int64_t) (v->view_offs / sizeof(float));
+        const int64_t r0 = v == out ? 0 : (int64_t) (v->view_offs / sizeof(float));
         if (r0 + v->ne[0] > N) break;
         if (cp->type != GGML_TYPE_F32 || !ggml_is_contiguous(cp) || ggml_nelements(cp) != ggml_nelements(v)) break;
         if (overlaps(cp, w) || overlaps(cp, x) || overlaps(cp, out) || (bias_t && overlaps(cp, bias_t)) || (res_t && overlaps(cp, res_t))) break;

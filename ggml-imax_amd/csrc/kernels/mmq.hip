@@ -450,7 +450,91 @@ __global__ __launch_bounds__(256 * SK) void k_mmq3(const uint8_t * __restrict__ 
     }
 }
 
+// ---- F16 weights, short prompts (<= 128 columns): 32 x 32 tiles, K split over the 4 waves -------
+// k_mmq3's 64 x 128 tiles give N / 64 workgroups at B <= 128 (64 of the 256 CUs at N = 4096). Here
+// a workgroup computes 32 weight rows x 32 prompt columns and wave w the K range [w K/4, (w+1) K/4)
+// on v_mfma_f32_32x32x16_f16, operands straight from global memory into a register ring (no LDS
+// staging): per 64-deep chunk a lane loads 64 contiguous bytes of its weight row (row n0 + lane % 32,
+// halves k + 32 (lane / 32) ..) and the same 64 bytes of its activation column (plain f16 [ncols][K]
+// layout), and step s of the chunk takes their s-th 16 bytes -- a K permutation applied to both
+// operands alike (the MFMA sums the same products). The four partial tiles meet in LDS and are
+// added in wave order. Products of fp16 values are exact in f32; only the summation order differs
+// from the reference's ggml_vec_dot_f16 (~1e-7 relative).
+template <int PF>
+__global__ __launch_bounds__(256, 2) void k_mmf16p(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                   const uint16_t * __restrict__ xh, int64_t ncols, float * __restrict__ dst,
+                                                   size_t ycol) {
+    __shared__ __attribute__((aligned(16))) float red[4][16][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t nrt = (N + 31) / 32;
+    const int64_t n0 = ((int64_t) blockIdx.x % nrt) * 32, c0 = ((int64_t) blockIdx.x / nrt) * 32;
+    const int64_t kw = K / 4;                 // this wave's K range (K % 256 == 0)
+    const int nch = (int) (kw / 64);           // 64-deep chunks
+    const uint8_t * wp = W + std::min<int64_t>(n0 + r, N - 1) * nb01 + (size_t) (w * kw + 32 * h) * 2;
+    const uint8_t * xp = (const uint8_t *) xh + (size_t) std::min<int64_t>(c0 + r, ncols - 1) * (size_t) K * 2 + (size_t) (w * kw + 32 * h) * 2;
+    struct Chunk {
+        uint4 a[4], b[4];
+    };
+    auto load = [&](Chunk & c, int i) {
+        i = i < nch ? i : nch - 1;  // past the end: a harmless re-read of the last chunk
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            c.a[q] = *(const uint4 *) (wp + (size_t) i * 128 + 16 * q);
+            c.b[q] = *(const uint4 *) (xp + (size_t) i * 128 + 16 * q);
+        }
+    };
+    Chunk ring[PF];
+#pragma unroll
+    for (int u = 0; u < PF; u++) load(ring[u], u);
+    float16v acc = {};
+    for (int i0 = 0; i0 < nch; i0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            if (i0 + u >= nch) break;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ring[u].a[q]), __builtin_bit_cast(half8, ring[u].b[q]), acc, 0, 0, 0);
+            load(ring[u], i0 + u + PF);
+        }
+    }
+#pragma unroll
+    for (int el = 0; el < 16; el++) red[w][el][lane] = acc[el];
+    __syncthreads();
+    // wave w stores accumulator elements 4w .. 4w + 3 (rows n0 + 8 w + 4 (l / 32) + e) of column c0 + l % 32
+    const int64_t b = c0 + r;
+    const int64_t n = n0 + 8 * w + 4 * h;
+    float y[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const int el = 4 * w + e;
+        y[e] = red[0][el][lane] + red[1][el][lane];
+        y[e] = y[e] + red[2][el][lane];
+        y[e] = y[e] + red[3][el][lane];
+    }
+    if (b >= ncols) return;
+    float * out = (float *) ((char *) dst + b * ycol);
+    if (n + 3 < N) {
+        *(float4 *) (out + n) = make_float4(y[0], y[1], y[2], y[3]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[e];
+    }
+}
+
 } // namespace
+
+bool mi_mmf16p_supported(int64_t K, int64_t N, size_t nb01, int64_t ncols, size_t ycol) {
+    return (g_mi_tuning.mmq_variant & ((1 << 18) | 1)) == 0 && ncols > 8 && ncols <= 128 && K % 256 == 0 && N >= 1 &&
+           nb01 % 16 == 0 && ycol % 16 == 0;
+}
+
+void mi_mul_mat_f16p(const void * W, size_t nb01, int64_t K, int64_t N, const uint16_t * xh, int64_t ncols, float * dst, size_t ycol,
+                     hipStream_t s) {
+    const int64_t tiles = ((N + 31) / 32) * ((ncols + 31) / 32);
+    hipLaunchKernelGGL((k_mmf16p<3>), dim3((unsigned) tiles), dim3(256), 0, s, (const uint8_t *) W, nb01, K, N, xh, ncols, dst, ycol);
+}
 
 bool mi_mmq_wants_blocked() { return (g_mi_tuning.mmq_variant & 1) == 0; }
 

@@ -890,7 +890,11 @@ __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
 // dequantized weight planes (accumulator column = the lane's own weight row r).
 // NW = 4: two workgroups per CU (<= 256 VGPRs at two waves per SIMD), each wave computing groups
 // w and w + 4 one after the other (each group's sum goes to LDS when it ends).
-template <int TYPE, int NC, int NW, int ABL = 0>
+// RING: weight register buffers; superblock k + RING - 1's weights are requested when step k starts.
+// r03v counters (RING 2, B = 32, 16 members): waves wait ~45 % of their cycles (SQ_WAIT_INST_ANY),
+// MFMA 9 % busy, 18 VALU per MFMA. RING 4 measured slower (r03w): the activation fragments of step
+// k + 1 are requested after those weights, and vmcnt retires in order.
+template <int TYPE, int NC, int NW, int ABL = 0, int RING = 4>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -966,12 +970,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
 #pragma unroll
     for (int t = 0; t < NC; t++) gsum[t] = f32x16{};
     if (nsb > 0) {
-        Wt wt[2];
+        Wt wt[RING];
         i32x4 xa[NC][8];
         half8 xu[NC];
         float da[NC];
         const int sbf = sb_at(0);
-        load_w(wt[0], sbf);
+#pragma unroll
+        for (int u = 0; u < RING - 1; u++) load_w(wt[u], sb_at(u));
 #pragma unroll
         for (int t = 0; t < NC; t++) {
 #pragma unroll
@@ -979,13 +984,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
             xu[t] = ld_u(sbf, t);
             da[t] = ld_d(sbf, t);
         }
-        // the wave's k-th superblock: `cur` holds its weights; the next one's loads are issued as
-        // the registers free up (weights into `nxt` first, activations step by step)
+        // the wave's k-th superblock: `cur` holds its weights; superblock k + RING - 1's weights go
+        // into `nxt` (the buffer the previous step consumed), the next superblock's activations are
+        // requested step by step as their registers free up
         auto step = [&](const Wt & cur, Wt & nxt, const int k) {
             const int sb = sb_at(k);
             const int sn = sb_at(k + 1);  // clamped: a past-the-end prefetch re-reads the last one
             const bool first = sb % gs == 0, last = sb % gs == gs - 1 || sb == S - 1;
-            load_w(nxt, sn);
+            load_w(nxt, sb_at(k + RING - 1));
             const uint32_t w0 = cur.hdr.y, w1 = cur.hdr.z, w2 = cur.hdr.w;
             // the 6-bit scales of sub-blocks 0..3 / 4..7 as bytes (get_scale_min_k4)
             const uint32_t sca = w0 & 0x3F3F3F3Fu;
@@ -1081,10 +1087,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
             __builtin_amdgcn_wave_barrier();  // the LDS row is rewritten by the next superblock
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
         };
-        for (int k = 0; k < nsb; k += 2) {
-            step(wt[0], wt[1], k);
-            if (k + 1 >= nsb) break;
-            step(wt[1], wt[0], k + 1);
+        for (int k = 0; k < nsb; k += RING) {
+#pragma unroll
+            for (int u = 0; u < RING; u++) {
+                if (k + u >= nsb) break;
+                step(wt[u], wt[(u + RING - 1) % RING], k + u);
+            }
         }
     }
     mi_lds_barrier();
@@ -1129,7 +1137,7 @@ struct Q0Raw {
     float da[8];  // this lane's column's activation scales of the unit's 8 blocks
 };
 
-template <bool Q8>
+template <bool Q8, int RING = 2>
 __global__ __launch_bounds__(256, 2) void k_mmq0p(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     constexpr int NW = 4;
@@ -1227,10 +1235,11 @@ __global__ __launch_bounds__(256, 2) void k_mmq0p(mi_mmx_group grp) {
 
     f32x16 gsum = {};
     if (nsb > 0) {
-        Q0Raw<Q8> ru[2];
+        Q0Raw<Q8> ru[RING];  // unit k + RING - 1's weights are requested when unit k starts (k_mmqp)
         i32x4 xa[8];
         const int uf = sb_at(0);
-        load_unit(ru[0], uf);
+#pragma unroll
+        for (int v = 0; v < RING - 1; v++) load_unit(ru[v], sb_at(v));
 #pragma unroll
         for (int j = 0; j < 8; j++) xa[j] = ld_x(uf, j);
         auto unit = [&](const Q0Raw<Q8> & cur, Q0Raw<Q8> & nxt, const int k) {
@@ -1238,7 +1247,7 @@ __global__ __launch_bounds__(256, 2) void k_mmq0p(mi_mmx_group grp) {
             const int un = sb_at(k + 1);  // clamped: a past-the-end prefetch re-reads the last one
             const bool last = u % gs == gs - 1 || u == S - 1;
             if (u % gs == 0) gsum = f32x16{};
-            load_unit(nxt, un);
+            load_unit(nxt, sb_at(k + RING - 1));
             if (h == 0) {
 #pragma unroll
                 for (int j = 0; j < 8; j++) dal[w][j][r] = cur.da[j];
@@ -1272,10 +1281,12 @@ __global__ __launch_bounds__(256, 2) void k_mmq0p(mi_mmx_group grp) {
                 for (int el = 0; el < 16; el++) red[(gi * 16 + el) * 64 + lane] = gsum[el];
             }
         };
-        for (int k = 0; k < nsb; k += 2) {
-            unit(ru[0], ru[1], k);
-            if (k + 1 >= nsb) break;
-            unit(ru[1], ru[0], k + 1);
+        for (int k = 0; k < nsb; k += RING) {
+#pragma unroll
+            for (int v = 0; v < RING; v++) {
+                if (k + v >= nsb) break;
+                unit(ru[v], ru[(v + RING - 1) % RING], k + v);
+            }
         }
     }
     mi_lds_barrier();
@@ -1830,7 +1841,7 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         }
         const bool q8 = type == 8;
         switch (pick) {
-            case 0: {
+            case 0: {  // (a deeper weight ring, RING 3, spills: 36-dword units)
                 const dim3 grid((unsigned) mmx_deal(g, 32, 32));
                 if (!q8) hipLaunchKernelGGL((k_mmq0p<false>), grid, dim3(256), 0, s, g);
                 else hipLaunchKernelGGL((k_mmq0p<true>), grid, dim3(256), 0, s, g);
@@ -1907,16 +1918,22 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         const int64_t t64 = mmx_deal(g, 32, 64);
         const int nc = (var & (1 << 26)) ? 2 : 1;  // 64-column tiles spill at present: opt-in only
         const dim3 gridp((unsigned) (nc == 2 ? t64 : mmx_deal(g, 32, 32)));
-        // 4 waves per tile (two workgroups per CU) unless variant bit 2^27 (8 waves, one per CU)
+        // 4 waves per tile (two workgroups per CU) unless variant bit 2^27 (8 waves, one per CU);
+        // weight ring of 2 (variant bit 2^19: 4 -- slower, profiles/r03w_mmqp_ring.txt: vmcnt retires
+        // in issue order, so a step waiting for its activations also waits for every weight request
+        // issued before them; a deeper weight lead alone only adds outstanding loads)
         const bool w8 = (var & (1 << 27)) != 0;
-#define MI_MMQP(TY, NCC, NWW) hipLaunchKernelGGL((k_mmqp<TY, NCC, NWW>), gridp, dim3(64 * NWW), 0, s, g)
+        const bool r2 = (var & (1 << 19)) == 0;
+#define MI_MMQP(TY, NCC, NWW, RG) hipLaunchKernelGGL((k_mmqp<TY, NCC, NWW, 0, RG>), gridp, dim3(64 * NWW), 0, s, g)
+#define MI_MMQP1(TY, NWW) do { if (r2) MI_MMQP(TY, 1, NWW, 2); else MI_MMQP(TY, 1, NWW, 4); } while (0)
         if (type == 12) {
-            if (nc == 2) { if (w8) MI_MMQP(12, 2, 8); else MI_MMQP(12, 2, 4); }
-            else { if (w8) MI_MMQP(12, 1, 8); else MI_MMQP(12, 1, 4); }
+            if (nc == 2) { if (w8) MI_MMQP(12, 2, 8, 2); else MI_MMQP(12, 2, 4, 2); }
+            else { if (w8) MI_MMQP1(12, 8); else MI_MMQP1(12, 4); }
         } else {
-            if (nc == 2) { if (w8) MI_MMQP(13, 2, 8); else MI_MMQP(13, 2, 4); }
-            else { if (w8) MI_MMQP(13, 1, 8); else MI_MMQP(13, 1, 4); }
+            if (nc == 2) { if (w8) MI_MMQP(13, 2, 8, 2); else MI_MMQP(13, 2, 4, 2); }
+            else { if (w8) MI_MMQP1(13, 8); else MI_MMQP1(13, 4); }
         }
+#undef MI_MMQP1
 #undef MI_MMQP
         return;
     }

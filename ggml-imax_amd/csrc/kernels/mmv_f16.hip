@@ -371,6 +371,10 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
             if (EPI >= 1) v = v + eb;
             if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
             dst[row] = v;
+            // a CPY of the output rows (e.g. the logits into the caller's pinned host buffer: the
+            // stores go out over PCIe while the GEMV runs, instead of a copy queued behind it)
+            if (e.copy[0].ptr && row >= e.copy[0].row0 && row < e.copy[0].row1)
+                *(float *) (e.copy[0].ptr + (row - e.copy[0].row0) * sizeof(float)) = v;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) cur[u] = nxt[u];
@@ -551,7 +555,7 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
     ks = (nit + per - 1) / per;
     const bool one = per <= 8;
     const int rgs = g_mi_tuning.f16_rgs > 0 ? std::max(1, std::min(g_mi_tuning.f16_rgs, 8 / ks)) : 1;
-    if (ncols == 1 && groups >= 4096 && K <= 1024 && !xh && !e.resid && !e.copy[0].ptr && g_mi_tuning.f16_rgs == 0 && !pro.parts) {
+    if (ncols == 1 && groups >= 4096 && K <= 1024 && !xh && !e.resid && !e.copy[1].ptr && g_mi_tuning.f16_rgs == 0 && !pro.parts) {
         // tall matrix: grid-stride row groups (k_gemv_f16_tall)
         const dim3 grid((unsigned) std::min<int64_t>((groups + 3) / 4, 512));
         const size_t lds = (size_t) kp * sizeof(uint16_t);
