@@ -427,6 +427,7 @@ struct mi_backend_ctx {
     int last_launches = 0;
     uint16_t * tables = nullptr;  // device: exp, gelu, silu fp16 tables (3 x 65536)
     hipEvent_t split_ready = nullptr;  // src1 of a split mul_mat is ready on `stream`
+    hipEvent_t plan_marker = nullptr;  // recorded behind each plan launch (mi_graph_plan_compute)
     uint64_t scratch_gen = 0;     // bumped whenever `scratch` is reallocated (captures refer to it)
     // hipGraph plans (mi_graph_plan_create): captured launches of a whole ggml graph
     bool graphs = true;
@@ -2250,6 +2251,15 @@ static enum ggml_status mi_graph_plan_compute(ggml_backend_t backend, ggml_backe
         return mi_graph_launch_nodes(ctx, &plan->graph);
     }
     MI_CHECK(hipGraphLaunch(plan->exec, ctx->stream));
+    // GGML_MI355X_PLAN_FLUSH (A/B): 1 = a marker event behind the launch, 2 = hipStreamQuery, 0 (the
+    // default) = nothing; no variant was faster than the noise in the GPT-2 decode loop (r03y2)
+    static const int flush = getenv("GGML_MI355X_PLAN_FLUSH") ? atoi(getenv("GGML_MI355X_PLAN_FLUSH")) : 0;
+    if (flush == 1) {
+        if (!ctx->plan_marker) MI_CHECK(hipEventCreateWithFlags(&ctx->plan_marker, hipEventDisableTiming));
+        MI_CHECK(hipEventRecord(ctx->plan_marker, ctx->stream));
+    } else if (flush == 2) {
+        (void) hipStreamQuery(ctx->stream);
+    }
     ctx->last_launches = plan->launches;
     return GGML_STATUS_SUCCESS;
 }
@@ -2422,6 +2432,8 @@ static void mi_backend_free(ggml_backend_t backend) {
         if (ctx->scratch) MI_CHECK(hipFree(ctx->scratch));
         if (ctx->tables) MI_CHECK(hipFree(ctx->tables));
         for (auto & t : ctx->rope_tables) MI_CHECK(hipFree(t.dev));
+        if (ctx->plan_marker) MI_CHECK(hipEventDestroy(ctx->plan_marker));
+        if (ctx->split_ready) MI_CHECK(hipEventDestroy(ctx->split_ready));
         MI_CHECK(hipStreamDestroy(ctx->stream));
     }
     delete ctx;

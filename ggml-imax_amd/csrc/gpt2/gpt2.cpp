@@ -400,12 +400,6 @@ ggml_cgraph * build_graph(gpt2_model & m, int n_past, int N, int slot = 0) {
     ggml_set_name(inpL, "logits");
     ggml_set_output(inpL);
     ggml_build_forward_expand(gf, inpL);
-    if (m.logits_host && N == 1) {
-        // decode with pinned host staging: the graph itself copies the logits into it (a backend
-        // that fuses the CPY into the lm_head GEMV stores them over PCIe as they are produced),
-        // instead of a device-to-host copy queued behind the graph (gpt2_eval)
-        ggml_build_forward_expand(gf, ggml_cpy(ctx, inpL, ggml_view_1d(ctx, m.logits_host, hp.n_vocab, 0)));
-    }
     ggml_free(ctx);  // the context memory is graph_buf; the graph stays valid until the next build
     return gf;
 }
@@ -659,8 +653,9 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
     const size_t lg_off = all_logits ? 0 : sizeof(float) * nv * (N - 1), lg_size = sizeof(float) * nv * (all_logits ? N : 1);
     // logits staged through host memory by a copy queued right behind the graph
     const bool staged = m->host_io && lg_size <= ggml_nbytes(m->logits_host);
-    // (one-token graphs copy their logits into the staging themselves: build_graph)
-    if (staged && N != 1) ggml_backend_tensor_get_async(m->backend, out, m->logits_host->data, lg_off, lg_size);
+    // (measured against an in-graph CPY into the staging that the lm_head GEMV's epilogue stores
+    // over PCIe: slower, the host's next-graph preparation ran ~150 us longer per token, r03y2)
+    if (staged) ggml_backend_tensor_get_async(m->backend, out, m->logits_host->data, lg_off, lg_size);
     const int64_t t2b = now_us();
     // While the device runs this graph, build and allocate the next decode step's (one token at
     // n_past + N) in the other arena: the graph depends on positions only, not on the token the
