@@ -722,7 +722,6 @@ static int mm_act_kind(const mi_mm_desc & m, const ggml_tensor * src1) {
     // GGML_MI355X_MMQ_VARIANT bit 2^30 selects the f16 GEMM for the quantized types too (A/B
     // timing; the low bits are mmq_exact.hip's own kernel variants)
     if (kind <= 1 && (g_mi_tuning.mmq_variant & (1 << 30)) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01)) return kind == 1 ? 8 : 9;
-    if (kind == 2 && mi_mmf16p_supported(m.K, m.N, m.nb01, ncols, m.nb1)) return 2;  // k_mmf16p: plain f16 columns
     return (kind == 2 ? 2 : kind + 3) + (mi_mmq_wants_blocked() ? 3 : 0);
 }
 
@@ -767,7 +766,7 @@ static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const vo
             // Q4_K / Q5_K / Q4_0 / Q8_0: the exact-integer int8 MFMA GEMMs (mmq_exact.hip)
             const mi_act_mmx act = xkind == 8 ? mi_act_mmx_carve(xa, m.K, ncols) : mi_act_mmx0_carve(xa, m.K, ncols);
             mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, act, m.dst, m.nb1, ctx->stream);
-        } else if (xkind == 2 && mm_batched(m, src1) && mi_mmf16p_supported(m.K, m.N, m.nb01, ncols, m.nb1)) {
+        } else if (xkind == 5 && m.type == GGML_TYPE_F16 && mi_mmf16p_supported(m.K, m.N, m.nb01, ncols, m.nb1)) {
             // F16 weights, a short prompt: 32 x 32 tiles with the K split over each tile's 4 waves
             mi_mul_mat_f16p(m.W, m.nb01, m.K, m.N, (const uint16_t *) xa, ncols, m.dst, m.nb1, ctx->stream);
         } else if (xkind >= 3 || (xkind == 2 && mm_batched(m, src1))) {

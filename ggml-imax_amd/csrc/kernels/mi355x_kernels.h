@@ -134,8 +134,8 @@ void mi_mul_mat_q_fused(mi_mmv_group & g, hipStream_t s);
 // weights with xh == nullptr, the q8 blocks in act expanded into `scratch` first.
 // dst columns of ycol bytes. Requires K % 256 == 0.
 bool mi_mmq_supported(int type, int64_t K, size_t nb01, size_t ycol);
-// F16 weights, 9..128 columns (mmq.hip k_mmf16p): xh = f16 activations in the plain [ncols][K]
-// layout; K % 256 == 0, 16-byte aligned rows (mmq_variant bits 1 / 2^18 turn it off)
+// F16 weights, 9..128 columns (mmq.hip k_mmf16p): xh = f16 activations in the K-blocked layout
+// [K/16][ncols][16]; K % 256 == 0, 16-byte aligned rows (mmq_variant bits 1 / 2^18 turn it off)
 bool mi_mmf16p_supported(int64_t K, int64_t N, size_t nb01, int64_t ncols, size_t ycol);
 void mi_mul_mat_f16p(const void * W, size_t nb01, int64_t K, int64_t N, const uint16_t * xh, int64_t ncols, float * dst, size_t ycol,
                      hipStream_t s);

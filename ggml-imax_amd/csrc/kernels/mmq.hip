@@ -453,51 +453,72 @@ __global__ __launch_bounds__(256 * SK) void k_mmq3(const uint8_t * __restrict__ 
 // ---- F16 weights, short prompts (<= 128 columns): 32 x 32 tiles, K split over the 4 waves -------
 // k_mmq3's 64 x 128 tiles give N / 64 workgroups at B <= 128 (64 of the 256 CUs at N = 4096). Here
 // a workgroup computes 32 weight rows x 32 prompt columns and wave w the K range [w K/4, (w+1) K/4)
-// on v_mfma_f32_32x32x16_f16, operands straight from global memory into a register ring (no LDS
-// staging): per 64-deep chunk a lane loads 64 contiguous bytes of its weight row (row n0 + lane % 32,
-// halves k + 32 (lane / 32) ..) and the same 64 bytes of its activation column (plain f16 [ncols][K]
-// layout), and step s of the chunk takes their s-th 16 bytes -- a K permutation applied to both
-// operands alike (the MFMA sums the same products). The four partial tiles meet in LDS and are
-// added in wave order. Products of fp16 values are exact in f32; only the summation order differs
-// from the reference's ggml_vec_dot_f16 (~1e-7 relative).
+// on v_mfma_f32_32x32x16_f16, 64 K per chunk, a register ring PF chunks deep:
+//  * weights: coalesced loads (8 lanes per 128-byte row segment, 8 rows per instruction) into a
+//    wave-private LDS tile (row stride 144 B: the MFMA fragment reads of 16 rows hit 16 distinct
+//    bank quads), then one ds_read_b128 per lane and K step (row lane % 32, halves 8 (lane / 32));
+//    LDS operations of one wave execute in order, so one buffer suffices;
+//  * activations: the K-blocked f16 layout [K/16][ncols][16] -- a 16-deep step of 32 columns is 1 KB
+//    contiguous, one 16-byte load per lane.
+// (A first version loaded both operands row-per-lane straight from global memory: every lane
+// touched its own cache line, TCP_TOTAL_CACHE_ACCESSES = 64 per load instruction, 19.5 us at B = 64,
+// profiles/r03z_f16_pmc.txt.) The four partial tiles meet in LDS and are added in wave order.
+// Products of fp16 values are exact in f32; only the summation order differs from the reference's
+// ggml_vec_dot_f16 (~1e-7 relative).
 template <int PF>
 __global__ __launch_bounds__(256, 2) void k_mmf16p(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                                    const uint16_t * __restrict__ xh, int64_t ncols, float * __restrict__ dst,
                                                    size_t ycol) {
+    constexpr int kRow = 72;  // halves per LDS row (64 + 8 pad)
+    __shared__ __attribute__((aligned(16))) _Float16 lw[4][32 * kRow];
     __shared__ __attribute__((aligned(16))) float red[4][16][64];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
+    const int lr = lane >> 3, lp = lane & 7;  // weight staging: row lr + 8 q, 16-byte piece lp
     const int64_t nrt = (N + 31) / 32;
     const int64_t n0 = ((int64_t) blockIdx.x % nrt) * 32, c0 = ((int64_t) blockIdx.x / nrt) * 32;
-    const int64_t kw = K / 4;                 // this wave's K range (K % 256 == 0)
-    const int nch = (int) (kw / 64);           // 64-deep chunks
-    const uint8_t * wp = W + std::min<int64_t>(n0 + r, N - 1) * nb01 + (size_t) (w * kw + 32 * h) * 2;
-    const uint8_t * xp = (const uint8_t *) xh + (size_t) std::min<int64_t>(c0 + r, ncols - 1) * (size_t) K * 2 + (size_t) (w * kw + 32 * h) * 2;
+    const int64_t kw = K / 4;        // this wave's K range (K % 256 == 0)
+    const int nch = (int) (kw / 64);  // 64-deep chunks
+    const uint8_t * wq[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) wq[q] = W + std::min<int64_t>(n0 + lr + 8 * q, N - 1) * nb01 + (size_t) (w * kw) * 2 + 16 * lp;
+    const int64_t col = std::min<int64_t>(c0 + r, ncols - 1);
+    const uint16_t * xc = xh + ((size_t) (w * kw / 16) * ncols + col) * 16 + 8 * h;
+    const size_t xstep = (size_t) ncols * 16;  // halves per 16-deep K step
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // (a HIP uint4 array is not promoted to registers)
     struct Chunk {
-        uint4 a[4], b[4];
+        u32x4 wv[4];
+        u32x4 xv[4];
     };
     auto load = [&](Chunk & c, int i) {
         i = i < nch ? i : nch - 1;  // past the end: a harmless re-read of the last chunk
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            c.a[q] = *(const uint4 *) (wp + (size_t) i * 128 + 16 * q);
-            c.b[q] = *(const uint4 *) (xp + (size_t) i * 128 + 16 * q);
-        }
+        for (int q = 0; q < 4; q++) c.wv[q] = *(const u32x4 *) (wq[q] + (size_t) i * 128);
+#pragma unroll
+        for (int st = 0; st < 4; st++) c.xv[st] = *(const u32x4 *) (xc + ((size_t) i * 4 + st) * xstep);
     };
+    _Float16 * tile = lw[w];
     Chunk ring[PF];
 #pragma unroll
     for (int u = 0; u < PF; u++) load(ring[u], u);
     float16v acc = {};
-    for (int i0 = 0; i0 < nch; i0 += PF) {
+    auto step = [&](Chunk & c, int i) {
+        if (i >= nch) return;  // uniform
 #pragma unroll
-        for (int u = 0; u < PF; u++) {
-            if (i0 + u >= nch) break;
+        for (int q = 0; q < 4; q++) *(u32x4 *) (tile + (lr + 8 * q) * kRow + 8 * lp) = c.wv[q];
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ring[u].a[q]), __builtin_bit_cast(half8, ring[u].b[q]), acc, 0, 0, 0);
-            load(ring[u], i0 + u + PF);
+        for (int st = 0; st < 4; st++) {
+            const half8 a = *(const half8 *) (tile + r * kRow + 16 * st + 8 * h);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, __builtin_bit_cast(half8, c.xv[st]), acc, 0, 0, 0);
         }
+        load(c, i + PF);
+    };
+    static_assert(PF == 2 || PF == 3, "the ring below is written out for 2 or 3 chunks");
+    for (int i0 = 0; i0 < nch; i0 += PF) {  // ring slots named statically (no private-array indexing)
+        step(ring[0], i0);
+        step(ring[1], i0 + 1);
+        if constexpr (PF == 3) step(ring[PF - 1], i0 + 2);
     }
 #pragma unroll
     for (int el = 0; el < 16; el++) red[w][el][lane] = acc[el];
@@ -526,7 +547,7 @@ __global__ __launch_bounds__(256, 2) void k_mmf16p(const uint8_t * __restrict__ 
 } // namespace
 
 bool mi_mmf16p_supported(int64_t K, int64_t N, size_t nb01, int64_t ncols, size_t ycol) {
-    return (g_mi_tuning.mmq_variant & ((1 << 18) | 1)) == 0 && ncols > 8 && ncols <= 128 && K % 256 == 0 && N >= 1 &&
+    return mi_mmq_wants_blocked() && (g_mi_tuning.mmq_variant & (1 << 18)) == 0 && ncols > 8 && ncols <= 128 && K % 256 == 0 && N >= 1 &&
            nb01 % 16 == 0 && ycol % 16 == 0;
 }
 

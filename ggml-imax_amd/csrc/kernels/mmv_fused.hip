@@ -658,7 +658,9 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
 #pragma unroll
         for (int u = 0; u < NB; u++) {
             const int k = k0 + u;
-            if (k >= nrows) break;  // wave-uniform
+            // wave-uniform; `continue`, not `break`: with an early exit the ORD instances were not
+            // unrolled and their ring went to scratch memory
+            if (k >= nrows) continue;
             prefetch(ring[(u + PD) % NB], k + PD < klast ? k + PD : klast);
             const int row = row_begin + 4 * k + wave;
             if constexpr (ORD) {
