@@ -658,9 +658,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
 #pragma unroll
         for (int u = 0; u < NB; u++) {
             const int k = k0 + u;
-            // wave-uniform; `continue`, not `break`: with an early exit the ORD instances were not
-            // unrolled and their ring went to scratch memory
-            if (k >= nrows) continue;
+            if (k >= nrows) break;  // wave-uniform
             prefetch(ring[(u + PD) % NB], k + PD < klast ? k + PD : klast);
             const int row = row_begin + 4 * k + wave;
             if constexpr (ORD) {
