@@ -465,20 +465,20 @@ __global__ __launch_bounds__(256 * SK) void k_mmq3(const uint8_t * __restrict__ 
 // profiles/r03z_f16_pmc.txt.) The four partial tiles meet in LDS and are added in wave order.
 // Products of fp16 values are exact in f32; only the summation order differs from the reference's
 // ggml_vec_dot_f16 (~1e-7 relative).
-template <int PF>
-__global__ __launch_bounds__(256, 2) void k_mmf16p(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+template <int PF, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmf16p(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                                    const uint16_t * __restrict__ xh, int64_t ncols, float * __restrict__ dst,
                                                    size_t ycol) {
     constexpr int kRow = 72;  // halves per LDS row (64 + 8 pad)
-    __shared__ __attribute__((aligned(16))) _Float16 lw[4][32 * kRow];
-    __shared__ __attribute__((aligned(16))) float red[4][16][64];
+    __shared__ __attribute__((aligned(16))) _Float16 lw[NW][32 * kRow];
+    __shared__ __attribute__((aligned(16))) float red[NW][16][64];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
     const int lr = lane >> 3, lp = lane & 7;  // weight staging: row lr + 8 q, 16-byte piece lp
     const int64_t nrt = (N + 31) / 32;
     const int64_t n0 = ((int64_t) blockIdx.x % nrt) * 32, c0 = ((int64_t) blockIdx.x / nrt) * 32;
-    const int64_t kw = K / 4;        // this wave's K range (K % 256 == 0)
+    const int64_t kw = K / NW;       // this wave's K range (K % (64 NW) == 0)
     const int nch = (int) (kw / 64);  // 64-deep chunks
     const uint8_t * wq[4];
 #pragma unroll
@@ -523,7 +523,9 @@ __global__ __launch_bounds__(256, 2) void k_mmf16p(const uint8_t * __restrict__ 
 #pragma unroll
     for (int el = 0; el < 16; el++) red[w][el][lane] = acc[el];
     __syncthreads();
-    // wave w stores accumulator elements 4w .. 4w + 3 (rows n0 + 8 w + 4 (l / 32) + e) of column c0 + l % 32
+    // wave w < 4 stores accumulator elements 4w .. 4w + 3 (rows n0 + 8 w + 4 (l / 32) + e) of column
+    // c0 + l % 32, the NW partial tiles added in wave order
+    if (w >= 4) return;
     const int64_t b = c0 + r;
     const int64_t n = n0 + 8 * w + 4 * h;
     float y[4];
@@ -531,8 +533,8 @@ __global__ __launch_bounds__(256, 2) void k_mmf16p(const uint8_t * __restrict__ 
     for (int e = 0; e < 4; e++) {
         const int el = 4 * w + e;
         y[e] = red[0][el][lane] + red[1][el][lane];
-        y[e] = y[e] + red[2][el][lane];
-        y[e] = y[e] + red[3][el][lane];
+#pragma unroll
+        for (int v = 2; v < NW; v++) y[e] = y[e] + red[v][el][lane];
     }
     if (b >= ncols) return;
     float * out = (float *) ((char *) dst + b * ycol);
@@ -554,7 +556,11 @@ bool mi_mmf16p_supported(int64_t K, int64_t N, size_t nb01, int64_t ncols, size_
 void mi_mul_mat_f16p(const void * W, size_t nb01, int64_t K, int64_t N, const uint16_t * xh, int64_t ncols, float * dst, size_t ycol,
                      hipStream_t s) {
     const int64_t tiles = ((N + 31) / 32) * ((ncols + 31) / 32);
-    hipLaunchKernelGGL((k_mmf16p<3>), dim3((unsigned) tiles), dim3(256), 0, s, (const uint8_t *) W, nb01, K, N, xh, ncols, dst, ycol);
+    // variant bit 2^20: 8 waves per tile (K in eighths: twice the loads in flight per CU when the
+    // tiles do not fill the chip twice over); K % 512 == 0
+    const bool w8 = K % 512 == 0 && tiles < 512 && (g_mi_tuning.mmq_variant & (1 << 20)) != 0;
+    if (w8) hipLaunchKernelGGL((k_mmf16p<3, 8>), dim3((unsigned) tiles), dim3(512), 0, s, (const uint8_t *) W, nb01, K, N, xh, ncols, dst, ycol);
+    else hipLaunchKernelGGL((k_mmf16p<3, 4>), dim3((unsigned) tiles), dim3(256), 0, s, (const uint8_t *) W, nb01, K, N, xh, ncols, dst, ycol);
 }
 
 bool mi_mmq_wants_blocked() { return (g_mi_tuning.mmq_variant & 1) == 0; }
