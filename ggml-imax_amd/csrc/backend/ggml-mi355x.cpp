@@ -447,6 +447,7 @@ struct mi_backend_ctx {
         hipEvent_t done = nullptr;  // recorded behind every launch of `exec`
         uint64_t last_use = 0;
         int launches = 0;
+        bool no_update = false;  // hipGraphExecUpdate refused once: replay-only
     };
     std::vector<gcache_entry> gcache;
     uint64_t gclock = 0;
@@ -532,7 +533,8 @@ static bool mi_supports_op(ggml_backend_t, const ggml_tensor * op) {
             // src1 F32, or src1 already of the weight's vec_dot_type, which the reference CPU reads as
             // it lies (ggml.c:11952; F16 x F16, Q4_K/Q5_K x Q8_K, Q4_0/Q8_0 x Q8_0): the quantized
             // ones with whole superblocks, on the device's own weights
-            if (b->type == GGML_TYPE_F32 || (b->type == GGML_TYPE_F16 && a->type == GGML_TYPE_F16)) return true;
+            // (the split-buffer path converts an F32 src1 on the main device: F16 src1 only unsplit)
+            if (b->type == GGML_TYPE_F32 || (b->type == GGML_TYPE_F16 && a->type == GGML_TYPE_F16 && !is_split_tensor(a))) return true;
             return b->type == q8_src1_type(a->type) && a->ne[0] % 256 == 0 && !is_split_tensor(a);
         }
         case GGML_OP_ADD:
@@ -2028,8 +2030,9 @@ static hipGraph_t capture_pass(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
     return graph;
 }
 
-// The exact launch-relevant content of a graph: per node its output address, op, type, shape,
-// strides, op_params, view source and every source's address, type, shape and strides; plus the
+// The exact launch-relevant content of a graph: per node its output address, op, type, flags,
+// shape, strides, op_params, view source and every source's address, type, flags, shape and
+// strides; plus the
 // scratch buffer the captured kernels use and the tuning knobs that choose kernels. Two graphs
 // with equal keys launch identical kernels with identical arguments.
 static void graph_key(const mi_backend_ctx * ctx, const ggml_cgraph * g, std::vector<uint64_t> & k) {
@@ -2046,7 +2049,8 @@ static void graph_key(const mi_backend_ctx * ctx, const ggml_cgraph * g, std::ve
     }
     auto tensor = [&](const ggml_tensor * t) {
         k.push_back((uint64_t) (uintptr_t) t->data);
-        k.push_back((uint64_t) t->type | ((uint64_t) t->op << 16));
+        // flags too: whether a node's value is stored or fused away depends on GGML_TENSOR_FLAG_OUTPUT
+        k.push_back((uint64_t) t->type | ((uint64_t) t->op << 16) | ((uint64_t) (uint32_t) t->flags << 32));
         for (int d = 0; d < 4; d++) k.push_back((uint64_t) t->ne[d]);
         for (int d = 0; d < 4; d++) k.push_back((uint64_t) t->nb[d]);
     };
@@ -2138,10 +2142,13 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
     }
     ctx->graph_stats[5]++;
     const int launches = ctx->last_launches;
+    // An executable graph of this topology that is not in flight is updated in place (never one
+    // still running). In a decode loop every step has a new key (the KV length moves) and the
+    // previous step's executable is usually still running: rather than wait for it, a second one
+    // per topology is instantiated, and the two then alternate. An entry whose update was refused
+    // (a changed kernel choice) is no longer tried for updates; it still replays its own key.
     mi_backend_ctx::gcache_entry * slot = nullptr;
-    for (auto & e : ctx->gcache) {
-        if (e.topo != topo) continue;
-        MI_CHECK(hipEventSynchronize(e.done));  // never update an executable graph still in flight
+    auto try_update = [&](mi_backend_ctx::gcache_entry & e) {
         hipGraphNode_t err_node = nullptr;
         hipGraphExecUpdateResult res;
         if (hipGraphExecUpdate(e.exec, graph, &err_node, &res) == hipSuccess && res == hipGraphExecUpdateSuccess) {
@@ -2149,8 +2156,27 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
             slot = &e;
         } else {
             (void) hipGetLastError();
+            e.no_update = true;
         }
+    };
+    int same_topo = 0;
+    mi_backend_ctx::gcache_entry * busy = nullptr;
+    for (auto & e : ctx->gcache) {
+        if (e.topo != topo || e.no_update) continue;
+        same_topo++;
+        const hipError_t q = hipEventQuery(e.done);
+        if (q == hipErrorNotReady) {
+            (void) hipGetLastError();
+            if (!busy || e.last_use < busy->last_use) busy = &e;
+            continue;
+        }
+        MI_CHECK(q);
+        try_update(e);
         break;
+    }
+    if (!slot && busy && same_topo >= 2) {
+        MI_CHECK(hipEventSynchronize(busy->done));
+        try_update(*busy);
     }
     if (!slot) {
         if (ctx->gcache.size() >= kGraphCacheEntries) {
@@ -2269,6 +2295,18 @@ static enum ggml_status mi_graph_plan_compute(ggml_backend_t backend, ggml_backe
 // (tests/test_gpt2.py::test_reference_quantized_gpt2_is_ulp_sensitive): such graphs run every decode
 // reduction in the reference CPU's order (bit-identical). Any other graph (F16 models, a mul_mat of
 // input data) keeps the tree order, within 1e-5 of the reference per op.
+// A split input of the reference scheduler is a NONE tensor holding a value another split computed:
+// ggml_backend_sched_split_graph creates it with ggml_dup_tensor_layout and names it
+// "<backend>#<source name>#<copy>" (ggml-backend.c:1498-1523), so it counts as computed here.
+static bool sched_split_copy(const ggml_tensor * t) {
+    const char * a = strchr(t->name, '#');
+    if (!a || a == t->name) return false;
+    const char * b = strrchr(t->name, '#');
+    if (b == a || b[1] == '\0') return false;
+    for (const char * c = b + 1; *c; c++) if (*c < '0' || *c > '9') return false;
+    return true;
+}
+
 static int graph_decode_order(const ggml_cgraph * g) {
     for (int i = 0; i < g->n_nodes; i++) {
         const ggml_tensor * n = g->nodes[i];
@@ -2278,7 +2316,7 @@ static int graph_decode_order(const ggml_cgraph * g) {
                x->op == GGML_OP_TRANSPOSE) {
             x = x->view_src ? x->view_src : x->src[0];
         }
-        if (x->op != GGML_OP_NONE) return 1;
+        if (x->op != GGML_OP_NONE || sched_split_copy(x)) return 1;
     }
     return 0;
 }
@@ -2696,6 +2734,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "mmq_variant") == 0) {
         g_mi_tuning.mmq_variant = value;
+        return true;
+    }
+    if (strcmp(name, "mmq_long") == 0 && value >= 0 && value <= 2) {
+        g_mi_tuning.mmq_long = value;
         return true;
     }
     if (strcmp(name, "mmv_order") == 0 && value >= -1 && value <= 1) {

@@ -646,6 +646,7 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
     const ggml_status st = plan ? ggml_backend_graph_plan_compute(m->backend, plan) : ggml_backend_graph_compute_async(m->backend, gf);
     if (st != GGML_STATUS_SUCCESS) {
         fprintf(stderr, "gpt2_eval: graph compute failed\n");
+        if (plan) ggml_backend_graph_plan_free(m->backend, plan);
         return 1;
     }
     ggml_tensor * out = ggml_graph_get_tensor(gf, "logits");
@@ -680,6 +681,7 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
     } else {
         if (!logits) {
             fprintf(stderr, "gpt2_eval: logits == NULL needs the host staging of gpt2_model_load_ex\n");
+            if (plan) ggml_backend_graph_plan_free(m->backend, plan);
             return 1;
         }
         ggml_backend_tensor_get(out, logits, lg_off, lg_size);

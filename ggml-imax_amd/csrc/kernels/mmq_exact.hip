@@ -1112,6 +1112,204 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
     }
 }
 
+// ---- long prompts, weights dequantized in registers: k_mmqr ------------------------------------------
+// Why (k_mmqw's stage stamps, profiles/r03t_mmqw_stage_stamps.txt): with the weight planes staged
+// through LDS by loader waves, every MFMA wave runs [16 MFMAs | combine | barrier] in lock step with
+// the others, so the matrix pipe idles through the combine and the barrier (~60 % of a stage).
+// Here there is no workgroup barrier at all: each wave dequantizes its own 32 weight rows into the
+// MFMA operand registers (k_mmqp's step: the lane's own weight row is the B operand, plane factors
+// from two SWAR extractions of the scale bytes) and runs every superblock of K itself, so a wave's
+// instruction stream interleaves dequantization VALU, MFMAs and the previous superblock's combine,
+// and the two waves of a SIMD fill each other's gaps (MFMA and VALU are separate pipes).
+// Workgroup: 8 waves, tile 128 weight rows x 64 prompt columns; wave w computes rows 32 (w & 3)..
+// x columns 32 (w >> 2).. (one 32 x 32 accumulator per plane). Row tiles fastest in the grid, so
+// blocks b and b + 8 (one XCD under round-robin placement) share column tiles and an XCD's L2 holds
+// the weights of only nrt / 8 row tiles. Same operands and canonical combine (mmqx_term, cfold_vec
+// in superblock order) as every kernel of this file: bit-identical.
+// Loads (vmcnt retires in issue order, so waiting for one load waits for every older one): the
+// activation fragments of superblock s are requested XL superblocks ahead, step by step into the
+// registers their predecessors just freed; superblock s + RING's weights are requested at the END of
+// superblock s (RING = XL + 1 slots), i.e. after the activations it must not hold back. A wait for
+// the activations of s then forces only weights requested XL superblocks earlier: both operands get
+// XL superblocks of latency cover (XL = 1 measured latency-bound: 42.9 us at B = 512).
+template <int TYPE, int XL, int SCT = 0>
+__global__ __launch_bounds__(512, 2) void k_mmqr(mi_mmx_group grp) {
+    MI_MMX_MEMBER(grp);
+    using F = XFmt<TYPE>;
+    constexpr int NP = F::NP;
+    constexpr int RING = XL + 1;
+    __shared__ __attribute__((aligned(16))) float dal[8][32];  // per-wave da row
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t ncols = act.ncols;
+    const int S = (int) (K / 256);
+    const int gs = cfold_gs(S);
+    const int64_t nrt = (N + 127) / 128;
+    const int64_t n0 = (mmx_tile % nrt) * 128 + 32 * (w & 3);
+    const int64_t c0 = (mmx_tile / nrt) * 64 + 32 * (w >> 2);
+    if (n0 >= N || c0 >= ncols) return;  // wave-uniform; no workgroup barrier below
+
+    const int nrows = (int) std::min<int64_t>(32, N - n0);
+    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
+    constexpr uint32_t kQs = F::Q5 ? 48 : 16;
+    const uint32_t wv = (uint32_t) (min(r, nrows - 1) * nb01);
+    const uint32_t acol = (uint32_t) std::min<int64_t>(c0 + r, ncols - 1);
+    const uint32_t xstep = (uint32_t) ncols * 32;
+
+    auto ld = [](__amdgpu_buffer_rsrc_t res, uint32_t voff, uint32_t soff) -> uint4 {
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(res, voff, soff, 0));
+    };
+    struct Wt {
+        uint4 hdr, q4[4], qh;
+    };
+    auto load_w = [&](Wt & o, int sb) {
+        sb = min(sb, S - 1);  // clamped: past-the-end requests re-read the last superblock
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * F::BS);
+        o.hdr = ld(wres, wv, so);
+#pragma unroll
+        for (int p = 0; p < 4; p++) o.q4[p] = ld(wres, wv + kQs + 32 * p + 16 * h, so);
+        if constexpr (F::Q5) o.qh = ld(wres, wv + 16 + 16 * h, so);
+    };
+    auto ld_x = [&](int sb, int kk) -> i32x4 {
+        sb = min(sb, S - 1);
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((sb * 8 + kk) * (int) xstep);
+        return __builtin_bit_cast(i32x4, ld(xres, acol * 32 + 16 * h, so));
+    };
+    auto ld_u = [&](int sb) -> half8 {
+        sb = min(sb, S - 1);
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * (int) ncols * 32);
+        return __builtin_bit_cast(half8, ld(ures, acol * 32 + 16 * h, so));
+    };
+    auto ld_d = [&](int sb) -> float {
+        sb = min(sb, S - 1);
+        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * (int) ncols * 4);
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, acol * 4, so, 0));
+    };
+
+    f32x16 y = f32x16(-0.0f), gsum = {};
+    Wt wt[RING];
+    i32x4 xa[XL][8];
+    half8 xu[XL];
+    float da[XL];
+#pragma unroll
+    for (int u = 0; u < XL; u++) {
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) xa[u][kk] = ld_x(u, kk);
+        xu[u] = ld_u(u);
+        da[u] = ld_d(u);
+    }
+#pragma unroll
+    for (int u = 0; u < RING; u++) load_w(wt[u], u);
+    // superblock sb from slots (sb % RING, sb % XL), then the slots' refills: sb + XL's activations,
+    // sb + RING's weights. The loop runs whole unrolled rounds (every slot index static); the steps
+    // past S compute nothing but still issue their (clamped) requests, so every path through the
+    // body issues the same loads and the compiler's vmcnt bookkeeping stays exact (a load under a
+    // branch makes it drain at the join).
+    auto step = [&](Wt & cur, i32x4 (&xs)[8], half8 & xuc, float & dac, const int sb) {
+        if (sb < S) {  // wave-uniform
+            const uint32_t w0 = cur.hdr.y, w1 = cur.hdr.z, w2 = cur.hdr.w;
+            const uint32_t sca = w0 & 0x3F3F3F3Fu;
+            const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
+            const float dw = mi_h2f((uint16_t) (cur.hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (cur.hdr.x >> 16));
+            const uint32_t ma = w1 & 0x3F3F3F3Fu;
+            const uint32_t mb = ((w2 >> 4) & 0x0F0F0F0Fu) | ((w1 >> 2) & 0x30303030u);
+            const uint32_t mw = h ? mb : ma;
+            i32x16 acc[NP];
+            uint32_t lo[4], hi[4];
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) {
+                if ((kk & 1) == 0) {
+                    const uint4 q = cur.q4[kk >> 1];
+                    const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        lo[e] = qv[e] & 0x0F0F0F0Fu;
+                        hi[e] = (qv[e] >> 4) & 0x0F0F0F0Fu;
+                    }
+                }
+                uint32_t v[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    v[e] = (kk & 1) ? hi[e] : lo[e];
+                    if constexpr (F::Q5) {
+                        const uint32_t hb[4] = {cur.qh.x, cur.qh.y, cur.qh.z, cur.qh.w};
+                        v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
+                    }
+                }
+                const uint32_t scw = kk < 4 ? sca : scb;
+#pragma unroll
+                for (int p = 0; p < NP; p++) {
+                    const uint32_t f = __builtin_amdgcn_ubfe(scw, 8 * (kk & 3) + (F::Q5 ? 2 * p : 3 * p), F::Q5 ? 2 : 3);
+                    const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+                    acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xs[kk], b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
+                }
+            }
+            // U on the f16 MFMA: A = [S & 63, S >> 6] of the lane's column, B = [m, 64 m] of its row
+            half8 mu;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t m = (mw >> (8 * q)) & 0xFF;
+                mu[2 * q] = (_Float16) (float) m;
+                mu[2 * q + 1] = (_Float16) (float) (64 * m);
+            }
+            if (h == 0) dal[w][r] = dac;
+            __builtin_amdgcn_wave_barrier();
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xuc, mu, f32x16{}, 0, 0, 0);
+            f32x16 tv;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; g4++) {
+                const float4 d4 = *(const float4 *) &dal[w][8 * g4 + 4 * h];
+                const float dav[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int el = 4 * g4 + e;
+                    int T = acc[NP - 1][el];
+#pragma unroll
+                    for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
+                    tv[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the LDS row is rewritten by the next superblock
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            cfold_vec(gsum, y, tv, sb, gs, S);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) xs[kk] = ld_x(sb + XL, kk);
+        xuc = ld_u(sb + XL);
+        dac = ld_d(sb + XL);
+        load_w(cur, sb + RING);  // after this superblock's activation requests (see above)
+    };
+    constexpr int UNR = XL * RING;  // every slot index static
+    if constexpr (SCT > 0) {
+        // S == SCT (host-checked): straight-line code, no loop-carried vmcnt bookkeeping (the
+        // compiler drains vmcnt at the loop header of the rolled form); the sched barriers keep
+        // each superblock's instructions (and registers) inside its own step
+#pragma unroll
+        for (int u = 0; u < SCT; u++) {
+            step(wt[u % RING], xa[u % XL], xu[u % XL], da[u % XL], u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        for (int sb0 = 0; sb0 < S; sb0 += UNR) {
+#pragma unroll
+            for (int u = 0; u < UNR; u++) step(wt[u % RING], xa[u % XL], xu[u % XL], da[u % XL], sb0 + u);
+        }
+    }
+    // accumulator element el: prompt column c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
+    const int64_t n = n0 + r;
+    if (n >= N) return;
+#pragma unroll
+    for (int el = 0; el < 16; el++) {
+        const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * h;
+        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y[el];
+    }
+}
+
 // ---- Q4_0 / Q8_0 prefill: the reference's exact int32 block sums on the int8 matrix cores --------
 // The reference dots (vec_dot_q4_0_q8_0, src/ggml-quants.c:3469-3874, AVX2 :3600-3623;
 // vec_dot_q8_0_q8_0, :4819, AVX2 :4925+) compute, per 32-block b, the exact int32
@@ -1946,6 +2144,17 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         const dim3 grid4((unsigned) mmx_deal(g, XBM, 64));
         if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, g);
         else hipLaunchKernelGGL((k_mmqx<13, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, g);
+        return;
+    }
+    if (g_mi_tuning.mmq_long == 2) {  // weights dequantized in registers, 128 x 64 tiles of 8 waves
+        const dim3 gridr((unsigned) mmx_deal(g, 128, 64));
+        if (K == 4096) {
+            if (type == 12) hipLaunchKernelGGL((k_mmqr<12, 2, 16>), gridr, dim3(512), 0, s, g);
+            else hipLaunchKernelGGL((k_mmqr<13, 1, 16>), gridr, dim3(512), 0, s, g);
+        } else {
+            if (type == 12) hipLaunchKernelGGL((k_mmqr<12, 2>), gridr, dim3(512), 0, s, g);
+            else hipLaunchKernelGGL((k_mmqr<13, 1>), gridr, dim3(512), 0, s, g);
+        }
         return;
     }
     const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));

@@ -459,15 +459,24 @@ template <int TA>
 static void launch_get_rows_add(const mi_tensor_desc & d, const mi_tensor_desc & a, const mi_tensor_desc & ia, const mi_tensor_desc & b,
                                 const mi_tensor_desc & ib, int64_t n, hipStream_t s) {
     (void) n;
-    if (d.ne[1] > 65535 || d.ne[0] >= ((int64_t) 1 << 31)) abort();
+    if (d.ne[0] >= ((int64_t) 1 << 31)) abort();  // row length indexed with 32 bits (never an embedding)
     const int ne0 = (int) d.ne[0];
-    const dim3 g((unsigned) std::min<int64_t>((ne0 + 1023) / 1024, 64), (unsigned) d.ne[1]);
-    switch (b.type) {
-        case 2: hipLaunchKernelGGL((k_get_rows_add<TA, 2>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
-        case 8: hipLaunchKernelGGL((k_get_rows_add<TA, 8>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
-        case 12: hipLaunchKernelGGL((k_get_rows_add<TA, 12>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
-        case 13: hipLaunchKernelGGL((k_get_rows_add<TA, 13>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
-        default: hipLaunchKernelGGL((k_get_rows_add<TA, 0>), g, dim3(256), 0, s, d, a, ia, b, ib, ne0); break;
+    // grid.y is at most 65535 rows: longer index vectors in chunks (descriptors advanced by rows)
+    for (int64_t r0 = 0; r0 < d.ne[1]; r0 += 65535) {
+        const int64_t nr = std::min<int64_t>(65535, d.ne[1] - r0);
+        mi_tensor_desc dc = d, iac = ia, ibc = ib;
+        dc.data += r0 * d.nb[1];
+        iac.data += r0 * ia.nb[0];
+        ibc.data += r0 * ib.nb[0];
+        dc.ne[1] = nr;
+        const dim3 g((unsigned) std::min<int64_t>((ne0 + 1023) / 1024, 64), (unsigned) nr);
+        switch (b.type) {
+            case 2: hipLaunchKernelGGL((k_get_rows_add<TA, 2>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
+            case 8: hipLaunchKernelGGL((k_get_rows_add<TA, 8>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
+            case 12: hipLaunchKernelGGL((k_get_rows_add<TA, 12>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
+            case 13: hipLaunchKernelGGL((k_get_rows_add<TA, 13>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
+            default: hipLaunchKernelGGL((k_get_rows_add<TA, 0>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
+        }
     }
 }
 

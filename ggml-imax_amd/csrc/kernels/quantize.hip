@@ -213,14 +213,24 @@ static __device__ __forceinline__ const char * col_base(const mi_src_cols & x, u
 // k_quantize_q8_K (quantize_row_q8_K_reference, src/ggml-quants.c:3370-3407). An all-zero
 // superblock gets d = 0, zero quants and zero bsums (the reference leaves its bsums untouched;
 // every dot product multiplies them by d = 0).
-__global__ __launch_bounds__(256) void k_quantize_rows_q8_K(mi_src_cols x, int64_t K, char * dst, mi_src_cols dl) {
+// A16: the source columns are 16-byte aligned (base and nb1..nb3), so a lane reads its 4 values with
+// one float4 load; otherwise (a view at an odd float offset) with four scalar loads.
+template <bool A16>
+__global__ __launch_bounds__(256) void k_quantize_rows_q8_K(mi_src_cols x, int64_t K, mi_src_cols dl) {
     const int wave = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int64_t b = (int64_t) blockIdx.y * 4 + wave;
     if (b >= K / 256) return;
     const uint32_t c = blockIdx.x;
-    const float4 v4 = *(const float4 *) ((const float *) col_base(x, c) + b * 256 + lane * 4);
-    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+    const float * src = (const float *) col_base(x, c) + b * 256 + lane * 4;
+    float v[4];
+    if constexpr (A16) {
+        const float4 v4 = *(const float4 *) src;
+        v[0] = v4.x, v[1] = v4.y, v[2] = v4.z, v[3] = v4.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[i] = src[i];
+    }
     uint32_t packed;
     int sum32;
     float d;
@@ -235,7 +245,6 @@ __global__ __launch_bounds__(256) void k_quantize_rows_q8_K(mi_src_cols x, int64
     *(uint32_t *) (blk + 4 + lane * 4) = packed;
     if ((lane & 3) == 0) *(int16_t *) (blk + 260 + 2 * (lane >> 2)) = (int16_t) s;
     if (lane == 0) *(float *) blk = d;
-    (void) dst;
 }
 
 // CPY F32 -> Q8_0: one block per half-wave (k_quantize_q8_0's rounding, the AVX2 branch of
@@ -261,7 +270,12 @@ __global__ __launch_bounds__(256) void k_quantize_rows_q8_0(mi_src_cols x, int64
 void mi_quantize_rows_q8(const mi_src_cols & x, int64_t K, bool is_q8K, const mi_src_cols & dst, hipStream_t s) {
     const int64_t ncols = x.ne1 * x.ne2 * x.ne3;
     if (ncols == 0) return;
-    if (is_q8K) hipLaunchKernelGGL(k_quantize_rows_q8_K, dim3((unsigned) ncols, (unsigned) ((K / 256 + 3) / 4)), dim3(256), 0, s, x, K, nullptr, dst);
+    if (is_q8K) {
+        const bool a16 = (((uintptr_t) x.base) | x.nb1 | x.nb2 | x.nb3) % 16 == 0;
+        const dim3 grid((unsigned) ncols, (unsigned) ((K / 256 + 3) / 4));
+        if (a16) hipLaunchKernelGGL(k_quantize_rows_q8_K<true>, grid, dim3(256), 0, s, x, K, dst);
+        else hipLaunchKernelGGL(k_quantize_rows_q8_K<false>, grid, dim3(256), 0, s, x, K, dst);
+    }
     else hipLaunchKernelGGL(k_quantize_rows_q8_0, dim3((unsigned) ncols, (unsigned) ((K / 32 + 7) / 8)), dim3(256), 0, s, x, K, dst);
 }
 

@@ -14,10 +14,14 @@ sp = lib.ggml_backend_mi355x_get_stream(be)
 Bs = [int(b) for b in sys.argv[1:]] or [512, 64]
 refs = {}
 VARS = [int(v) for v in os.environ.get("MMQ_VARIANTS", "0").split(",")]
+# PF_LONG: mmq_long settings to compare (Q4_K / Q5_K past 128 columns: 1 k_mmqw, 2 k_mmqr)
+LONGS = [int(v) for v in os.environ.get("PF_LONG", "0").split(",")]
+VARS = [(v, l) for v in VARS for l in LONGS]
 for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
     for B in Bs:
-      for var in VARS:
+      for var, lng in VARS:
         lib.ggml_backend_mi355x_set_tuning(b"mmq_variant", var)
+        lib.ggml_backend_mi355x_set_tuning(b"mmq_long", lng)
         t = bench.TYPE_NAMES[tname]
         R = int(os.environ.get("PF_R", "8"))  # weight copies per step (36 x 9.4 MB > the 256 MB Infinity Cache)
         wl = bench.MulMatWorkload(lib, be, t, 4096, 4096, B, R)
@@ -36,7 +40,7 @@ for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
         y = G.tensor_get(lib, wl.y[0])
         ref = refs.setdefault((tname, B), y)
         same = "bit-equal to the first variant" if np.array_equal(y.view(np.uint32), ref.view(np.uint32)) else "DIFFERS from the first variant"
-        print(f"{tname:5s} B={B:4d} var={var:5d} R={R}: {ms * 1e3 / R:8.2f} us/mul_mat in a graph of {R}  {2 * 4096 * 4096 * B * R / (ms / 1e3) / 1e12:7.1f} TFLOP/s  "
+        print(f"{tname:5s} B={B:4d} var={var:5d} long={lng} R={R}: {ms * 1e3 / R:8.2f} us/mul_mat in a graph of {R}  {2 * 4096 * 4096 * B * R / (ms / 1e3) / 1e12:7.1f} TFLOP/s  "
               f"| one per graph {ms1 * 1e3:8.2f} us  {same}")
         wl.free()
 lib.ggml_backend_free(be)
