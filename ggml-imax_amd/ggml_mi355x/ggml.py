@@ -17,7 +17,9 @@ import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_ROOT, "lib")
-CORE_LIB = os.path.join(LIB_DIR, "libggml_core.so")
+# GGML_MI355X_CORE_LIB: an alternative build of the host runtime (the sanitizer build of
+# `make -C ggml-imax_amd sanitize`, run by tools/sanitize.sh)
+CORE_LIB = os.environ.get("GGML_MI355X_CORE_LIB") or os.path.join(LIB_DIR, "libggml_core.so")
 BACKEND_LIB = os.path.join(LIB_DIR, "libggml_mi355x.so")
 GPT2_LIB = os.path.join(LIB_DIR, "libgpt2_mi355x.so")
 
@@ -261,11 +263,18 @@ BACKEND_EXPORTS = [k for k in _SIGS if k.startswith("ggml_backend_mi355x") or k 
 class Lib:
     """Binds the ggml API from one or more shared libraries (first match wins)."""
 
+    _namespaces = {}  # isolated library sets loaded by dlmopen, one link namespace each
+
     def __init__(self, paths, isolated: bool = False):
         # isolated: bind the library's internal calls to itself (RTLD_DEEPBIND, not global), so
-        # the reference libggml and the runtime can live in one process without interposing
-        mode = (ctypes.RTLD_LOCAL | os.RTLD_DEEPBIND) if isolated else ctypes.RTLD_GLOBAL
-        self.handles = [ctypes.CDLL(p, mode=mode) for p in paths]
+        # the reference libggml and the runtime can live in one process without interposing.
+        # Under AddressSanitizer (which refuses RTLD_DEEPBIND; tools/sanitize.sh sets
+        # GGML_MI355X_ISOLATE=dlmopen) the set goes into a link namespace of its own instead.
+        if isolated and os.environ.get("GGML_MI355X_ISOLATE") == "dlmopen":
+            self.handles = Lib._dlmopen(tuple(paths))
+        else:
+            mode = (ctypes.RTLD_LOCAL | os.RTLD_DEEPBIND) if isolated else ctypes.RTLD_GLOBAL
+            self.handles = [ctypes.CDLL(p, mode=mode) for p in paths]
         self.paths = list(paths)
         for name, (argtypes, restype) in _SIGS.items():
             if argtypes is None:
@@ -282,6 +291,27 @@ class Lib:
             fn.argtypes = argtypes
             fn.restype = restype
             setattr(self, name, fn)
+
+    @staticmethod
+    def _dlmopen(paths):
+        if paths in Lib._namespaces:
+            return Lib._namespaces[paths]
+        libc = ctypes.CDLL(None)
+        libc.dlmopen.restype = c_void_p
+        libc.dlmopen.argtypes = [ctypes.c_long, c_char_p, c_int]
+        libc.dlinfo.argtypes = [c_void_p, c_int, c_void_p]
+        lmid, handles = -1, []  # LM_ID_NEWLM, then the namespace of the first library
+        for p in paths:
+            h = libc.dlmopen(lmid, p.encode(), 2)  # RTLD_NOW
+            if not h:
+                raise OSError(f"dlmopen {p} failed")
+            if lmid == -1:
+                lm = ctypes.c_long()
+                libc.dlinfo(h, 1, ctypes.byref(lm))  # RTLD_DI_LMID
+                lmid = lm.value
+            handles.append(ctypes.CDLL(p, handle=h))
+        Lib._namespaces[paths] = handles
+        return handles
 
     def has(self, name: str) -> bool:
         return hasattr(self, name)
