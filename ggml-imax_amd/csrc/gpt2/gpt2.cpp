@@ -16,6 +16,7 @@
 #include "ggml_sched_abi.h"
 #endif
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -85,6 +86,15 @@ struct gpt2_model {
     void * sched = nullptr;                     // ggml_backend_sched_t
     int n_gpu_layers = 0;
     int sched_flags = 0;                        // GPT2_SCHED_*
+    // batched independent sequences (examples/gpt-2/main-batched.cpp:76-102): the KV cache as
+    // cells, each holding a position and the set of sequences that see it, filled from `kv_head`
+    struct kv_cell {
+        int32_t pos = -1;
+        std::vector<int32_t> seq;
+        bool has(int32_t s) const { return std::find(seq.begin(), seq.end(), s) != seq.end(); }
+    };
+    std::vector<kv_cell> cells;
+    uint32_t kv_head = 0, kv_n = 0;
 };
 
 namespace {
@@ -404,6 +414,90 @@ ggml_cgraph * build_graph(gpt2_model & m, int n_past, int N, int slot = 0) {
     return gf;
 }
 
+// gpt2_graph of examples/gpt-2/main-batched.cpp:552-717: n_tokens tokens of any sequences at
+// their own positions, written to the KV cells kv_head.., attending to the first n_kv cells
+// through KQ_mask ([n_kv, n_tokens], 0 or -inf, broadcast over the heads)
+ggml_cgraph * build_graph_batched(gpt2_model & m, int n_tokens, int n_kv, int kv_head, int slot = 0) {
+    const auto & hp = m.hp;
+    const int n_embd = hp.n_embd, n_layer = hp.n_layer, n_ctx = hp.n_ctx, n_head = hp.n_head;
+    const size_t buf_size = ggml_tensor_overhead() * kMaxNodes + ggml_graph_overhead_custom(kMaxNodes, false);
+    std::vector<uint8_t> & arena = m.graph_buf[slot];
+    if (arena.size() != buf_size) arena.resize(buf_size);
+    ggml_init_params ip = {buf_size, arena.data(), true};
+    ggml_context * ctx = ggml_init(ip);
+    ggml_cgraph * gf = ggml_new_graph_custom(ctx, kMaxNodes, false);
+
+    ggml_tensor * inp_tokens = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, n_tokens);
+    ggml_set_name(inp_tokens, "inp_tokens");
+    ggml_set_input(inp_tokens);
+    ggml_tensor * position = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, n_tokens);
+    ggml_set_name(position, "position");
+    ggml_set_input(position);
+    ggml_tensor * inpL = ggml_add(ctx, ggml_get_rows(ctx, m.wte, inp_tokens), ggml_get_rows(ctx, m.wpe, position));
+    ggml_tensor * KQ_mask = ggml_new_tensor_3d(ctx, GGML_TYPE_F32, n_kv, n_tokens, 1);
+    ggml_set_name(KQ_mask, "KQ_mask");
+    ggml_set_input(KQ_mask);
+
+    const size_t esk = ggml_element_size(m.memory_k), esv = ggml_element_size(m.memory_v);
+    for (int il = 0; il < n_layer; ++il) {
+        const layer_w & L = m.layers[il];
+        ggml_tensor * cur = ggml_norm(ctx, inpL, hp.eps);
+        cur = ggml_add(ctx, ggml_mul(ctx, cur, L.ln_1_g), L.ln_1_b);
+        cur = ggml_mul_mat(ctx, L.c_attn_attn_w, cur);
+        cur = ggml_add(ctx, cur, L.c_attn_attn_b);
+        {
+            ggml_tensor * Qcur = ggml_view_2d(ctx, cur, n_embd, n_tokens, cur->nb[1], 0 * sizeof(float) * n_embd);
+            ggml_tensor * Kcur = ggml_view_2d(ctx, cur, n_embd, n_tokens, cur->nb[1], 1 * sizeof(float) * n_embd);
+            ggml_tensor * Vcur = ggml_view_2d(ctx, cur, n_embd, n_tokens, cur->nb[1], 2 * sizeof(float) * n_embd);
+            ggml_tensor * k = ggml_view_1d(ctx, m.memory_k, (int64_t) n_tokens * n_embd, (esk * n_embd) * (il * n_ctx + kv_head));
+            ggml_tensor * v = ggml_view_1d(ctx, m.memory_v, (int64_t) n_tokens * n_embd, (esv * n_embd) * (il * n_ctx + kv_head));
+            ggml_build_forward_expand(gf, ggml_cpy(ctx, Kcur, k));
+            ggml_build_forward_expand(gf, ggml_cpy(ctx, Vcur, v));
+
+            ggml_tensor * Q = ggml_permute(ctx, ggml_cont_3d(ctx, Qcur, n_embd / n_head, n_head, n_tokens), 0, 2, 1, 3);
+            ggml_tensor * K = ggml_permute(
+                ctx,
+                ggml_reshape_3d(ctx, ggml_view_1d(ctx, m.memory_k, (int64_t) n_kv * n_embd, il * n_ctx * esk * n_embd),
+                                n_embd / n_head, n_head, n_kv),
+                0, 2, 1, 3);
+            ggml_tensor * KQ = ggml_mul_mat(ctx, K, Q);
+            ggml_tensor * KQ_scaled = ggml_scale(ctx, KQ, 1.0f / sqrtf(float(n_embd) / n_head));
+            ggml_tensor * KQ_masked = ggml_add(ctx, KQ_scaled, KQ_mask);
+            ggml_tensor * KQ_soft_max = ggml_soft_max(ctx, KQ_masked);
+            ggml_tensor * V_trans = ggml_cont_3d(
+                ctx,
+                ggml_permute(ctx,
+                             ggml_reshape_3d(ctx, ggml_view_1d(ctx, m.memory_v, (int64_t) n_kv * n_embd, il * n_ctx * esv * n_embd),
+                                             n_embd / n_head, n_head, n_kv),
+                             1, 2, 0, 3),
+                n_kv, n_embd / n_head, n_head);
+            ggml_tensor * KQV = ggml_mul_mat(ctx, V_trans, KQ_soft_max);
+            ggml_tensor * KQV_merged = ggml_permute(ctx, KQV, 0, 2, 1, 3);
+            cur = ggml_cont_2d(ctx, KQV_merged, n_embd, n_tokens);
+        }
+        cur = ggml_mul_mat(ctx, L.c_attn_proj_w, cur);
+        cur = ggml_add(ctx, cur, L.c_attn_proj_b);
+        cur = ggml_add(ctx, cur, inpL);
+        ggml_tensor * inpFF = cur;
+        cur = ggml_norm(ctx, inpFF, hp.eps);
+        cur = ggml_add(ctx, ggml_mul(ctx, cur, L.ln_2_g), L.ln_2_b);
+        cur = ggml_mul_mat(ctx, L.c_mlp_fc_w, cur);
+        cur = ggml_add(ctx, cur, L.c_mlp_fc_b);
+        cur = ggml_gelu(ctx, cur);
+        cur = ggml_mul_mat(ctx, L.c_mlp_proj_w, cur);
+        cur = ggml_add(ctx, cur, L.c_mlp_proj_b);
+        inpL = ggml_add(ctx, cur, inpFF);
+    }
+    inpL = ggml_norm(ctx, inpL, hp.eps);
+    inpL = ggml_add(ctx, ggml_mul(ctx, inpL, m.ln_f_g), m.ln_f_b);
+    inpL = ggml_mul_mat(ctx, m.lm_head, inpL);
+    ggml_set_name(inpL, "logits");
+    ggml_set_output(inpL);
+    ggml_build_forward_expand(gf, inpL);
+    ggml_free(ctx);
+    return gf;
+}
+
 void split_words(std::string str, std::vector<std::string> & words) {
     // examples/common.cpp:272-283
     static const std::regex re(R"('s|'t|'re|'ve|'m|'ll|'d| ?[[:alpha:]]+| ?[[:digit:]]+| ?[^\s[:alpha:][:digit:]]+|\s+(?!\S)|\s+)");
@@ -560,6 +654,98 @@ void gpt2_model_free(gpt2_model * m) {
 }
 
 void gpt2_model_hparams(const gpt2_model * m, gpt2_hparams_c * out) { *out = m->hp; }
+
+// ---- batched independent sequences (examples/gpt-2/main-batched.cpp) ------------------------------
+
+void gpt2_kv_cache_clear(gpt2_model * m) {
+    m->cells.assign((size_t) m->hp.n_ctx, gpt2_model::kv_cell());
+    m->kv_head = m->kv_n = 0;
+}
+
+// gpt2_kv_cache_seq_cp (main-batched.cpp:814-827): cells of seq_src at positions [p0, p1) are seen by
+// seq_dst too (p0 < 0: from 0, p1 < 0: to the end)
+void gpt2_kv_cache_seq_cp(gpt2_model * m, int32_t seq_src, int32_t seq_dst, int32_t p0, int32_t p1) {
+    if (m->cells.size() != (size_t) m->hp.n_ctx) gpt2_kv_cache_clear(m);
+    if (p0 < 0) p0 = 0;
+    if (p1 < 0) p1 = INT32_MAX;
+    for (auto & c : m->cells) {
+        if (c.has(seq_src) && c.pos >= p0 && c.pos < p1 && !c.has(seq_dst)) c.seq.push_back(seq_dst);
+    }
+}
+
+// gpt2_decode (main-batched.cpp:854-968): the batch's tokens go into KV cells kv_head.., the graph
+// attends to cells [0, kv_head + n_tokens) through the host-built KQ mask (a cell is visible to a
+// token when it belongs to the token's sequence at a position <= the token's)
+int gpt2_decode_batch(gpt2_model * m, int n_tokens, const int32_t * tokens, const int32_t * pos, const int32_t * seq_id,
+                      float * logits, int all_logits) {
+    if (n_tokens <= 0 || !tokens || !pos || !seq_id) {
+        fprintf(stderr, "gpt2_decode_batch: empty batch\n");
+        return -1;
+    }
+    if (m->sched) {
+        fprintf(stderr, "gpt2_decode_batch: not available in scheduler mode\n");
+        return -1;
+    }
+    if (m->cells.size() != (size_t) m->hp.n_ctx) gpt2_kv_cache_clear(m);
+    if (m->kv_head + (uint32_t) n_tokens > (uint32_t) m->hp.n_ctx) {
+        fprintf(stderr, "gpt2_decode_batch: KV cache full (%u + %d > %d)\n", m->kv_head, n_tokens, m->hp.n_ctx);
+        return -2;
+    }
+    // the decode loop's prebuilt graph (gpt2_eval) would reuse the arena and allocator: dropped
+    if (m->next_plan) {
+        ggml_backend_synchronize(m->backend);
+        ggml_backend_graph_plan_free(m->backend, m->next_plan);
+        m->next_plan = nullptr;
+    }
+    m->next_gf = nullptr;
+    const int64_t t0 = now_us();
+    for (int i = 0; i < n_tokens; i++) {
+        auto & c = m->cells[m->kv_head + i];
+        c.pos = pos[i];
+        c.seq.clear();
+        c.seq.push_back(seq_id[i]);
+    }
+    m->kv_n = m->kv_head + (uint32_t) n_tokens;
+    const int n_kv = (int) m->kv_n;
+    m->graph_slot ^= 1;
+    ggml_cgraph * gf = build_graph_batched(*m, n_tokens, n_kv, (int) m->kv_head, m->graph_slot);
+    const int64_t t1 = now_us();
+    if (!ggml_gallocr_alloc_graph(m->allocr, gf)) {
+        fprintf(stderr, "gpt2_decode_batch: graph allocation failed\n");
+        return 1;
+    }
+    const int64_t t2 = now_us();
+    ggml_backend_tensor_set(ggml_graph_get_tensor(gf, "inp_tokens"), tokens, 0, (size_t) n_tokens * sizeof(int32_t));
+    ggml_backend_tensor_set(ggml_graph_get_tensor(gf, "position"), pos, 0, (size_t) n_tokens * sizeof(int32_t));
+    {
+        std::vector<float> mask((size_t) n_kv * n_tokens, 0.0f);
+        for (int j = 0; j < n_tokens; j++) {
+            for (int i = 0; i < n_kv; i++) {
+                const auto & c = m->cells[i];
+                if (!c.has(seq_id[j]) || c.pos > pos[j]) mask[(size_t) j * n_kv + i] = -INFINITY;
+            }
+        }
+        ggml_backend_tensor_set(ggml_graph_get_tensor(gf, "KQ_mask"), mask.data(), 0, mask.size() * sizeof(float));
+    }
+    const int64_t t3 = now_us();
+    if (ggml_backend_graph_compute(m->backend, gf) != GGML_STATUS_SUCCESS) {
+        fprintf(stderr, "gpt2_decode_batch: graph compute failed\n");
+        return 1;
+    }
+    ggml_tensor * out = ggml_graph_get_tensor(gf, "logits");
+    const size_t nv = (size_t) m->hp.n_vocab;
+    if (logits) {
+        if (all_logits) ggml_backend_tensor_get(out, logits, 0, sizeof(float) * nv * n_tokens);
+        else ggml_backend_tensor_get(out, logits, sizeof(float) * nv * (n_tokens - 1), sizeof(float) * nv);
+    }
+    m->kv_head += (uint32_t) n_tokens;
+    m->last_nodes = gf->n_nodes;
+    m->us_build = t1 - t0;
+    m->us_alloc = t2 - t1;
+    m->us_inputs = t3 - t2;
+    m->us_compute = now_us() - t3;
+    return 0;
+}
 size_t gpt2_model_size(const gpt2_model * m) { return m->weight_bytes; }
 size_t gpt2_compute_buffer_size(const gpt2_model * m) { return ggml_gallocr_get_buffer_size(m->allocr, 0); }
 

@@ -233,6 +233,26 @@ class Model:
             raise RuntimeError("gpt2_eval failed")
         return out
 
+    def decode_batch(self, tokens, pos, seq_id, all_logits: bool = True) -> np.ndarray:
+        """gpt2_decode_batch (examples/gpt-2/main-batched.cpp gpt2_decode): token i of sequence
+        seq_id[i] at position pos[i]; logits [n_tokens or 1, n_vocab]."""
+        tok = np.ascontiguousarray(np.asarray(tokens, dtype=np.int32))
+        p = np.ascontiguousarray(np.asarray(pos, dtype=np.int32))
+        s = np.ascontiguousarray(np.asarray(seq_id, dtype=np.int32))
+        n = len(tok)
+        assert len(p) == n and len(s) == n
+        out = np.empty((n if all_logits else 1, self.n_vocab), dtype=np.float32)
+        rc = self.lib.gpt2_decode_batch(self.m, n, tok.ctypes.data, p.ctypes.data, s.ctypes.data, out.ctypes.data, 1 if all_logits else 0)
+        if rc != 0:
+            raise RuntimeError(f"gpt2_decode_batch failed ({rc})")
+        return out
+
+    def kv_seq_cp(self, src: int, dst: int, p0: int = -1, p1: int = -1):
+        self.lib.gpt2_kv_cache_seq_cp(self.m, src, dst, p0, p1)
+
+    def kv_clear(self):
+        self.lib.gpt2_kv_cache_clear(self.m)
+
     def stats(self) -> dict:
         n = ctypes.c_int()
         b, a, i, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
@@ -266,3 +286,19 @@ class Model:
             self.free()
         except Exception:
             pass
+
+
+def run_batched(model: "Model", prompt: list[int], n_parallel: int, forced: list[list[int]]) -> np.ndarray:
+    """main-batched.cpp's flow, teacher-forced: the prompt decoded once as sequence 0, its cells
+    shared with sequences 1..n_parallel-1 (gpt2_kv_cache_seq_cp), then one batch per step holding
+    token forced[t][s] of every sequence s at position len(prompt) + t. Returns the prompt's last
+    logits followed by every step's n_parallel rows: [1 + steps * n_parallel, n_vocab]."""
+    model.kv_clear()
+    n = len(prompt)
+    outs = [model.decode_batch(prompt, list(range(n)), [0] * n, all_logits=False)]
+    for s in range(1, n_parallel):
+        model.kv_seq_cp(0, s, -1, -1)
+    for t, row in enumerate(forced):
+        assert len(row) == n_parallel
+        outs.append(model.decode_batch(row, [n + t] * n_parallel, list(range(n_parallel)), all_logits=True))
+    return np.concatenate(outs)

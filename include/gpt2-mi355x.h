@@ -64,6 +64,17 @@ GGML_API size_t gpt2_compute_buffer_size(const struct gpt2_model * model);
 // are then only in gpt2_logits_host(), valid until the next eval. Returns 0 on success.
 GGML_API int gpt2_eval(struct gpt2_model * model, int n_past, const int32_t * tokens, int n_tokens, float * logits,
                        int all_logits);
+// Batched independent sequences (examples/gpt-2/main-batched.cpp): the KV cache as cells with
+// positions and sequence ids. gpt2_decode_batch (gpt2_decode, :854-968) runs n_tokens tokens, token i
+// of sequence seq_id[i] at position pos[i], writing them into the next free cells and attending
+// through main-batched's KQ mask; logits of the last token (n_vocab floats) or of all tokens.
+// Returns 0 on success, -2 when the cache is full. gpt2_kv_cache_seq_cp (:814-827) lets seq_dst see
+// seq_src's cells at positions [p0, p1) (-1: open end), e.g. a shared prompt; gpt2_kv_cache_clear
+// empties the cache. (Not in scheduler mode; do not interleave with gpt2_eval on one model.)
+GGML_API int gpt2_decode_batch(struct gpt2_model * model, int n_tokens, const int32_t * tokens, const int32_t * pos,
+                               const int32_t * seq_id, float * logits, int all_logits);
+GGML_API void gpt2_kv_cache_seq_cp(struct gpt2_model * model, int32_t seq_src, int32_t seq_dst, int32_t p0, int32_t p1);
+GGML_API void gpt2_kv_cache_clear(struct gpt2_model * model);
 // the host staging of the logits (gpt2_model_load_ex with a host buffer type), or NULL
 GGML_API const float * gpt2_logits_host(const struct gpt2_model * model);
 

@@ -403,11 +403,16 @@ def _teacher_forced_direct(m, toks):
     return np.concatenate(outs)
 
 
-def _run_sched_child(model_path, tmp_path, layers):
+def _run_sched_child(model_path, tmp_path, layers, order="1"):
+    """order "1": the MI355X layers' decode GEMVs in the reference order (bit-identical splits);
+    None: the backend's default (per graph, ggml-mi355x.cpp graph_decode_order)."""
     import sys
-    # bit-identical splits: the MI355X layers' decode GEMVs in the reference order
+    env = dict(os.environ)
+    env.pop("GGML_MI355X_MMV_ORDER", None)
+    if order is not None:
+        env["GGML_MI355X_MMV_ORDER"] = order
     p = subprocess.run([sys.executable, SCHED_CHILD, model_path, str(tmp_path), ",".join(str(v) for v in layers)],
-                       capture_output=True, text=True, timeout=600, env=dict(os.environ, GGML_MI355X_MMV_ORDER="1"))
+                       capture_output=True, text=True, timeout=600, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     return p.stdout
 
@@ -462,3 +467,115 @@ def test_gpt2_scheduler_options_host_inputs_events_mid_layer_split(model_path, t
         diff = float(np.max(np.abs(got - base)))
         print(f"{spec}: max |d| = {diff:.3e}")
         assert np.array_equal(got.view(np.uint32), base.view(np.uint32)), (spec, diff)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+def test_gpt2_partial_offload_default_order(model_path, tmp_path):
+    """The same scheduler splits with the backend's DEFAULT settings (no GGML_MI355X_MMV_ORDER):
+    the f16 model's graphs keep the tree order, so every split is within the north_star's 1e-3
+    (of max |logit|) of the CPU-only run, a mid-layer split included."""
+    specs = ["0", "3", "6", "12", "6:2"]
+    out = _run_sched_child(model_path, tmp_path, specs, order=None)
+    print(out)
+    base = np.load(tmp_path / "ngl0.npy")
+    scale = float(np.max(np.abs(base)))
+    for spec in specs[1:]:
+        got = np.load(tmp_path / ("ngl" + spec.replace(":", "_") + ".npy"))
+        rel = float(np.max(np.abs(got - base))) / scale
+        print(f"{spec}: max |d| / max |logit| = {rel:.3e}")
+        assert rel <= 1e-3, (spec, rel)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+def test_quantized_gpt2_partial_offload_default_order_bit_identical(quantized_paths, tmp_path):
+    """A Q4_K model under the reference scheduler with the DEFAULT settings: the scheduler's split
+    inputs are fresh NONE tensors named "<backend>#<src>#<copy>" (ggml-backend.c:1498-1523) that
+    hold computed activations, so graph_decode_order must run those graphs in the reference order.
+    Every split, a mid-layer one included, is bit-identical to the CPU-only run."""
+    specs = ["0", "3", "6", "12", "6:2"]
+    out = _run_sched_child(quantized_paths["q4_k"], tmp_path, specs, order=None)
+    print(out)
+    base = np.load(tmp_path / "ngl0.npy")
+    for spec in specs[1:]:
+        got = np.load(tmp_path / ("ngl" + spec.replace(":", "_") + ".npy"))
+        diff = float(np.max(np.abs(got - base)))
+        print(f"{spec}: max |d| = {diff:.3e}")
+        assert np.array_equal(got.view(np.uint32), base.view(np.uint32)), (spec, diff)
+
+
+# ---- batched independent sequences (examples/gpt-2/main-batched.cpp) ---------------------------------
+
+def _batched_scenario(n_parallel, steps=6, seed=11):
+    """An 8-token prompt (one decode-path batch) shared by every sequence, then `steps` batches of
+    one token per sequence, the tokens drawn per sequence so the sequences diverge."""
+    rng = np.random.default_rng(seed + n_parallel)
+    return rng.integers(0, 50257, size=(steps, n_parallel)).tolist()
+
+
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+def test_batched_sequences_match_single_sequence_runs_on_reference_cpu(model_path):
+    """The driver's batched mode (KV cells + seq ids + main-batched's KQ mask, run on the reference
+    CPU ops) gives every sequence the logits of that sequence run alone through main-backend's
+    graph: the cell bookkeeping and the mask are right (different graphs: close, not bit-equal)."""
+    ref, be, m = _ref_model(model_path)
+    try:
+        prompt = m.tokenize(PROMPT)[:8]
+        npar, forced = 3, _batched_scenario(3, steps=4)
+        b = gpt2.run_batched(m, prompt, npar, forced)
+        for s in range(npar):
+            toks = prompt + [forced[t][s] for t in range(len(forced))]
+            want = m.eval(0, toks, all_logits=True)[len(prompt) - 1:]
+            got = np.stack([b[0]] + [b[1 + t * npar + s] for t in range(len(forced))])
+            assert _rel_err(got, want) <= 1e-3, (s, _rel_err(got, want))
+    finally:
+        m.free()
+        ref.ggml_backend_free(be)
+
+
+def _batched_gpu_vs_ref(model_path, n_parallel):
+    lib = G.runtime()
+    be = G.mi355x_backend(lib)
+    ours = gpt2.Model(lib, model_path, be, n_ctx=256, n_batch=8)
+    ref, rbe, rm = _ref_model(model_path)
+    try:
+        prompt = ours.tokenize(PROMPT)[:8]
+        forced = _batched_scenario(n_parallel)
+        a = gpt2.run_batched(ours, prompt, n_parallel, forced)
+        b = gpt2.run_batched(rm, prompt, n_parallel, forced)
+        return a, b
+    finally:
+        ours.free()
+        rm.free()
+        lib.ggml_backend_free(be)
+        ref.ggml_backend_free(rbe)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+@pytest.mark.parametrize("n_parallel", [2, 4, 8])
+def test_batched_sequences_match_reference_cpu(model_path, n_parallel):
+    """main-batched.cpp's flow (shared prompt, n_parallel sequences decoded together) on MI355X with
+    the default settings: every batch's logits within 1e-3 of max |logit| of the reference CPU
+    running the same driver and graph."""
+    a, b = _batched_gpu_vs_ref(model_path, n_parallel)
+    err = _rel_err(a, b)
+    print(f"n_parallel={n_parallel}: max rel logit error {err:.2e}")
+    assert err <= LOGIT_TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
+@pytest.mark.parametrize("n_parallel", [2, 4, 8])
+def test_batched_sequences_bit_identical_reference_order(model_path, n_parallel):
+    """The same with mmv_order=1: every batch (at most 8 tokens: the decode path) bit-identical to the
+    reference CPU's logits."""
+    lib = G.runtime()
+    assert lib.ggml_backend_mi355x_set_tuning(b"mmv_order", 1)
+    try:
+        a, b = _batched_gpu_vs_ref(model_path, n_parallel)
+    finally:
+        lib.ggml_backend_mi355x_set_tuning(b"mmv_order", -1)
+    print(f"n_parallel={n_parallel}: identical {float(np.mean(a == b)):.4f}, max rel err {_rel_err(a, b):.2e}")
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
