@@ -226,6 +226,50 @@ def gpt2_q4k_bench(lib, backend, n_decode):
     return r
 
 
+def gpt2_batched_bench(lib, backend, n_parallel=8, n_steps=48):
+    """examples/gpt-2/main-batched.cpp's workload on MI355X: an 8-token prompt decoded once and
+    shared by n_parallel sequences (KV cells + seq ids), then n_steps batches of one greedy token per
+    sequence through the KQ-mask graph (ggml_backend_graph_compute: captured into hipGraphs inside
+    graph_compute). Aggregate decode tokens/s over all sequences; the same loop with graph capture
+    off beside it (graph_compute decode with and without capture)."""
+    from ggml_mi355x import gpt2
+    m = gpt2.Model(lib, gpt2.ensure_model(), backend, n_ctx=256, n_batch=8)
+
+    def run():
+        prompt = m.tokenize(GPT2_PROMPT)[:8]
+        m.kv_clear()
+        lg = m.decode_batch(prompt, list(range(len(prompt))), [0] * len(prompt), all_logits=False)
+        for s in range(1, n_parallel):
+            m.kv_seq_cp(0, s, -1, -1)
+        nxt = [int(np.argmax(lg[-1]))] * n_parallel
+        seqs = list(range(n_parallel))
+        for w in range(4):  # warm-up steps (not timed)
+            lg = m.decode_batch(nxt, [len(prompt) + w] * n_parallel, seqs)
+            nxt = [int(v) for v in np.argmax(lg, axis=1)]
+        t0 = time.perf_counter()
+        for t in range(n_steps):
+            lg = m.decode_batch(nxt, [len(prompt) + 4 + t] * n_parallel, seqs)
+            nxt = [int(v) for v in np.argmax(lg, axis=1)]
+        return time.perf_counter() - t0
+
+    try:
+        dt = run()
+        r = {"workload": f"{n_parallel} sequences sharing an 8-token prompt, {n_steps} batched decode steps (main-batched.cpp)",
+             "decode_tokens_per_s": round(n_parallel * n_steps / dt, 1), "ms_per_step": round(dt / n_steps * 1e3, 4),
+             "kernel_launches_per_step": lib.ggml_backend_mi355x_last_launch_count(backend),
+             "parity": "within 1e-3 of the reference CPU, bit-identical with mmv_order=1 (tests/test_gpt2.py batched tests)"}
+        if hasattr(lib, "ggml_backend_mi355x_set_graph_capture"):
+            lib.ggml_backend_mi355x_set_graph_capture(backend, False)
+            try:
+                dt2 = run()
+            finally:
+                lib.ggml_backend_mi355x_set_graph_capture(backend, True)
+            r["no_graph_capture"] = {"decode_tokens_per_s": round(n_parallel * n_steps / dt2, 1), "ms_per_step": round(dt2 / n_steps * 1e3, 4)}
+        return r
+    finally:
+        m.free()
+
+
 def gpt2_cpu_baseline(threads, n_predict=64, path=None):
     """The reference's own examples/gpt-2/main-backend.cpp (oracle/_ref/gpt-2-backend, built from
     the reference sources) on the same synthetic model, CPU backend: its printed ms per token."""
@@ -637,6 +681,7 @@ def main():
         # BASELINE config 4 (the metric's "+ GPT-2 tokens/s" half)
         result["gpt2"] = gpt2_f16_bench(lib, backend, args.gpt2_tokens)
         result["gpt2_q4_k"] = gpt2_q4k_bench(lib, backend, args.gpt2_tokens)
+        result["gpt2_batched"] = gpt2_batched_bench(lib, backend)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(t, K, N, B, args.cpu_seconds)

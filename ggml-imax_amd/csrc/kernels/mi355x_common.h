@@ -1,6 +1,12 @@
 // mi355x_common.h -- device helpers shared by the gfx950 kernels (wave64, CDNA4).
 #pragma once
 
+// diagnostic builds (make DIAG=1): timing-ablation and stamp kernels, whose results are invalid,
+// become reachable through ggml_backend_mi355x_set_tuning; release builds compile them out
+#ifndef MI_DIAG
+#define MI_DIAG 0
+#endif
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -597,7 +597,7 @@ void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N,
     const int var = g_mi_tuning.mmq_variant;
     const bool v3 = (var & 1) == 0;
     const bool xcd = (var & 2) != 0;
-    const int abl = (var >> 3) & 3;
+    const int abl = MI_DIAG ? (var >> 3) & 3 : 0;  // timing ablations (results invalid): make DIAG=1 only
     const int nst2 = sk2 ? (int) (K / BK / 2) : 0;
     const dim3 grid1((unsigned) (((grid.x * grid.y) + 7) / 8 * 8));
 #define MI_MMQ3(T, NST) hipLaunchKernelGGL((k_mmq3<T, 2, NST, false>), grid, dim3(512), 0, s, w, nb01, K, N, xh, ncols, dst, ycol)

@@ -1132,7 +1132,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
 // superblock s (RING = XL + 1 slots), i.e. after the activations it must not hold back. A wait for
 // the activations of s then forces only weights requested XL superblocks earlier: both operands get
 // XL superblocks of latency cover (XL = 1 measured latency-bound: 42.9 us at B = 512).
-template <int TYPE, int XL, int SCT = 0>
+template <int TYPE, int XL, int CH>
 __global__ __launch_bounds__(512, 2) void k_mmqr(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -1195,21 +1195,12 @@ __global__ __launch_bounds__(512, 2) void k_mmqr(mi_mmx_group grp) {
     i32x4 xa[XL][8];
     half8 xu[XL];
     float da[XL];
-#pragma unroll
-    for (int u = 0; u < XL; u++) {
-#pragma unroll
-        for (int kk = 0; kk < 8; kk++) xa[u][kk] = ld_x(u, kk);
-        xu[u] = ld_u(u);
-        da[u] = ld_d(u);
-    }
-#pragma unroll
-    for (int u = 0; u < RING; u++) load_w(wt[u], u);
     // superblock sb from slots (sb % RING, sb % XL), then the slots' refills: sb + XL's activations,
     // sb + RING's weights. The loop runs whole unrolled rounds (every slot index static); the steps
     // past S compute nothing but still issue their (clamped) requests, so every path through the
     // body issues the same loads and the compiler's vmcnt bookkeeping stays exact (a load under a
     // branch makes it drain at the join).
-    auto step = [&](Wt & cur, i32x4 (&xs)[8], half8 & xuc, float & dac, const int sb) {
+    auto step = [&](Wt & cur, i32x4 (&xs)[8], half8 & xuc, float & dac, const int sb, const bool refill_x, const bool refill_w) {
         if (sb < S) {  // wave-uniform
             const uint32_t w0 = cur.hdr.y, w1 = cur.hdr.z, w2 = cur.hdr.w;
             const uint32_t sca = w0 & 0x3F3F3F3Fu;
@@ -1278,26 +1269,35 @@ __global__ __launch_bounds__(512, 2) void k_mmqr(mi_mmx_group grp) {
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             cfold_vec(gsum, y, tv, sb, gs, S);
         }
+        if (refill_x) {
 #pragma unroll
-        for (int kk = 0; kk < 8; kk++) xs[kk] = ld_x(sb + XL, kk);
-        xuc = ld_u(sb + XL);
-        dac = ld_d(sb + XL);
-        load_w(cur, sb + RING);  // after this superblock's activation requests (see above)
-    };
-    constexpr int UNR = XL * RING;  // every slot index static
-    if constexpr (SCT > 0) {
-        // S == SCT (host-checked): straight-line code, no loop-carried vmcnt bookkeeping (the
-        // compiler drains vmcnt at the loop header of the rolled form); the sched barriers keep
-        // each superblock's instructions (and registers) inside its own step
-#pragma unroll
-        for (int u = 0; u < SCT; u++) {
-            step(wt[u % RING], xa[u % XL], xu[u % XL], da[u % XL], u);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int kk = 0; kk < 8; kk++) xs[kk] = ld_x(sb + XL, kk);
+            xuc = ld_u(sb + XL);
+            dac = ld_d(sb + XL);
         }
-    } else {
-        for (int sb0 = 0; sb0 < S; sb0 += UNR) {
+        if (refill_w) load_w(cur, sb + RING);  // after this superblock's activation requests (see above)
+    };
+    // K in chunks of CH superblocks (CH % (XL RING) == 0: every slot index static), each chunk
+    // straight-line code: a rolled loop carrying the ring across its back edge makes the compiler
+    // drain vmcnt at the loop header, so the ring refills at a chunk start instead (one load latency
+    // per CH superblocks; K = 4096 is one chunk). The sched barriers keep each superblock's
+    // instructions (and registers) inside its own step.
+    static_assert(CH % (XL * RING) == 0, "chunk of whole slot rounds");
+    for (int c0 = 0; c0 < S; c0 += CH) {
 #pragma unroll
-            for (int u = 0; u < UNR; u++) step(wt[u % RING], xa[u % XL], xu[u % XL], da[u % XL], sb0 + u);
+        for (int u = 0; u < XL; u++) {
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) xa[u][kk] = ld_x(c0 + u, kk);
+            xu[u] = ld_u(c0 + u);
+            da[u] = ld_d(c0 + u);
+        }
+#pragma unroll
+        for (int u = 0; u < RING; u++) load_w(wt[u], c0 + u);
+        __builtin_amdgcn_sched_barrier(0);  // (else the scheduler sinks these loads to their first use)
+#pragma unroll
+        for (int u = 0; u < CH; u++) {
+            step(wt[u % RING], xa[u % XL], xu[u % XL], da[u % XL], c0 + u, u + XL < CH, u + RING < CH);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
     // accumulator element el: prompt column c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
@@ -2093,8 +2093,9 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         if (S <= 16 && (var & 2048)) {  // one round: a wave per superblock (variant bit 2048: k_mmqd1)
             const size_t lds = (size_t) S * 64 * 16 * sizeof(float) + (size_t) S * 32 * sizeof(float);
             // ABL bits 1..8 from variant bits 12..15, 16 from bit 23
+#if MI_DIAG  // timing ablations (results invalid): diagnostic builds only (make DIAG=1)
             const int abl = ((var >> 12) & 15) | (((var >> 23) & 1) << 4);
-            if (abl && type == 12) {  // timing ablations (results invalid)
+            if (abl && type == 12) {
 #define MI_MMQD1A(A) hipLaunchKernelGGL((k_mmqd1<12, A>), grid, dim3(64 * S), lds, s, g)
                 switch (abl) {
                 case 1: MI_MMQD1A(1); break;
@@ -2108,6 +2109,7 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
 #undef MI_MMQD1A
                 return;
             }
+#endif
             if (type == 12) hipLaunchKernelGGL((k_mmqd1<12>), grid, dim3(64 * S), lds, s, g);
             else hipLaunchKernelGGL((k_mmqd1<13>), grid, dim3(64 * S), lds, s, g);
             return;
@@ -2148,22 +2150,19 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     }
     if (g_mi_tuning.mmq_long == 2) {  // weights dequantized in registers, 128 x 64 tiles of 8 waves
         const dim3 gridr((unsigned) mmx_deal(g, 128, 64));
-        if (K == 4096) {
-            if (type == 12) hipLaunchKernelGGL((k_mmqr<12, 2, 16>), gridr, dim3(512), 0, s, g);
-            else hipLaunchKernelGGL((k_mmqr<13, 1, 16>), gridr, dim3(512), 0, s, g);
-        } else {
-            if (type == 12) hipLaunchKernelGGL((k_mmqr<12, 2>), gridr, dim3(512), 0, s, g);
-            else hipLaunchKernelGGL((k_mmqr<13, 1>), gridr, dim3(512), 0, s, g);
-        }
+        if (type == 12) hipLaunchKernelGGL((k_mmqr<12, 2, 18>), gridr, dim3(512), 0, s, g);
+        else hipLaunchKernelGGL((k_mmqr<13, 1, 16>), gridr, dim3(512), 0, s, g);
         return;
     }
     const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));
     // warp-specialized k_mmqw (4 loader + 8 MFMA waves; Q4_K B=512 32.1 -> 31.2 us, Q5_K 46.2 ->
     // 43.8 us grouped, profiles/r03r_prefill_mmqw.txt) unless variant bit 2^28 asks for k_mmqx
+#if MI_DIAG
     if ((var & 1024) && (var & (1 << 29)) && type == 12) {  // k_mmqw timing stamps (results invalid)
         hipLaunchKernelGGL((k_mmqw<12, 4, 8>), grid, dim3(768), 0, s, g);
         return;
     }
+#endif
     if (!(var & ((1 << 28) | 64 | 1024)) && (K / 256) % 4 == 0) {
         if (type == 12) hipLaunchKernelGGL((k_mmqw<12, 4>), grid, dim3(768), 0, s, g);
         else hipLaunchKernelGGL((k_mmqw<13, 4>), grid, dim3(768), 0, s, g);
@@ -2173,10 +2172,12 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     // for K = 4096, SCT = 16, spills: the compiler hoists loads across stages.)
 #define MI_MMQX_T(TY, LD) hipLaunchKernelGGL((k_mmqx<TY, false, 0, LD, 0>), grid, dim3(512), 0, s, g)
     const int lead = (var & 64) ? 1 : 4;
+#if MI_DIAG
     if (var & 1024) {  // timing stamps (results invalid)
         if (type == 12) hipLaunchKernelGGL((k_mmqx<12, false, 8, 4, 0>), grid, dim3(512), 0, s, g);
         return;
     }
+#endif
     if (type == 12) {
         if (lead == 1) MI_MMQX_T(12, 1); else MI_MMQX_T(12, 4);
     } else {

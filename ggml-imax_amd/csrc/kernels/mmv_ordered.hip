@@ -905,12 +905,14 @@ void mi_attn_ordered(const mi_attn_desc & a, const uint16_t * exp_table, hipStre
     const dim3 grid((unsigned) a.H, (unsigned) a.N);
     if (fast_ok && a.D == 64 && a.n_kv <= 512) {
         const size_t lds = (size_t) a.n_kv * (64 + 2) * sizeof(float);
-        switch (g_mi_tuning.attn_abl) {  // timing ablations only (results invalid)
+#if MI_DIAG
+        switch (g_mi_tuning.attn_abl) {  // timing ablations only (results invalid): make DIAG=1
             case 1: hipLaunchKernelGGL((k_attn_fast<64, 512, 1>), grid, dim3(512), lds, s, a, exp_table); return;
             case 2: hipLaunchKernelGGL((k_attn_fast<64, 512, 2>), grid, dim3(512), lds, s, a, exp_table); return;
             case 3: hipLaunchKernelGGL((k_attn_fast<64, 512, 3>), grid, dim3(512), lds, s, a, exp_table); return;
             default: break;
         }
+#endif
         if (a.n_kv <= 128) hipLaunchKernelGGL((k_attn_fast<64, 128>), grid, dim3(512), lds, s, a, exp_table);
         else if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_fast<64, 256>), grid, dim3(512), lds, s, a, exp_table);
         else hipLaunchKernelGGL((k_attn_fast<64, 512>), grid, dim3(512), lds, s, a, exp_table);
