@@ -1310,6 +1310,224 @@ __global__ __launch_bounds__(512, 2) void k_mmqr(mi_mmx_group grp) {
     }
 }
 
+// ---- long prompts, shared operands staged in LDS, weights dequantized in registers: k_mmqs --------
+// k_mmqr's per-wave direct loads put every operand through the vector L1 once per wave that uses it
+// (activations 4x, weights 2x: ~123 KB per superblock step per CU) and measured 43.8 us at B = 512
+// (load-path bound). Here the workgroup stages each superblock's operands ONCE into LDS -- the
+// activation quants of its 64 columns [8 steps][64][32] (16 KB), their U halves and scales, and the
+// raw weight blocks of its 128 rows (18 KB) -- and every wave reads its fragments from LDS, then
+// dequantizes its own 32 rows' planes in registers (k_mmqr's step) and runs its 32 x 32 tile.
+// Pipeline: the staging loads of superblock s + 2 are issued as step s starts and written into
+// the free LDS buffer at its end (two steps of latency cover; double-buffered LDS, one barrier per
+// step that waits for LDS traffic only, mi_lds_barrier). Staging roles are wave-uniform (waves 0-3
+// the activation quants, 4-7 the weights, U halves and scales), so every load uses a buffer
+// descriptor with an SGPR superblock offset. Activation fragments are stored with their two 16-byte
+// halves swapped for columns 16-31 of a 32-column group (the ds_read_b128 lane groups then hit 64
+// distinct banks). Same operands and canonical combine (mmqx_term, cfold_vec) as every kernel of
+// this file: bit-identical. Code: K in straight-line chunks of CH superblocks (as k_mmqr).
+template <int TYPE, int CH>
+__global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
+    MI_MMX_MEMBER(grp);
+    using F = XFmt<TYPE>;
+    constexpr int NP = F::NP;
+    constexpr int BM = 128, BN = 64;
+    constexpr int XB = 8 * BN * 32;           // activation quants of one superblock
+    constexpr int UB = BN * 32;               // U halves
+    constexpr int DB = BN * 4;                // d_a
+    constexpr int WB = BM * F::BS;            // raw weight blocks
+    constexpr int SB = XB + UB + DB + WB;     // one stage
+    constexpr int WCH = WB / 16;              // 16-byte weight chunks per stage (Q4_K 1152, Q5_K 1408)
+
+    const int tid = (int) threadIdx.x;
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int rw = w & 3, cw = w >> 2;
+    const int64_t ncols = act.ncols;
+    const int S = (int) (K / 256);
+    const int gs = cfold_gs(S);
+    const int64_t nrt = (N + BM - 1) / BM;
+    const int64_t n0 = (mmx_tile % nrt) * BM, c0 = (mmx_tile / nrt) * BN;
+    const int nrows = (int) std::min<int64_t>(BM, N - n0);
+
+    const uint32_t xstep = (uint32_t) ncols * 32;
+
+    // ---- staging: a stage is the concatenation [X 1024 | U 128 | d_a 16 | W WCH] of 16-byte chunks;
+    // thread t moves chunks t + 512 i (i < NLD). Every slot is a global load at a per-lane base +
+    // superblock x per-lane stride and an LDS store, with no branch (the compiler's vmcnt bookkeeping
+    // stays exact only on branch-free paths): slots past the end re-read the thread's first chunk and
+    // store into a 256-byte sink.
+    typedef __attribute__((address_space(1))) const i32x4 * gp_t;  // (native vectors: the HIP uint4
+    // class in a struct array kept the staging registers in scratch)
+    constexpr int NCH = 1024 + 128 + 16 + WCH;
+    constexpr int NLD = (NCH + 511) / 512;
+    constexpr int SINK = 2 * SB;                       // 256-byte sink after the two stages
+    __shared__ __attribute__((aligned(16))) char lds[2 * SB + 256];
+    const char * sbase[NLD];
+    uint32_t sstride[NLD], sdst[NLD];
+    auto col_of = [&](int c) { return std::min<int64_t>(c0 + c, ncols - 1); };
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+        int q = tid + 512 * i;
+        const bool real = q < NCH;
+        if (!real) q = tid;  // re-read chunk tid (an activation chunk), store into the sink
+        if (q < 1024) {  // activation quants: step kk, column col, half
+            const int kk = q >> 7, col = (q & 127) >> 1, half = q & 1;
+            sbase[i] = (const char *) act.xq + ((int64_t) kk * ncols + col_of(col)) * 32 + 16 * half;
+            sstride[i] = 8 * xstep;
+            sdst[i] = (uint32_t) (kk * (BN * 32) + col * 32 + 16 * (half ^ ((col >> 4) & 1)));
+        } else if (q < 1024 + 128) {  // U halves
+            const int qq = q - 1024, col = qq >> 1, half = qq & 1;
+            sbase[i] = (const char *) act.xu + col_of(col) * 32 + 16 * half;
+            sstride[i] = (uint32_t) ncols * 32;
+            sdst[i] = (uint32_t) (XB + col * 32 + 16 * (half ^ ((col >> 4) & 1)));
+        } else if (q < 1024 + 128 + 16) {  // d_a of columns 4 qq .. 4 qq + 3
+            const int qq = q - 1024 - 128;
+            sbase[i] = (const char *) act.xd + col_of(4 * qq) * 4;
+            sstride[i] = (uint32_t) ncols * 4;
+            sdst[i] = (uint32_t) (XB + UB + 16 * qq);
+        } else {  // raw weight blocks: row, 16-byte chunk c of the row's superblock
+            const int qq = q - 1024 - 128 - 16;
+            const int row = qq / (F::BS / 16), c = qq % (F::BS / 16);
+            sbase[i] = (const char *) W + (n0 + std::min(row, nrows - 1)) * (int64_t) nb01 + 16 * c;
+            sstride[i] = F::BS;
+            sdst[i] = (uint32_t) (XB + UB + DB + row * F::BS + 16 * c);
+        }
+        if (!real) sdst[i] = (uint32_t) (SINK + 16 * (tid & 15));
+    }
+    struct Stg {
+        i32x4 v[NLD];
+    };
+    auto stage_load = [&](Stg & st, int sb) {
+        sb = std::min(sb, S - 1);
+#pragma unroll
+        for (int i = 0; i < NLD; i++) st.v[i] = *(gp_t) (sbase[i] + (uint32_t) sb * sstride[i]);
+    };
+    auto stage_store = [&](const Stg & st, int buf) {
+#pragma unroll
+        for (int i = 0; i < NLD; i++) {
+            const uint32_t d = sdst[i] >= (uint32_t) SINK ? sdst[i] : sdst[i] + (uint32_t) (buf * SB);
+            *(i32x4 *) (lds + d) = st.v[i];
+        }
+    };
+
+    // ---- compute role (every wave): rows n0 + 32 rw + r, columns c0 + 32 cw + 16-column groups
+    const int col = 32 * cw + r;
+    const uint32_t xoff = (uint32_t) (col * 32 + 16 * (h ^ ((col >> 4) & 1)));
+    constexpr uint32_t kQs = F::Q5 ? 48 : 16;
+    const uint32_t woff = (uint32_t) (XB + UB + DB + (32 * rw + r) * F::BS);
+    f32x16 y = f32x16(-0.0f), gsum = {};
+
+    auto compute = [&](int buf, int sb) {
+        const char * base = lds + buf * SB;
+        const char * wr = base + woff;
+        const uint4 hdr = *(const uint4 *) wr;
+        uint4 q4[4], qh = {};
+#pragma unroll
+        for (int p = 0; p < 4; p++) q4[p] = *(const uint4 *) (wr + kQs + 32 * p + 16 * h);
+        if constexpr (F::Q5) qh = *(const uint4 *) (wr + 16 + 16 * h);
+        const uint32_t w0 = hdr.y, w1 = hdr.z, w2 = hdr.w;
+        const uint32_t sca = w0 & 0x3F3F3F3Fu;
+        const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
+        const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
+        const uint32_t ma = w1 & 0x3F3F3F3Fu;
+        const uint32_t mb = ((w2 >> 4) & 0x0F0F0F0Fu) | ((w1 >> 2) & 0x30303030u);
+        const uint32_t mw = h ? mb : ma;
+        i32x16 acc[NP];
+        uint32_t lo[4], hi[4];
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const i32x4 xa = *(const i32x4 *) (base + kk * (BN * 32) + xoff);
+            if ((kk & 1) == 0) {
+                const uint4 q = q4[kk >> 1];
+                const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    lo[e] = qv[e] & 0x0F0F0F0Fu;
+                    hi[e] = (qv[e] >> 4) & 0x0F0F0F0Fu;
+                }
+            }
+            uint32_t v[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                v[e] = (kk & 1) ? hi[e] : lo[e];
+                if constexpr (F::Q5) {
+                    const uint32_t hb[4] = {qh.x, qh.y, qh.z, qh.w};
+                    v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
+                }
+            }
+            const uint32_t scw = kk < 4 ? sca : scb;
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                const uint32_t f = __builtin_amdgcn_ubfe(scw, 8 * (kk & 3) + (F::Q5 ? 2 * p : 3 * p), F::Q5 ? 2 : 3);
+                const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+                acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa, b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
+            }
+        }
+        // U on the f16 MFMA: A = [S & 63, S >> 6] of the lane's column, B = [m, 64 m] of its row
+        half8 mu;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t m = (mw >> (8 * q)) & 0xFF;
+            mu[2 * q] = (_Float16) (float) m;
+            mu[2 * q + 1] = (_Float16) (float) (64 * m);
+        }
+        const half8 xu = *(const half8 *) (base + XB + xoff);
+        const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
+        const float * dal = (const float *) (base + XB + UB) + 32 * cw;
+        f32x16 tv;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; g4++) {
+            const float4 d4 = *(const float4 *) &dal[8 * g4 + 4 * h];
+            const float dav[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int el = 4 * g4 + e;
+                int T = acc[NP - 1][el];
+#pragma unroll
+                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
+                tv[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
+            }
+        }
+        cfold_vec(gsum, y, tv, sb, gs, S);
+    };
+
+    Stg st0, st1;  // (two variables, not an array: a register pair the unrolled steps alternate)
+    static_assert(CH % 2 == 0, "staging registers alternate");
+    for (int c0k = 0; c0k < S; c0k += CH) {
+        // chunk prologue: superblocks c0k, c0k + 1 requested, the first stored
+        stage_load(st0, c0k);
+        stage_load(st1, c0k + 1);
+        stage_store(st0, 0);
+        mi_lds_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // step u: `mine` held superblock c0k + u (stored last step) and now requests u + 2; `next`
+        // holds u + 1, stored into the buffer the previous step read
+        auto step = [&](Stg & mine, Stg & next, const int u) {
+            const int sb = c0k + u;
+            if (u + 2 < CH) stage_load(mine, sb + 2);
+            if (sb < S) compute(u & 1, sb);
+            if (u + 1 < CH) stage_store(next, (u + 1) & 1);
+            mi_lds_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        };
+#pragma unroll
+        for (int u = 0; u < CH; u += 2) {
+            step(st0, st1, u);
+            step(st1, st0, u + 1);
+        }
+    }
+
+    // accumulator element el: prompt column c0 + 32 cw + (el & 3) + 8 (el >> 2) + 4 h, row n0 + 32 rw + r
+    const int64_t n = n0 + 32 * rw + r;
+    if (n >= N) return;
+#pragma unroll
+    for (int el = 0; el < 16; el++) {
+        const int64_t c = c0 + 32 * cw + (el & 3) + 8 * (el >> 2) + 4 * h;
+        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y[el];
+    }
+}
+
 // ---- Q4_0 / Q8_0 prefill: the reference's exact int32 block sums on the int8 matrix cores --------
 // The reference dots (vec_dot_q4_0_q8_0, src/ggml-quants.c:3469-3874, AVX2 :3600-3623;
 // vec_dot_q8_0_q8_0, :4819, AVX2 :4925+) compute, per 32-block b, the exact int32
@@ -2152,6 +2370,12 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         const dim3 gridr((unsigned) mmx_deal(g, 128, 64));
         if (type == 12) hipLaunchKernelGGL((k_mmqr<12, 2, 18>), gridr, dim3(512), 0, s, g);
         else hipLaunchKernelGGL((k_mmqr<13, 1, 16>), gridr, dim3(512), 0, s, g);
+        return;
+    }
+    if (g_mi_tuning.mmq_long == 3) {  // + shared operands staged once per workgroup in LDS
+        const dim3 gridr((unsigned) mmx_deal(g, 128, 64));
+        if (type == 12) hipLaunchKernelGGL((k_mmqs<12, 16>), gridr, dim3(512), 0, s, g);
+        else hipLaunchKernelGGL((k_mmqs<13, 16>), gridr, dim3(512), 0, s, g);
         return;
     }
     const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));
