@@ -758,6 +758,14 @@ static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const vo
     m.nb3 = nb3;
 
     const int xkind = mm_act_kind(m, src1);
+    if (xkind == 5 && m.type == GGML_TYPE_F16 && src1->type == GGML_TYPE_F32 && src1->ne[2] == 1 && src1->ne[3] == 1 &&
+        mi_mmf16p_f32_supported(m.K, m.N, m.nb01, src1->ne[1], m.nb1, src1->data, src1->nb[1])) {
+        // F16 weights, a short prompt of plain f32 columns: one launch, activations rounded to f16
+        // inside the GEMM (k_mmf16p<F32X>)
+        mi_mul_mat_f16p_f32(m.W, m.nb01, m.K, m.N, (const float *) src1->data, src1->nb[1], src1->ne[1], m.dst, m.nb1, ctx->stream);
+        ctx->last_launches++;
+        return;
+    }
     if (xkind < 0) {
         MI_ASSERT(src0->type == GGML_TYPE_F32);
         mi_mul_mat_f32(m, src_cols(src1), ctx->stream);
@@ -2736,7 +2744,7 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.mmq_variant = value;
         return true;
     }
-    if (strcmp(name, "mmq_long") == 0 && value >= 0 && value <= 3) {
+    if (strcmp(name, "mmq_long") == 0 && value >= 0 && value <= 5) {
         g_mi_tuning.mmq_long = value;
         return true;
     }

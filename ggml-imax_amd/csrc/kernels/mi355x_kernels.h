@@ -140,6 +140,11 @@ bool mi_mmq_supported(int type, int64_t K, size_t nb01, size_t ycol);
 bool mi_mmf16p_supported(int64_t K, int64_t N, size_t nb01, int64_t ncols, size_t ycol);
 void mi_mul_mat_f16p(const void * W, size_t nb01, int64_t K, int64_t N, const uint16_t * xh, int64_t ncols, float * dst, size_t ycol,
                      hipStream_t s);
+// the same reading the f32 src1 columns (xnb1 bytes apart) and rounding them to f16 in the kernel
+// (one launch, no conversion pass); 16-byte aligned columns
+bool mi_mmf16p_f32_supported(int64_t K, int64_t N, size_t nb01, int64_t ncols, size_t ycol, const void * x, size_t xnb1);
+void mi_mul_mat_f16p_f32(const void * W, size_t nb01, int64_t K, int64_t N, const float * x, size_t xnb1, int64_t ncols, float * dst,
+                         size_t ycol, hipStream_t s);
 // scratch for the f16 expansion of quantized activations when xh == nullptr (0 for F16 weights)
 size_t mi_mmq_scratch_bytes(int type, int64_t K, int64_t ncols);
 void mi_mul_mat_mmq(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_q8 & act, const uint16_t * xh,

@@ -465,10 +465,14 @@ __global__ __launch_bounds__(256 * SK) void k_mmq3(const uint8_t * __restrict__ 
 // profiles/r03z_f16_pmc.txt.) The four partial tiles meet in LDS and are added in wave order.
 // Products of fp16 values are exact in f32; only the summation order differs from the reference's
 // ggml_vec_dot_f16 (~1e-7 relative).
-template <int PF, int NW>
+// F32X: the activations are the f32 src1 itself (columns of K contiguous floats, xcs floats apart),
+// rounded to f16 in the kernel as ggml_fp32_to_fp16_row does (RNE; ggml.c:605-616) right before
+// their MFMA -- no separate conversion launch (each column tile's activations are converted by every
+// row tile that reads them: VALU the memory-bound kernel has to spare)
+template <int PF, int NW, bool F32X = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmf16p(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                                    const uint16_t * __restrict__ xh, int64_t ncols, float * __restrict__ dst,
-                                                   size_t ycol) {
+                                                   size_t ycol, const float * __restrict__ xf = nullptr, int64_t xcs = 0) {
     constexpr int kRow = 72;  // halves per LDS row (64 + 8 pad)
     __shared__ __attribute__((aligned(16))) _Float16 lw[NW][32 * kRow];
     __shared__ __attribute__((aligned(16))) float red[NW][16][64];
@@ -484,19 +488,43 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmf16p(const uint8
 #pragma unroll
     for (int q = 0; q < 4; q++) wq[q] = W + std::min<int64_t>(n0 + lr + 8 * q, N - 1) * nb01 + (size_t) (w * kw) * 2 + 16 * lp;
     const int64_t col = std::min<int64_t>(c0 + r, ncols - 1);
-    const uint16_t * xc = xh + ((size_t) (w * kw / 16) * ncols + col) * 16 + 8 * h;
+    const uint16_t * xc = F32X ? nullptr : xh + ((size_t) (w * kw / 16) * ncols + col) * 16 + 8 * h;
+    const float * xfc = F32X ? xf + col * xcs + w * kw + 8 * h : nullptr;
     const size_t xstep = (size_t) ncols * 16;  // halves per 16-deep K step
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // (a HIP uint4 array is not promoted to registers)
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
     struct Chunk {
         u32x4 wv[4];
-        u32x4 xv[4];
+        u32x4 xv[F32X ? 0 : 4];
+        f32x4 xw[F32X ? 8 : 0];  // F32X: the 8 floats of each 16-deep step's lane half
     };
     auto load = [&](Chunk & c, int i) {
         i = i < nch ? i : nch - 1;  // past the end: a harmless re-read of the last chunk
 #pragma unroll
         for (int q = 0; q < 4; q++) c.wv[q] = *(const u32x4 *) (wq[q] + (size_t) i * 128);
+        if constexpr (F32X) {
 #pragma unroll
-        for (int st = 0; st < 4; st++) c.xv[st] = *(const u32x4 *) (xc + ((size_t) i * 4 + st) * xstep);
+            for (int st = 0; st < 4; st++) {
+                c.xw[2 * st] = *(const f32x4 *) (xfc + (size_t) i * 64 + 16 * st);
+                c.xw[2 * st + 1] = *(const f32x4 *) (xfc + (size_t) i * 64 + 16 * st + 4);
+            }
+        } else {
+#pragma unroll
+            for (int st = 0; st < 4; st++) c.xv[st] = *(const u32x4 *) (xc + ((size_t) i * 4 + st) * xstep);
+        }
+    };
+    auto xop = [&](const Chunk & c, int st) -> half8 {
+        if constexpr (F32X) {
+            half8 v;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                v[e] = (_Float16) c.xw[2 * st][e];
+                v[4 + e] = (_Float16) c.xw[2 * st + 1][e];
+            }
+            return v;
+        } else {
+            return __builtin_bit_cast(half8, c.xv[st]);
+        }
     };
     _Float16 * tile = lw[w];
     Chunk ring[PF];
@@ -510,7 +538,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmf16p(const uint8
 #pragma unroll
         for (int st = 0; st < 4; st++) {
             const half8 a = *(const half8 *) (tile + r * kRow + 16 * st + 8 * h);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, __builtin_bit_cast(half8, c.xv[st]), acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, xop(c, st), acc, 0, 0, 0);
         }
         load(c, i + PF);
     };
@@ -561,6 +589,21 @@ void mi_mul_mat_f16p(const void * W, size_t nb01, int64_t K, int64_t N, const ui
     const bool w8 = K % 512 == 0 && tiles < 512 && (g_mi_tuning.mmq_variant & (1 << 20)) != 0;
     if (w8) hipLaunchKernelGGL((k_mmf16p<3, 8>), dim3((unsigned) tiles), dim3(512), 0, s, (const uint8_t *) W, nb01, K, N, xh, ncols, dst, ycol);
     else hipLaunchKernelGGL((k_mmf16p<3, 4>), dim3((unsigned) tiles), dim3(256), 0, s, (const uint8_t *) W, nb01, K, N, xh, ncols, dst, ycol);
+}
+
+bool mi_mmf16p_f32_supported(int64_t K, int64_t N, size_t nb01, int64_t ncols, size_t ycol, const void * x, size_t xnb1) {
+    // opt-in (variant bit 2^17): measured SLOWER than the separate conversion launch + k_mmf16p
+    // (profiles/r04c_pf_f16.txt, 16 rotated weights: B=64 23.3 vs 17.3 us, B=32 22.9 vs 17.2 us) --
+    // every row tile re-reads and re-converts its columns' f32 (twice the bytes of f16, 128 row tiles)
+    return mi_mmf16p_supported(K, N, nb01, ncols, ycol) && ((uintptr_t) x % 16) == 0 && xnb1 % 16 == 0 &&
+           (g_mi_tuning.mmq_variant & (1 << 17)) != 0;
+}
+
+void mi_mul_mat_f16p_f32(const void * W, size_t nb01, int64_t K, int64_t N, const float * x, size_t xnb1, int64_t ncols, float * dst,
+                         size_t ycol, hipStream_t s) {
+    const int64_t tiles = ((N + 31) / 32) * ((ncols + 31) / 32);
+    hipLaunchKernelGGL((k_mmf16p<2, 4, true>), dim3((unsigned) tiles), dim3(256), 0, s, (const uint8_t *) W, nb01, K, N, nullptr, ncols,
+                       dst, ycol, x, (int64_t) (xnb1 / sizeof(float)));
 }
 
 bool mi_mmq_wants_blocked() { return (g_mi_tuning.mmq_variant & 1) == 0; }

@@ -1418,7 +1418,48 @@ __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
     const uint32_t woff = (uint32_t) (XB + UB + DB + (32 * rw + r) * F::BS);
     f32x16 y = f32x16(-0.0f), gsum = {};
 
-    auto compute = [&](int buf, int sb) {
+    // The combine of a superblock reads its accumulators and its scales / U halves / mins from the
+    // LDS buffer it was computed from (still intact during the next step: a buffer is restaged only
+    // at the end of the step after its own). comb_slice does accumulator elements 2 j, 2 j + 1.
+    struct Comb {
+        f32x16 Uv, tv;
+        float dw, dm;
+    };
+    auto comb_begin = [&](int buf, Comb & c) {
+        const char * base = lds + buf * SB;
+        const uint4 hdr = *(const uint4 *) (base + woff);
+        c.dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF));
+        c.dm = mi_h2f((uint16_t) (hdr.x >> 16));
+        const uint32_t ma = hdr.z & 0x3F3F3F3Fu;
+        const uint32_t mb = ((hdr.w >> 4) & 0x0F0F0F0Fu) | ((hdr.z >> 2) & 0x30303030u);
+        const uint32_t mw = h ? mb : ma;
+        half8 mu;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t m = (mw >> (8 * q)) & 0xFF;
+            mu[2 * q] = (_Float16) (float) m;
+            mu[2 * q + 1] = (_Float16) (float) (64 * m);
+        }
+        const half8 xu = *(const half8 *) (base + XB + xoff);
+        // U on the f16 MFMA: A = [S & 63, S >> 6] of the lane's column, B = [m, 64 m] of its row
+        c.Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
+    };
+    auto comb_slice = [&](int buf, const i32x16 (&acc)[NP], Comb & c, int j) {
+        const float * dal = (const float *) (lds + buf * SB + XB + UB) + 32 * cw;
+        const float2 d2 = *(const float2 *) &dal[8 * (j >> 1) + 4 * h + 2 * (j & 1)];
+        const float dav[2] = {d2.x, d2.y};
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int el = 2 * j + e;
+            int T = acc[NP - 1][el];
+#pragma unroll
+            for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
+            c.tv[el] = mmqx_term(T, c.Uv[el], c.dw, c.dm, dav[e]);
+        }
+    };
+    // superblock sb's MFMAs into acc from LDS buffer buf; `hook(kk)` runs after step kk's MFMAs (the
+    // deferred combine of the previous superblock interleaves there)
+    auto mfma_sb = [&](int buf, i32x16 (&acc)[NP], auto && hook) {
         const char * base = lds + buf * SB;
         const char * wr = base + woff;
         const uint4 hdr = *(const uint4 *) wr;
@@ -1426,14 +1467,9 @@ __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
 #pragma unroll
         for (int p = 0; p < 4; p++) q4[p] = *(const uint4 *) (wr + kQs + 32 * p + 16 * h);
         if constexpr (F::Q5) qh = *(const uint4 *) (wr + 16 + 16 * h);
-        const uint32_t w0 = hdr.y, w1 = hdr.z, w2 = hdr.w;
+        const uint32_t w0 = hdr.y, w2 = hdr.w;
         const uint32_t sca = w0 & 0x3F3F3F3Fu;
         const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
-        const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
-        const uint32_t ma = w1 & 0x3F3F3F3Fu;
-        const uint32_t mb = ((w2 >> 4) & 0x0F0F0F0Fu) | ((w1 >> 2) & 0x30303030u);
-        const uint32_t mw = h ? mb : ma;
-        i32x16 acc[NP];
         uint32_t lo[4], hi[4];
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) {
@@ -1463,37 +1499,84 @@ __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
                 const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
                 acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa, b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
             }
+            hook(kk);
         }
-        // U on the f16 MFMA: A = [S & 63, S >> 6] of the lane's column, B = [m, 64 m] of its row
-        half8 mu;
+    };
+    auto compute = [&](int buf, int sb) {
+        i32x16 acc[NP];
+        mfma_sb(buf, acc, [](int) {});
+        Comb c;
+        comb_begin(buf, c);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t m = (mw >> (8 * q)) & 0xFF;
-            mu[2 * q] = (_Float16) (float) m;
-            mu[2 * q + 1] = (_Float16) (float) (64 * m);
-        }
-        const half8 xu = *(const half8 *) (base + XB + xoff);
-        const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
-        const float * dal = (const float *) (base + XB + UB) + 32 * cw;
-        f32x16 tv;
+        for (int j = 0; j < 8; j++) comb_slice(buf, acc, c, j);
+        cfold_vec(gsum, y, c.tv, sb, gs, S);
+    };
+    // deferred: superblock sb's MFMAs with the combine of sb - 1 (accumulators accp, buffer buf ^ 1)
+    // interleaved, one pair of elements per 32-deep step; returns with sb's accumulators in accc
+    auto compute_defer = [&](int buf, int sb, i32x16 (&accc)[NP], const i32x16 (&accp)[NP], bool prev) {
+        Comb c;
+        if (prev) comb_begin(buf ^ 1, c);
+        mfma_sb(buf, accc, [&](int kk) {
+            if (prev) comb_slice(buf ^ 1, accp, c, kk);
+        });
+        if (prev) cfold_vec(gsum, y, c.tv, sb - 1, gs, S);
+    };
+    auto finish_defer = [&](int buf, int sb, const i32x16 (&accp)[NP]) {
+        Comb c;
+        comb_begin(buf, c);
 #pragma unroll
-        for (int g4 = 0; g4 < 4; g4++) {
-            const float4 d4 = *(const float4 *) &dal[8 * g4 + 4 * h];
-            const float dav[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int el = 4 * g4 + e;
-                int T = acc[NP - 1][el];
-#pragma unroll
-                for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
-                tv[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
-            }
-        }
-        cfold_vec(gsum, y, tv, sb, gs, S);
+        for (int j = 0; j < 8; j++) comb_slice(buf, accp, c, j);
+        cfold_vec(gsum, y, c.tv, sb, gs, S);
     };
 
     Stg st0, st1;  // (two variables, not an array: a register pair the unrolled steps alternate)
-    static_assert(CH % 2 == 0, "staging registers alternate");
+    static_assert(CH % 2 == 0 || CH == -1, "staging registers alternate");
+    if constexpr (CH == -1) {
+        // rolled + deferred combine: superblock sb's combine runs under sb + 1's MFMAs (two
+        // accumulator sets, alternating with the step parity). The buffer a deferred combine reads
+        // (sb's) is restaged only at the end of step sb + 1, after the combine.
+        i32x16 acc0[NP], acc1[NP];
+        stage_load(st0, 0);
+        stage_load(st1, 1);
+        stage_store(st0, 0);
+        mi_lds_barrier();
+        // superblock 0 (no previous), then pairs (odd, even) so every slot index is static
+        stage_load(st0, 2);
+        compute_defer(0, 0, acc0, acc1, false);
+        stage_store(st1, 1);
+        mi_lds_barrier();
+        for (int sb = 1; sb < S - 1; sb += 2) {
+            stage_load(st1, sb + 2);
+            compute_defer(1, sb, acc1, acc0, true);
+            stage_store(st0, 0);
+            mi_lds_barrier();
+            stage_load(st0, sb + 3);
+            compute_defer(0, sb + 1, acc0, acc1, true);
+            stage_store(st1, 1);
+            mi_lds_barrier();
+        }
+        // S even: the last superblock S - 1 is odd (buffer 1)
+        compute_defer(1, S - 1, acc1, acc0, true);
+        finish_defer(1, S - 1, acc1);
+    } else if constexpr (CH == 0) {
+        // rolled: two steps per iteration, no branch in the body (S even, host-checked; requests
+        // past the end are clamped re-reads), so the compiler's vmcnt bookkeeping across the back
+        // edge stays exact and the code stays small
+        stage_load(st0, 0);
+        stage_load(st1, 1);
+        stage_store(st0, 0);
+        mi_lds_barrier();
+        for (int sb = 0; sb < S; sb += 2) {
+            stage_load(st0, sb + 2);
+            compute(0, sb);
+            stage_store(st1, 1);
+            mi_lds_barrier();
+            stage_load(st1, sb + 3);
+            compute(1, sb + 1);
+            stage_store(st0, 0);
+            mi_lds_barrier();
+        }
+    } else
     for (int c0k = 0; c0k < S; c0k += CH) {
         // chunk prologue: superblocks c0k, c0k + 1 requested, the first stored
         stage_load(st0, c0k);
@@ -2372,10 +2455,19 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         else hipLaunchKernelGGL((k_mmqr<13, 1, 16>), gridr, dim3(512), 0, s, g);
         return;
     }
-    if (g_mi_tuning.mmq_long == 3) {  // + shared operands staged once per workgroup in LDS
+    if (g_mi_tuning.mmq_long >= 3) {  // + shared operands staged in LDS (4: rolled loop, 5: + deferred combine)
         const dim3 gridr((unsigned) mmx_deal(g, 128, 64));
-        if (type == 12) hipLaunchKernelGGL((k_mmqs<12, 16>), gridr, dim3(512), 0, s, g);
-        else hipLaunchKernelGGL((k_mmqs<13, 16>), gridr, dim3(512), 0, s, g);
+        const bool rolled = g_mi_tuning.mmq_long >= 4 && (K / 256) % 2 == 0;
+        if (rolled && g_mi_tuning.mmq_long == 5) {
+            if (type == 12) hipLaunchKernelGGL((k_mmqs<12, -1>), gridr, dim3(512), 0, s, g);
+            else hipLaunchKernelGGL((k_mmqs<13, -1>), gridr, dim3(512), 0, s, g);
+        } else if (rolled) {
+            if (type == 12) hipLaunchKernelGGL((k_mmqs<12, 0>), gridr, dim3(512), 0, s, g);
+            else hipLaunchKernelGGL((k_mmqs<13, 0>), gridr, dim3(512), 0, s, g);
+        } else {
+            if (type == 12) hipLaunchKernelGGL((k_mmqs<12, 16>), gridr, dim3(512), 0, s, g);
+            else hipLaunchKernelGGL((k_mmqs<13, 16>), gridr, dim3(512), 0, s, g);
+        }
         return;
     }
     const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));

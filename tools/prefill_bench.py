@@ -17,11 +17,15 @@ VARS = [int(v) for v in os.environ.get("MMQ_VARIANTS", "0").split(",")]
 # PF_LONG: mmq_long settings to compare (Q4_K / Q5_K past 128 columns: 1 k_mmqw, 2 k_mmqr)
 LONGS = [int(v) for v in os.environ.get("PF_LONG", "0").split(",")]
 VARS = [(v, l) for v in VARS for l in LONGS]
+# PF_MMV_BLOCKS: decode GEMV grid targets to compare (0 = automatic)
+BLOCKS = [int(v) for v in os.environ.get("PF_MMV_BLOCKS", "0").split(",")]
+VARS = [(v, l, b) for (v, l) in VARS for b in BLOCKS]
 for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
     for B in Bs:
-      for var, lng in VARS:
+      for var, lng, blk in VARS:
         lib.ggml_backend_mi355x_set_tuning(b"mmq_variant", var)
         lib.ggml_backend_mi355x_set_tuning(b"mmq_long", lng)
+        lib.ggml_backend_mi355x_set_tuning(b"mmv_blocks", blk)
         t = bench.TYPE_NAMES[tname]
         R = int(os.environ.get("PF_R", "8"))  # weight copies per step (36 x 9.4 MB > the 256 MB Infinity Cache)
         wl = bench.MulMatWorkload(lib, be, t, 4096, 4096, B, R)
@@ -40,7 +44,7 @@ for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
         y = G.tensor_get(lib, wl.y[0])
         ref = refs.setdefault((tname, B), y)
         same = "bit-equal to the first variant" if np.array_equal(y.view(np.uint32), ref.view(np.uint32)) else "DIFFERS from the first variant"
-        print(f"{tname:5s} B={B:4d} var={var:5d} long={lng} R={R}: {ms * 1e3 / R:8.2f} us/mul_mat in a graph of {R}  {2 * 4096 * 4096 * B * R / (ms / 1e3) / 1e12:7.1f} TFLOP/s  "
+        print(f"{tname:5s} B={B:4d} var={var:5d} long={lng} blocks={blk} R={R}: {ms * 1e3 / R:8.2f} us/mul_mat in a graph of {R}  {2 * 4096 * 4096 * B * R / (ms / 1e3) / 1e12:7.1f} TFLOP/s  "
               f"| one per graph {ms1 * 1e3:8.2f} us  {same}")
         wl.free()
 lib.ggml_backend_free(be)
