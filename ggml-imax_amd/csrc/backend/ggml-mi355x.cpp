@@ -449,6 +449,11 @@ struct mi_backend_ctx {
         int launches = 0;
         bool no_update = false;  // hipGraphExecUpdate refused once: replay-only
     };
+    // per-node timer (the reference's GGML_PERF, ggml.c:19195-19205): HIP events around every
+    // dispatch unit of a directly launched graph; see ggml_backend_mi355x_set_perf
+    bool perf = getenv("GGML_MI355X_PERF") != nullptr;
+    std::vector<hipEvent_t> perf_ev;   // pool
+    std::vector<int> perf_at;          // node index at which unit k starts
     std::vector<gcache_entry> gcache;
     uint64_t gclock = 0;
     std::unordered_map<uint64_t, int> topo_launches;  // kernel launches of a topology's last direct run
@@ -1995,7 +2000,59 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
 
 static bool graphs_enabled(const mi_backend_ctx * ctx) {
     static const bool env_no_graphs = getenv("GGML_MI355X_DISABLE_GRAPHS") != nullptr;
-    return ctx->graphs && !env_no_graphs;
+    return ctx->graphs && !env_no_graphs && !ctx->perf;  // the per-node timer needs direct launches
+}
+
+// ---- per-node timer ----------------------------------------------------------------------------
+// A dispatch unit is one pass of mi_graph_launch_nodes' loop: a node, or a fused chain of nodes
+// run by one kernel. perf_mark records an event before each unit; perf_finish records the end,
+// waits for the stream and adds each unit's device time to the perf fields of its last node (the
+// other nodes of a fused chain get a run with no time, as the reference's fused-away work would),
+// and the whole graph's to the cgraph's (ggml.c:19907-19922). ggml_graph_print shows them.
+static bool perf_active(const mi_backend_ctx * ctx) {
+    if (!ctx->perf) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    MI_CHECK(hipStreamIsCapturing(ctx->stream, &cs));
+    return cs == hipStreamCaptureStatusNone;
+}
+
+static void perf_mark(mi_backend_ctx * ctx, int i) {
+    const size_t k = ctx->perf_at.size();
+    if (k == ctx->perf_ev.size()) {
+        hipEvent_t e;
+        MI_CHECK(hipEventCreate(&e));
+        ctx->perf_ev.push_back(e);
+    }
+    MI_CHECK(hipEventRecord(ctx->perf_ev[k], ctx->stream));
+    ctx->perf_at.push_back(i);
+}
+
+static void perf_finish(mi_backend_ctx * ctx, ggml_cgraph * g, int64_t t_host0) {
+    const size_t n = ctx->perf_at.size();
+    perf_mark(ctx, g->n_nodes);
+    MI_CHECK(hipEventSynchronize(ctx->perf_ev[n]));
+    for (size_t k = 0; k < n; k++) {
+        float ms = 0.0f;
+        MI_CHECK(hipEventElapsedTime(&ms, ctx->perf_ev[k], ctx->perf_ev[k + 1]));
+        const int lo = ctx->perf_at[k], hi = ctx->perf_at[k + 1];
+        int last = -1;
+        for (int j = lo; j < hi; j++) {
+            if (is_noop(g->nodes[j])) continue;
+            g->nodes[j]->perf_runs++;
+            last = j;
+        }
+        if (last >= 0) {
+            const int64_t us = (int64_t) llround(ms * 1000.0);
+            g->nodes[last]->perf_time_us += us;
+            g->nodes[last]->perf_cycles += us;  // (device time: no CPU cycles; microseconds here)
+        }
+    }
+    float total = 0.0f;
+    if (n) MI_CHECK(hipEventElapsedTime(&total, ctx->perf_ev[0], ctx->perf_ev[n]));
+    g->perf_runs++;
+    g->perf_time_us += (int64_t) llround(total * 1000.0);
+    g->perf_cycles += ggml_time_us() - t_host0;  // host wall time of the call, microseconds
+    ctx->perf_at.clear();
 }
 
 // a graph that can be captured: no split-buffer mul_mat (several streams, events, peer copies)
@@ -2370,8 +2427,12 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
     }
     tl_absorbed = &absorbed_nodes;
     size_t next_attn = 0;
+    const bool perf = perf_active(ctx);
+    const int64_t perf_t0 = perf ? ggml_time_us() : 0;
+    ctx->perf_at.clear();
     for (int i = 0; i < cgraph->n_nodes; i++) {
         ggml_tensor * node = cgraph->nodes[i];
+        if (perf && !is_noop(node)) perf_mark(ctx, i);
         if (absorbed(i) && q_copy_bytes) {
             for (const auto & pl : attn) {
                 if (pl.q_copy_at != i) continue;
@@ -2455,6 +2516,7 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
         fprintf(stderr, "%s: kernel launch failed: %s\n", __func__, hipGetErrorString(err));
         return GGML_STATUS_FAILED;
     }
+    if (perf) perf_finish(ctx, cgraph, perf_t0);
     return GGML_STATUS_SUCCESS;
 }
 
@@ -2479,6 +2541,7 @@ static void mi_backend_free(ggml_backend_t backend) {
         for (auto & t : ctx->rope_tables) MI_CHECK(hipFree(t.dev));
         if (ctx->plan_marker) MI_CHECK(hipEventDestroy(ctx->plan_marker));
         if (ctx->split_ready) MI_CHECK(hipEventDestroy(ctx->split_ready));
+        for (hipEvent_t e : ctx->perf_ev) MI_CHECK(hipEventDestroy(e));
         MI_CHECK(hipStreamDestroy(ctx->stream));
     }
     delete ctx;
@@ -2713,6 +2776,11 @@ void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable) 
     auto * ctx = (mi_backend_ctx *) backend->context;
     ctx->graphs = enable;
     ctx->graph_fail_streak = 0;
+}
+
+void ggml_backend_mi355x_set_perf(ggml_backend_t backend, bool enable) {
+    MI_ASSERT(ggml_backend_is_mi355x(backend));
+    ((mi_backend_ctx *) backend->context)->perf = enable;
 }
 
 void ggml_backend_mi355x_graph_stats(ggml_backend_t backend, int64_t * stats4) {

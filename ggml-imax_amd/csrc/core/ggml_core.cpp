@@ -10,6 +10,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdarg>
+#include <cinttypes>
 #include <cstring>
 #include <ctime>
 #include <execinfo.h>
@@ -869,6 +870,35 @@ void ggml_graph_clear(struct ggml_cgraph * cgraph) {
     cgraph->n_leafs = 0;
     cgraph->n_nodes = 0;
     memset(cgraph->visited_hash_table.keys, 0, cgraph->visited_hash_table.size * sizeof(ggml_tensor *));
+}
+
+// src/ggml.c:20421-20462: the nodes with their perf counters (filled by a backend's per-node timer,
+// e.g. ggml_backend_mi355x_set_perf: perf_cycles then holds microseconds, so both columns read ms),
+// the leafs, and the time per op
+void ggml_graph_print(const struct ggml_cgraph * cgraph) {
+    int64_t per_op_us[GGML_OP_COUNT] = {0};
+    printf("=== GRAPH ===\n");
+    printf("n_nodes = %d\n", cgraph->n_nodes);
+    for (int i = 0; i < cgraph->n_nodes; i++) {
+        const ggml_tensor * node = cgraph->nodes[i];
+        per_op_us[node->op] += std::max<int64_t>(1, node->perf_time_us);
+        const double runs = node->perf_runs ? (double) node->perf_runs : 1.0;
+        printf(" - %3d: [ %5" PRId64 ", %5" PRId64 ", %5" PRId64 "] %16s %s (%3d) cpu = %7.3f / %7.3f ms, wall = %7.3f / %7.3f ms\n", i,
+               node->ne[0], node->ne[1], node->ne[2], ggml_op_name(node->op), (node->flags & GGML_TENSOR_FLAG_PARAM) ? "x" : node->grad ? "g" : " ",
+               node->perf_runs, (double) node->perf_cycles / 1000.0, (double) node->perf_cycles / 1000.0 / runs,
+               (double) node->perf_time_us / 1000.0, (double) node->perf_time_us / 1000.0 / runs);
+    }
+    printf("n_leafs = %d\n", cgraph->n_leafs);
+    for (int i = 0; i < cgraph->n_leafs; i++) {
+        const ggml_tensor * node = cgraph->leafs[i];
+        printf(" - %3d: [ %5" PRId64 ", %5" PRId64 "] %8s %16s\n", i, node->ne[0], node->ne[1], ggml_op_name(node->op), node->name);
+    }
+    for (int i = 0; i < GGML_OP_COUNT; i++) {
+        if (per_op_us[i] == 0) continue;
+        printf("perf_total_per_op_us[%16s] = %7.3f ms\n", ggml_op_name((ggml_op) i), (double) per_op_us[i] / 1000.0);
+    }
+    printf("========================================\n");
+    fflush(stdout);
 }
 
 } // extern "C"

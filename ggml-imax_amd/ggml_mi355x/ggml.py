@@ -118,6 +118,7 @@ _SIGS = {
     "ggml_new_graph": ([c_void_p], POINTER(ggml_cgraph)),
     "ggml_new_graph_custom": ([c_void_p, c_size_t, c_bool], POINTER(ggml_cgraph)),
     "ggml_build_forward_expand": ([POINTER(ggml_cgraph), T], None),
+    "ggml_graph_print": ([POINTER(ggml_cgraph)], None),
     "ggml_quantize_chunk": ([c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p], c_size_t),
     "ggml_fp32_to_fp16": ([c_float], ctypes.c_uint16),
     "ggml_fp16_to_fp32": ([ctypes.c_uint16], c_float),
@@ -236,6 +237,7 @@ _SIGS = {
     "ggml_backend_mi355x_last_launch_count": ([c_void_p], c_int),
     "ggml_backend_mi355x_set_tuning": ([c_char_p, c_int], c_bool),
     "ggml_backend_mi355x_set_graph_capture": ([c_void_p, c_bool], None),
+    "ggml_backend_mi355x_set_perf": ([c_void_p, c_bool], None),
     "ggml_backend_mi355x_graph_stats": ([c_void_p, c_void_p], None),
     "ggml_backend_mi355x_graph_stats_ex": ([c_void_p, c_void_p, c_int], c_int),
     "ggml_backend_mi355x_quantize_activations": ([c_void_p, c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p], c_bool),

@@ -63,6 +63,13 @@ GGML_API int ggml_backend_mi355x_last_launch_count(ggml_backend_t backend);
 // hipGraphLaunch. GGML_MI355X_DISABLE_GRAPHS=1 (process-wide, as GGML_CUDA_DISABLE_GRAPHS,
 // ggml-cuda.cu:2462) or set_graph_capture(false) makes both launch directly.
 GGML_API void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable);
+// Per-node timer, the reference's GGML_PERF (ggml.c:19195-19205, :19907-19922) for this backend:
+// with it on (or GGML_MI355X_PERF set), graphs launch directly and every node's device time is
+// measured with HIP events around the kernel that computes it; node->perf_runs / perf_time_us (and
+// perf_cycles, in microseconds) and the cgraph's totals accumulate as the reference's CPU executor
+// fills them, and ggml_graph_print() prints them. A fused chain's time goes to its last node, the
+// others get runs without time. Timing synchronizes the stream once per graph.
+GGML_API void ggml_backend_mi355x_set_perf(ggml_backend_t backend, bool enable);
 // counters since init: [0] captures (plans and graph_compute), [1] graph instantiations,
 // [2] in-place updates, [3] direct (uncaptured) computes
 GGML_API void ggml_backend_mi355x_graph_stats(ggml_backend_t backend, int64_t * stats4);

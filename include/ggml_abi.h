@@ -355,6 +355,7 @@ GGML_API void   ggml_build_forward_expand(struct ggml_cgraph * cgraph, struct gg
 GGML_API struct ggml_tensor * ggml_graph_get_tensor(struct ggml_cgraph * cgraph, const char * name);
 GGML_API struct ggml_cgraph ggml_graph_view(struct ggml_cgraph * cgraph, int i0, int i1);
 GGML_API void   ggml_graph_clear(struct ggml_cgraph * cgraph);
+GGML_API void   ggml_graph_print(const struct ggml_cgraph * cgraph);  // ggml.h:2030
 
 // quantization (ggml.h:2233-2254): imatrix == NULL reference path for the path's types
 GGML_API void   ggml_quantize_init(enum ggml_type type);

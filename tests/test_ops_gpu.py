@@ -424,3 +424,48 @@ def test_attention_projection_fused(libs, consumer, n_past):
     assert n_fast < n_ord if consumer == "ln_fc" else n_fast <= n_ord
     # reference order: the unfused kernels, bit for bit
     assert_exact(o_1, o_r, "residual stream, reference order")
+
+
+# ---- per-node timer (the reference's GGML_PERF, ggml.c:19195-19205) --------------------------------
+
+@pytest.mark.gpu
+def test_per_node_timer_fills_perf_fields(capfd):
+    """ggml_backend_mi355x_set_perf: every computed node of a graph gets perf_runs per compute and
+    device microseconds (a fused chain's time on its last node); the node times add up to at most
+    the graph's; ggml_graph_print prints the reference's table."""
+    import ctypes
+    lib = G.runtime()
+    be = G.mi355x_backend(lib)
+    try:
+        lib.ggml_backend_mi355x_set_perf(be, True)
+        K, N, B = 4096, 4096, 4
+        overhead = lib.ggml_tensor_overhead() * 16 + lib.ggml_graph_overhead()
+        with G.Context(lib, overhead, no_alloc=True) as c:
+            w = lib.ggml_new_tensor_2d(c.ctx, G.GGML_TYPE_F16, K, N)
+            x = lib.ggml_new_tensor_2d(c.ctx, G.GGML_TYPE_F32, K, B)
+            y = lib.ggml_mul_mat(c.ctx, w, x)
+            z = lib.ggml_scale(c.ctx, y, 0.5)
+            out = lib.ggml_soft_max(c.ctx, z)
+            g = lib.ggml_new_graph(c.ctx)
+            lib.ggml_build_forward_expand(g, out)
+            buf = lib.ggml_backend_alloc_ctx_tensors(c.ctx, be)
+            try:
+                G.tensor_set(lib, w, (np.random.default_rng(1).standard_normal(K * N) * 0.01).astype(np.float16))
+                G.tensor_set(lib, x, np.random.default_rng(2).standard_normal(K * B).astype(np.float32))
+                for _ in range(3):
+                    assert lib.ggml_backend_graph_compute(be, g) == G.GGML_STATUS_SUCCESS
+                gc = g.contents
+                nodes = [gc.nodes[i].contents for i in range(gc.n_nodes)]
+                assert all(n.perf_runs == 3 for n in nodes), [n.perf_runs for n in nodes]
+                mm = [n for n in nodes if n.op == G.GGML_OP_MUL_MAT][0]
+                assert mm.perf_time_us > 0
+                assert gc.perf_runs == 3
+                assert sum(n.perf_time_us for n in nodes) <= gc.perf_time_us + len(nodes)
+                lib.ggml_graph_print(g)
+            finally:
+                lib.ggml_backend_buffer_free(buf)
+        printed = capfd.readouterr().out
+        assert "=== GRAPH ===" in printed and "MUL_MAT" in printed and "perf_total_per_op_us" in printed
+    finally:
+        lib.ggml_backend_mi355x_set_perf(be, False)
+        lib.ggml_backend_free(be)
