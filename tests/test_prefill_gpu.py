@@ -154,13 +154,20 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
         variants = [0, 16, 128, 128 | 65536, 128 | (1 << 24), 128 | (1 << 25)]
     else:
         variants = [0, 2048, 1 << 27, 128 | 131072, 128 | 65536, 128 | 131072 | (1 << 28)] + ([1 << 21] if B <= 16 else [])
+    # long-prompt kernels forced onto these shapes (variant bits 128 | 131072, mmq_long): k_mmqw (1),
+    # k_mmqr (2, weights dequantized in registers), k_mmqs (3 chunked, 4 rolled, 5 deferred combine)
+    longs = [(128 | 131072, L) for L in (1, 2, 3, 4, 5)] if tname in ("q4_K", "q5_K") else []
     outs = {}
     try:
-        for v in variants:
-            assert rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", v)
+        for v in variants + longs:
+            vv, lng = v if isinstance(v, tuple) else (v, 0)
+            assert rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", vv)
+            assert rt.ggml_backend_mi355x_set_tuning(b"mmq_long", lng)
             outs[v] = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
     finally:
         rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", 0)
+        rt.ggml_backend_mi355x_set_tuning(b"mmq_long", 0)
+    variants = variants + longs
     ref = orc.mul_mat(t, wq, K, N, x, B)
     assert rel_err(outs[0], ref) <= EXACT_TOL
     for v in variants[1:]:

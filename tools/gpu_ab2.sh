@@ -9,5 +9,5 @@ for spec in "q4_K 4096 4096 32" "q4_0 4096 4096 36" "q4_K 4096 11008 14" "q5_K 4
   echo "== $1 ${2}x${3} R=$4" | tee -a $OUT/nt.txt
   timeout -k 10 120 python3 -u tools/mmv_tune.py --variants 0:0,100:0 --rounds 9 --type $1 --K $2 --N $3 --rotate $4 2>&1 | grep -v amdgpu.ids | tee -a $OUT/nt.txt
 done
-timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py tests/test_llama_block_gpu.py -x -v --timeout 200 --timeout-method thread -m gpu -k "per_node or llama" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py tests/test_llama_block_gpu.py tests/test_prefill_gpu.py -x -v --timeout 200 --timeout-method thread -m gpu -k "per_node or llama or bit_equal" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 grep -E "PASS|FAIL|T=|launches" $OUT/pytest.log | tail -12
