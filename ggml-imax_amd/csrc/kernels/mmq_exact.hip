@@ -68,22 +68,36 @@ __device__ __forceinline__ float mmqx_term(int T, float U, float dw, float dm, f
 // The canonical combine order of an output's superblock terms, shared by every kernel of this
 // file (so any column shard of a prompt gives the same bits whichever kernel computes it): the S
 // superblocks form kCfoldGroups contiguous groups of gs = ceil(S / kCfoldGroups) (the last ones
-// shorter or empty), each group's terms are left-folded (g = t_first; g = g + t; ...), then the
-// group sums are left-folded (y = g_0; y = y + g_1; ...). The pipelined kernel (k_mmqp) gives each
-// group to one of its waves.
+// shorter or empty), each group's terms are left-folded from -0 (g = -0; g = g + t; ...); the sums
+// of groups 0..3 and of groups 4..7 are left-folded separately from -0 (lo = lo + g_0 ...; hi = hi +
+// g_4 ...) and y = lo + hi. (-0 + x == x for every float x, signed zeros and NaNs included, so an
+// empty half changes nothing.) The pipelined kernel (k_mmqp) gives each group to one of its waves,
+// the split-K kernel (k_mmqt) each half to one wave of a pair.
 constexpr int kCfoldGroups = 8;
+constexpr int kCfoldHalf = kCfoldGroups / 2;  // first group of the high half
 __host__ __device__ constexpr int cfold_gs(int S) { return (S + kCfoldGroups - 1) / kCfoldGroups; }
-// term t of superblock sb (terms arrive in superblock order): g / y updated in place
-__device__ __forceinline__ void cfold(float & g, float & y, float t, int sb, int gs, int S) {
+// first superblock of the high half
+__host__ __device__ constexpr int cfold_split(int S) { return kCfoldHalf * cfold_gs(S) < S ? kCfoldHalf * cfold_gs(S) : S; }
+// Sequential form: term t of superblock sb (terms arrive in superblock order); g, y, lo updated in
+// place, y and lo starting at -0: y folds the current half, lo receives the low half's sum when the
+// high half's first group ends. The result is cfold_end(lo, y).
+__device__ __forceinline__ void cfold(float & g, float & y, float & lo, float t, int sb, int gs, int S) {
     const int pos = sb % gs;
     g = pos == 0 ? t : g + t;
-    if (pos == gs - 1 || sb == S - 1) y = sb < gs ? g : y + g;
+    if (pos == gs - 1 || sb == S - 1) {
+        if (sb / gs == kCfoldHalf) {
+            lo = y;
+            y = g;
+        } else {
+            y = y + g;
+        }
+    }
 }
-// the same for a whole accumulator (sb wave-uniform) without per-element selects: a group sum
-// starts at -0 (-0 + t == t for every float t, signed zeros and NaNs included), y starts at -0 too
-// (callers initialize it so); the resets are uniform branches kept as branches (the empty asm
-// stops their if-conversion into 16 v_cndmask per superblock)
-__device__ __forceinline__ void cfold_vec(f32x16 & g, f32x16 & y, const f32x16 & t, int sb, int gs, int S) {
+__device__ __forceinline__ float cfold_end(float lo, float y) { return lo + y; }
+// the same for a whole accumulator (sb wave-uniform) without per-element selects; the resets are
+// uniform branches kept as branches (the empty asm stops their if-conversion into 16 v_cndmask
+// per superblock)
+__device__ __forceinline__ void cfold_vec(f32x16 & g, f32x16 & y, f32x16 & lo, const f32x16 & t, int sb, int gs, int S) {
     const int pos = sb % gs;
     if (pos == 0) {
         asm volatile("" ::: "memory");
@@ -92,8 +106,42 @@ __device__ __forceinline__ void cfold_vec(f32x16 & g, f32x16 & y, const f32x16 &
     g = g + t;
     if (pos == gs - 1 || sb == S - 1) {
         asm volatile("" ::: "memory");
-        y = y + g;
+        if (sb / gs == kCfoldHalf) {
+            lo = y;
+            y = g;
+        } else {
+            y = y + g;
+        }
     }
+}
+// cfold_vec for kernels without 16 registers to spare: the low half's sum is parked by `park(y)`
+// (e.g. in the thread's own output locations) when the high half's first group ends; the result is
+// then unpark() + y if cfold_split(S) < S, else y
+template <typename Park>
+__device__ __forceinline__ void cfold_vec_park(f32x16 & g, f32x16 & y, const f32x16 & t, int sb, int gs, int S, Park && park) {
+    const int pos = sb % gs;
+    if (pos == 0) {
+        asm volatile("" ::: "memory");
+        g = f32x16(-0.0f);
+    }
+    g = g + t;
+    if (pos == gs - 1 || sb == S - 1) {
+        asm volatile("" ::: "memory");
+        if (sb / gs == kCfoldHalf) {
+            park(y);
+            y = g;
+        } else {
+            y = y + g;
+        }
+    }
+}
+// group sums v = 0 .. ngroups - 1 read by `at(v)`, folded canonically
+template <typename At>
+__device__ __forceinline__ float cfold_groups(int ngroups, At && at) {
+    float lo = -0.0f, hi = -0.0f;
+    for (int v = 0; v < ngroups && v < kCfoldHalf; v++) lo = lo + at(v);
+    for (int v = kCfoldHalf; v < ngroups; v++) hi = hi + at(v);
+    return lo + hi;
 }
 
 template <int TYPE>
@@ -460,6 +508,39 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
     };
 
     f32x16 y = f32x16(-0.0f), gsum = {};  // y = -0: cfold_vec's first group sum lands exactly
+    // the thread's output elements D[n][b]: column b = lane & 31 of this wave's 32, rows n = (reg & 3)
+    // + 8 (reg >> 2) + 4 (lane >> 5); also where the low half's sum is parked (no register to spare)
+    const int64_t bo = b0 + 32 * cw + r;
+    auto y_io = [&](f32x16 & v, bool st) {
+        if (bo >= ncols) return;
+        float * out = (float *) ((char *) dst + bo * ycol);
+#pragma unroll
+        for (int gq = 0; gq < 4; gq++) {
+            const int64_t n = n0 + 32 * rw + 8 * gq + 4 * h;
+            if (n + 3 < N) {
+                if (st) {
+                    *(float4 *) (out + n) = make_float4(v[4 * gq], v[4 * gq + 1], v[4 * gq + 2], v[4 * gq + 3]);
+                } else {
+                    const float4 t = *(const float4 *) (out + n);
+                    v[4 * gq] = t.x; v[4 * gq + 1] = t.y; v[4 * gq + 2] = t.z; v[4 * gq + 3] = t.w;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    if (n + e < N) {
+                        if (st) out[n + e] = v[4 * gq + e];
+                        else v[4 * gq + e] = out[n + e];
+                    }
+                }
+            }
+        }
+    };
+    auto park = [&](const f32x16 & v) {
+        if constexpr ((ABL & 8) == 0) {
+            f32x16 t = v;
+            y_io(t, true);
+        }
+    };
     const int gs = cfold_gs(S);
     // The raw weights of superblock sb + 1 are dequantized into LDS at the end of stage sb; they
     // were requested LEAD stages earlier (a ring of LEAD raw slots: HBM latency is several stage
@@ -540,8 +621,8 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
         if constexpr ((ABL & 2) != 0) {  // timing ablation: no combine
 #pragma unroll
             for (int i = 0; i < 16; i++) {
-                float gg = gsum[i], yy = y[i];
-                cfold(gg, yy, (float) acc[0][i], sb, gs, S);
+                float gg = gsum[i], yy = y[i], ll = -0.0f;  // (timing ablation: results invalid)
+                cfold(gg, yy, ll, (float) acc[0][i], sb, gs, S);
                 gsum[i] = gg;
                 y[i] = yy;
             }
@@ -572,7 +653,7 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
                     tv[i] = mmqx_term(T, Uv[i], dw[e], dm[e], da);
                 }
             }
-            cfold_vec(gsum, y, tv, sb, gs, S);
+            cfold_vec_park(gsum, y, tv, sb, gs, S, park);
         }
         stamp(4 + 4 * sb);
         mi_lds_barrier();
@@ -590,8 +671,6 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
         }
     }
 
-    // D[n][b]: column b = lane & 31 of this wave's 32, rows n = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
-    const int64_t b = b0 + 32 * cw + r;
     rstamp(1);
     if constexpr ((ABL & 8) != 0) {
         // dst holds the stamps; keep the results alive (an unlikely-value store) so nothing is
@@ -602,18 +681,12 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
         if (t == 1.2345e-30f) dst[4096 + threadIdx.x] = t;
         return;
     }
-    if (b >= ncols) return;
-    float * out = (float *) ((char *) dst + b * ycol);
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-        const int64_t n = n0 + 32 * rw + 8 * g + 4 * h;
-        if (n + 3 < N) {
-            *(float4 *) (out + n) = make_float4(y[4 * g], y[4 * g + 1], y[4 * g + 2], y[4 * g + 3]);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[4 * g + e];
-        }
+    if (cfold_split(S) < S) {  // cfold_end: the parked low half + the high half
+        f32x16 lo = {};
+        y_io(lo, false);
+        y = lo + y;
     }
+    y_io(y, true);
 }
 
 
@@ -785,6 +858,39 @@ __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
     rstamp(0);
     stamp(0);
     f32x16 y = f32x16(-0.0f), gsum = {};
+    // the thread's output elements D[n][b]: column b = lane & 31 of this wave's 32, rows n = (reg & 3)
+    // + 8 (reg >> 2) + 4 (lane >> 5); also where the low half's sum is parked (no register to spare)
+    const int64_t bo = b0 + 32 * cw + r;
+    auto y_io = [&](f32x16 & v, bool st) {
+        if (bo >= ncols) return;
+        float * out = (float *) ((char *) dst + bo * ycol);
+#pragma unroll
+        for (int gq = 0; gq < 4; gq++) {
+            const int64_t n = n0 + 32 * rw + 8 * gq + 4 * h;
+            if (n + 3 < N) {
+                if (st) {
+                    *(float4 *) (out + n) = make_float4(v[4 * gq], v[4 * gq + 1], v[4 * gq + 2], v[4 * gq + 3]);
+                } else {
+                    const float4 t = *(const float4 *) (out + n);
+                    v[4 * gq] = t.x; v[4 * gq + 1] = t.y; v[4 * gq + 2] = t.z; v[4 * gq + 3] = t.w;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    if (n + e < N) {
+                        if (st) out[n + e] = v[4 * gq + e];
+                        else v[4 * gq + e] = out[n + e];
+                    }
+                }
+            }
+        }
+    };
+    auto park = [&](const f32x16 & v) {
+        if constexpr ((ABL & 8) == 0) {
+            f32x16 t = v;
+            y_io(t, true);
+        }
+    };
     Xs xs;
     load_x(xs, 0);
     mi_lds_barrier();
@@ -845,7 +951,7 @@ __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
                 tv[i2] = mmqx_term(T, Uv[i2], dw[e], dm[e], da);
             }
         }
-        cfold_vec(gsum, y, tv, sb, gs, S);
+        cfold_vec_park(gsum, y, tv, sb, gs, S, park);
         stamp(4 + 4 * sb);
         mi_lds_barrier();
         stamp(5 + 4 * sb);
@@ -858,20 +964,12 @@ __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
         if (t == 1.2345e-30f) dst[4096 + threadIdx.x] = t;
         return;
     }
-
-    const int64_t b = b0 + 32 * cw + r;
-    if (b >= ncols) return;
-    float * out = (float *) ((char *) dst + b * ycol);
-#pragma unroll
-    for (int gq = 0; gq < 4; gq++) {
-        const int64_t n = n0 + 32 * rw + 8 * gq + 4 * h;
-        if (n + 3 < N) {
-            *(float4 *) (out + n) = make_float4(y[4 * gq], y[4 * gq + 1], y[4 * gq + 2], y[4 * gq + 3]);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; e++) if (n + e < N) out[n + e] = y[4 * gq + e];
-        }
+    if (cfold_split(S) < S) {  // cfold_end: the parked low half + the high half
+        f32x16 lo = {};
+        y_io(lo, false);
+        y = lo + y;
     }
+    y_io(y, true);
 }
 
 // ---- short prompts, pipelined: 8 waves per tile, one superblock group each -----------------------
@@ -1096,15 +1194,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
         }
     }
     mi_lds_barrier();
-    // the group sums left-folded (canonical order) by the whole workgroup: output o = el 64 + l
+    // the group sums folded (canonical order) by the whole workgroup: output o = el 64 + l
     // (el: accumulator element of tile el / 16, l: lane) -- lanes 0..31 store 32 consecutive rows
     const int ngroups = (S + gs - 1) / gs;
 #pragma unroll
     for (int i = 0; i < NE / NW; i++) {
         const int o = (int) threadIdx.x + 64 * NW * i;
         const int el = o >> 6, l = o & 63;
-        float y = red[el * 64 + l];
-        for (int v = 1; v < ngroups; v++) y = y + red[(v * NE + el) * 64 + l];
+        const float y = cfold_groups(ngroups, [&](int v) { return red[(v * NE + el) * 64 + l]; });
         const int e = el & 15, t = el >> 4;
         const int64_t n = n0 + (l & 31);
         const int64_t c = c0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
@@ -1112,219 +1209,23 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
     }
 }
 
-// ---- long prompts, weights dequantized in registers: k_mmqr ------------------------------------------
-// Why (k_mmqw's stage stamps, profiles/r03t_mmqw_stage_stamps.txt): with the weight planes staged
-// through LDS by loader waves, every MFMA wave runs [16 MFMAs | combine | barrier] in lock step with
-// the others, so the matrix pipe idles through the combine and the barrier (~60 % of a stage).
-// Here there is no workgroup barrier at all: each wave dequantizes its own 32 weight rows into the
-// MFMA operand registers (k_mmqp's step: the lane's own weight row is the B operand, plane factors
-// from two SWAR extractions of the scale bytes) and runs every superblock of K itself, so a wave's
-// instruction stream interleaves dequantization VALU, MFMAs and the previous superblock's combine,
-// and the two waves of a SIMD fill each other's gaps (MFMA and VALU are separate pipes).
-// Workgroup: 8 waves, tile 128 weight rows x 64 prompt columns; wave w computes rows 32 (w & 3)..
-// x columns 32 (w >> 2).. (one 32 x 32 accumulator per plane). Row tiles fastest in the grid, so
-// blocks b and b + 8 (one XCD under round-robin placement) share column tiles and an XCD's L2 holds
-// the weights of only nrt / 8 row tiles. Same operands and canonical combine (mmqx_term, cfold_vec
-// in superblock order) as every kernel of this file: bit-identical.
-// Loads (vmcnt retires in issue order, so waiting for one load waits for every older one): the
-// activation fragments of superblock s are requested XL superblocks ahead, step by step into the
-// registers their predecessors just freed; superblock s + RING's weights are requested at the END of
-// superblock s (RING = XL + 1 slots), i.e. after the activations it must not hold back. A wait for
-// the activations of s then forces only weights requested XL superblocks earlier: both operands get
-// XL superblocks of latency cover (XL = 1 measured latency-bound: 42.9 us at B = 512).
-template <int TYPE, int XL, int CH>
-__global__ __launch_bounds__(512, 2) void k_mmqr(mi_mmx_group grp) {
-    MI_MMX_MEMBER(grp);
-    using F = XFmt<TYPE>;
-    constexpr int NP = F::NP;
-    constexpr int RING = XL + 1;
-    __shared__ __attribute__((aligned(16))) float dal[8][32];  // per-wave da row
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane((int) threadIdx.x >> 6);
-    const int r = lane & 31, h = lane >> 5;
-    const int64_t ncols = act.ncols;
-    const int S = (int) (K / 256);
-    const int gs = cfold_gs(S);
-    const int64_t nrt = (N + 127) / 128;
-    const int64_t n0 = (mmx_tile % nrt) * 128 + 32 * (w & 3);
-    const int64_t c0 = (mmx_tile / nrt) * 64 + 32 * (w >> 2);
-    if (n0 >= N || c0 >= ncols) return;  // wave-uniform; no workgroup barrier below
-
-    const int nrows = (int) std::min<int64_t>(32, N - n0);
-    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc((void *) (W + n0 * nb01), (short) 0, (int) (nrows * nb01), 0x00020000);
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xq, (short) 0, (int) (K * ncols), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ures = __builtin_amdgcn_make_buffer_rsrc((void *) act.xu, (short) 0, (int) (S * ncols * 32), 0x00020000);
-    const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc((void *) act.xd, (short) 0, (int) (S * ncols * 4), 0x00020000);
-    constexpr uint32_t kQs = F::Q5 ? 48 : 16;
-    const uint32_t wv = (uint32_t) (min(r, nrows - 1) * nb01);
-    const uint32_t acol = (uint32_t) std::min<int64_t>(c0 + r, ncols - 1);
-    const uint32_t xstep = (uint32_t) ncols * 32;
-
-    auto ld = [](__amdgpu_buffer_rsrc_t res, uint32_t voff, uint32_t soff) -> uint4 {
-        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(res, voff, soff, 0));
-    };
-    struct Wt {
-        uint4 hdr, q4[4], qh;
-    };
-    auto load_w = [&](Wt & o, int sb) {
-        sb = min(sb, S - 1);  // clamped: past-the-end requests re-read the last superblock
-        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * F::BS);
-        o.hdr = ld(wres, wv, so);
-#pragma unroll
-        for (int p = 0; p < 4; p++) o.q4[p] = ld(wres, wv + kQs + 32 * p + 16 * h, so);
-        if constexpr (F::Q5) o.qh = ld(wres, wv + 16 + 16 * h, so);
-    };
-    auto ld_x = [&](int sb, int kk) -> i32x4 {
-        sb = min(sb, S - 1);
-        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane((sb * 8 + kk) * (int) xstep);
-        return __builtin_bit_cast(i32x4, ld(xres, acol * 32 + 16 * h, so));
-    };
-    auto ld_u = [&](int sb) -> half8 {
-        sb = min(sb, S - 1);
-        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * (int) ncols * 32);
-        return __builtin_bit_cast(half8, ld(ures, acol * 32 + 16 * h, so));
-    };
-    auto ld_d = [&](int sb) -> float {
-        sb = min(sb, S - 1);
-        const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(sb * (int) ncols * 4);
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dres, acol * 4, so, 0));
-    };
-
-    f32x16 y = f32x16(-0.0f), gsum = {};
-    Wt wt[RING];
-    i32x4 xa[XL][8];
-    half8 xu[XL];
-    float da[XL];
-    // superblock sb from slots (sb % RING, sb % XL), then the slots' refills: sb + XL's activations,
-    // sb + RING's weights. The loop runs whole unrolled rounds (every slot index static); the steps
-    // past S compute nothing but still issue their (clamped) requests, so every path through the
-    // body issues the same loads and the compiler's vmcnt bookkeeping stays exact (a load under a
-    // branch makes it drain at the join).
-    auto step = [&](Wt & cur, i32x4 (&xs)[8], half8 & xuc, float & dac, const int sb, const bool refill_x, const bool refill_w) {
-        if (sb < S) {  // wave-uniform
-            const uint32_t w0 = cur.hdr.y, w1 = cur.hdr.z, w2 = cur.hdr.w;
-            const uint32_t sca = w0 & 0x3F3F3F3Fu;
-            const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
-            const float dw = mi_h2f((uint16_t) (cur.hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (cur.hdr.x >> 16));
-            const uint32_t ma = w1 & 0x3F3F3F3Fu;
-            const uint32_t mb = ((w2 >> 4) & 0x0F0F0F0Fu) | ((w1 >> 2) & 0x30303030u);
-            const uint32_t mw = h ? mb : ma;
-            i32x16 acc[NP];
-            uint32_t lo[4], hi[4];
-#pragma unroll
-            for (int kk = 0; kk < 8; kk++) {
-                if ((kk & 1) == 0) {
-                    const uint4 q = cur.q4[kk >> 1];
-                    const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        lo[e] = qv[e] & 0x0F0F0F0Fu;
-                        hi[e] = (qv[e] >> 4) & 0x0F0F0F0Fu;
-                    }
-                }
-                uint32_t v[4];
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    v[e] = (kk & 1) ? hi[e] : lo[e];
-                    if constexpr (F::Q5) {
-                        const uint32_t hb[4] = {cur.qh.x, cur.qh.y, cur.qh.z, cur.qh.w};
-                        v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
-                    }
-                }
-                const uint32_t scw = kk < 4 ? sca : scb;
-#pragma unroll
-                for (int p = 0; p < NP; p++) {
-                    const uint32_t f = __builtin_amdgcn_ubfe(scw, 8 * (kk & 3) + (F::Q5 ? 2 * p : 3 * p), F::Q5 ? 2 : 3);
-                    const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
-                    acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xs[kk], b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
-                }
-            }
-            // U on the f16 MFMA: A = [S & 63, S >> 6] of the lane's column, B = [m, 64 m] of its row
-            half8 mu;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t m = (mw >> (8 * q)) & 0xFF;
-                mu[2 * q] = (_Float16) (float) m;
-                mu[2 * q + 1] = (_Float16) (float) (64 * m);
-            }
-            if (h == 0) dal[w][r] = dac;
-            __builtin_amdgcn_wave_barrier();
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xuc, mu, f32x16{}, 0, 0, 0);
-            f32x16 tv;
-#pragma unroll
-            for (int g4 = 0; g4 < 4; g4++) {
-                const float4 d4 = *(const float4 *) &dal[w][8 * g4 + 4 * h];
-                const float dav[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int el = 4 * g4 + e;
-                    int T = acc[NP - 1][el];
-#pragma unroll
-                    for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
-                    tv[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();  // the LDS row is rewritten by the next superblock
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            cfold_vec(gsum, y, tv, sb, gs, S);
-        }
-        if (refill_x) {
-#pragma unroll
-            for (int kk = 0; kk < 8; kk++) xs[kk] = ld_x(sb + XL, kk);
-            xuc = ld_u(sb + XL);
-            dac = ld_d(sb + XL);
-        }
-        if (refill_w) load_w(cur, sb + RING);  // after this superblock's activation requests (see above)
-    };
-    // K in chunks of CH superblocks (CH % (XL RING) == 0: every slot index static), each chunk
-    // straight-line code: a rolled loop carrying the ring across its back edge makes the compiler
-    // drain vmcnt at the loop header, so the ring refills at a chunk start instead (one load latency
-    // per CH superblocks; K = 4096 is one chunk). The sched barriers keep each superblock's
-    // instructions (and registers) inside its own step.
-    static_assert(CH % (XL * RING) == 0, "chunk of whole slot rounds");
-    for (int c0 = 0; c0 < S; c0 += CH) {
-#pragma unroll
-        for (int u = 0; u < XL; u++) {
-#pragma unroll
-            for (int kk = 0; kk < 8; kk++) xa[u][kk] = ld_x(c0 + u, kk);
-            xu[u] = ld_u(c0 + u);
-            da[u] = ld_d(c0 + u);
-        }
-#pragma unroll
-        for (int u = 0; u < RING; u++) load_w(wt[u], c0 + u);
-        __builtin_amdgcn_sched_barrier(0);  // (else the scheduler sinks these loads to their first use)
-#pragma unroll
-        for (int u = 0; u < CH; u++) {
-            step(wt[u % RING], xa[u % XL], xu[u % XL], da[u % XL], c0 + u, u + XL < CH, u + RING < CH);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    // accumulator element el: prompt column c0 + (el & 3) + 8 (el >> 2) + 4 h, weight row n0 + r
-    const int64_t n = n0 + r;
-    if (n >= N) return;
-#pragma unroll
-    for (int el = 0; el < 16; el++) {
-        const int64_t c = c0 + (el & 3) + 8 * (el >> 2) + 4 * h;
-        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y[el];
-    }
-}
-
 // ---- long prompts, shared operands staged in LDS, weights dequantized in registers: k_mmqs --------
-// k_mmqr's per-wave direct loads put every operand through the vector L1 once per wave that uses it
-// (activations 4x, weights 2x: ~123 KB per superblock step per CU) and measured 43.8 us at B = 512
-// (load-path bound). Here the workgroup stages each superblock's operands ONCE into LDS -- the
-// activation quants of its 64 columns [8 steps][64][32] (16 KB), their U halves and scales, and the
-// raw weight blocks of its 128 rows (18 KB) -- and every wave reads its fragments from LDS, then
-// dequantizes its own 32 rows' planes in registers (k_mmqr's step) and runs its 32 x 32 tile.
+// (Round 4's first register-dequant kernel loaded every operand per wave straight from L2 -- the
+// activations 4x, the weights 2x per CU: ~123 KB per superblock step -- and measured 43.8 us at
+// B = 512, load-path bound, profiles/r04a_pf_long_mmqr.txt; removed.) Here the workgroup stages each
+// superblock's operands ONCE into LDS -- the activation quants of its 64 columns [8 steps][64][32]
+// (16 KB), their U halves and scales, and the raw weight blocks of its 128 rows (18 KB) -- and every
+// wave reads its fragments from LDS, then dequantizes its own 32 rows' planes in registers (k_mmqp's
+// step) and runs its 32 x 32 tile.
 // Pipeline: the staging loads of superblock s + 2 are issued as step s starts and written into
 // the free LDS buffer at its end (two steps of latency cover; double-buffered LDS, one barrier per
-// step that waits for LDS traffic only, mi_lds_barrier). Staging roles are wave-uniform (waves 0-3
-// the activation quants, 4-7 the weights, U halves and scales), so every load uses a buffer
-// descriptor with an SGPR superblock offset. Activation fragments are stored with their two 16-byte
-// halves swapped for columns 16-31 of a 32-column group (the ds_read_b128 lane groups then hit 64
-// distinct banks). Same operands and canonical combine (mmqx_term, cfold_vec) as every kernel of
-// this file: bit-identical. Code: K in straight-line chunks of CH superblocks (as k_mmqr).
+// step that waits for LDS traffic only, mi_lds_barrier). Every staging load is a per-lane base plus
+// the superblock times a per-lane stride, with no branch around it. Activation fragments are stored
+// with their two 16-byte halves swapped for columns 16-31 of a 32-column group (the ds_read_b128
+// lane groups then hit 64 distinct banks). Same operands and canonical combine (mmqx_term,
+// cfold_vec) as every kernel of this file: bit-identical. CH > 0: K in straight-line chunks of CH
+// superblocks; 0: a rolled loop of step pairs; -1: rolled, each superblock's combine deferred under
+// the next one's MFMAs.
 template <int TYPE, int CH>
 __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
@@ -1416,7 +1317,7 @@ __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
     const uint32_t xoff = (uint32_t) (col * 32 + 16 * (h ^ ((col >> 4) & 1)));
     constexpr uint32_t kQs = F::Q5 ? 48 : 16;
     const uint32_t woff = (uint32_t) (XB + UB + DB + (32 * rw + r) * F::BS);
-    f32x16 y = f32x16(-0.0f), gsum = {};
+    f32x16 y = f32x16(-0.0f), ylo = f32x16(-0.0f), gsum = {};
 
     // The combine of a superblock reads its accumulators and its scales / U halves / mins from the
     // LDS buffer it was computed from (still intact during the next step: a buffer is restaged only
@@ -1509,7 +1410,7 @@ __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
         comb_begin(buf, c);
 #pragma unroll
         for (int j = 0; j < 8; j++) comb_slice(buf, acc, c, j);
-        cfold_vec(gsum, y, c.tv, sb, gs, S);
+        cfold_vec(gsum, y, ylo, c.tv, sb, gs, S);
     };
     // deferred: superblock sb's MFMAs with the combine of sb - 1 (accumulators accp, buffer buf ^ 1)
     // interleaved, one pair of elements per 32-deep step; returns with sb's accumulators in accc
@@ -1519,14 +1420,14 @@ __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
         mfma_sb(buf, accc, [&](int kk) {
             if (prev) comb_slice(buf ^ 1, accp, c, kk);
         });
-        if (prev) cfold_vec(gsum, y, c.tv, sb - 1, gs, S);
+        if (prev) cfold_vec(gsum, y, ylo, c.tv, sb - 1, gs, S);
     };
     auto finish_defer = [&](int buf, int sb, const i32x16 (&accp)[NP]) {
         Comb c;
         comb_begin(buf, c);
 #pragma unroll
         for (int j = 0; j < 8; j++) comb_slice(buf, accp, c, j);
-        cfold_vec(gsum, y, c.tv, sb, gs, S);
+        cfold_vec(gsum, y, ylo, c.tv, sb, gs, S);
     };
 
     Stg st0, st1;  // (two variables, not an array: a register pair the unrolled steps alternate)
@@ -1601,6 +1502,7 @@ __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
         }
     }
 
+    y = ylo + y;  // cfold_end
     // accumulator element el: prompt column c0 + 32 cw + (el & 3) + 8 (el >> 2) + 4 h, row n0 + 32 rw + r
     const int64_t n = n0 + 32 * rw + r;
     if (n >= N) return;
@@ -1608,6 +1510,265 @@ __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
     for (int el = 0; el < 16; el++) {
         const int64_t c = c0 + 32 * cw + (el & 3) + 8 * (el >> 2) + 4 * h;
         if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y[el];
+    }
+}
+
+// ---- long prompts, K split over wave pairs: k_mmqt ------------------------------------------------
+// k_mmqs dequantizes a wave's 32 weight rows once per 32 columns, and the dequantization is the
+// larger share of its VALU (~112 of ~300 instructions per 17 MFMAs). Here each wave runs 32 rows x 64
+// columns -- two 32 x 32 tiles per dequantized plane, 34 MFMAs per superblock -- and the 8 waves of
+// the 128-row x 64-column tile split K in two: waves 0-3 fold the low half of the canonical order
+// (superblocks [0, SK), groups 0..3), waves 4-7 the high half ([SK, S), groups 4..7), and the
+// halves meet once at the end in LDS (y = lo + hi: the canonical combine, bit-identical to every
+// kernel of this file). A stage holds one superblock of each half: per half the activation quants
+// [8 steps][64 columns][32] (16 KB, 16-byte halves swapped for columns 16-31 of a 32-column group,
+// as k_mmqs), the U halves (2 KB), the raw weight blocks of the 128 rows (18 KB) and d_a (256 B).
+// Staging is LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write pass): a stage is
+// 72 one-KB wave-instructions, 9 per wave (each a per-lane source address, the destination
+// lane-linear), plus one 256-byte d_a DMA per half. The next stage's DMAs are issued as a step
+// starts; the step ends with s_waitcnt vmcnt(0) + s_barrier (two LDS buffers; every global load of
+// this kernel is a DMA, so vmcnt(0) waits for exactly the next stage). Q4_K only: a Q5_K stage pair
+// (2 x 161 KB) exceeds the LDS.
+// Per superblock and wave: 34 MFMAs (2 tiles x (2 planes x 8 steps + 1 U)) for one dequantization.
+// LDS-DMA of 16 (4) bytes per lane: lane l's bytes land at LDS byte address lds + 16 l (4 l). As
+// inline asm, outside the compiler's wait bookkeeping: with the builtin, hipcc treats the DMA as a
+// pending write to any LDS address and waits vmcnt(0) before the next LDS read -- the current
+// stage's fragment reads -- which serializes the next stage's DMA with the current stage's
+// compute. The caller waits for the DMAs itself (vmcnt(0) before the stage barrier, an asm
+// statement with a memory clobber, which also keeps the DMAs of a stage ahead of it). No memory
+// clobber here: the compiler may move the current stage's LDS reads across a DMA (it writes the
+// other buffer). M0 is saved and restored within the statement (the compiler owns it).
+__device__ __forceinline__ void mi_glds16(const void * gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds));
+}
+__device__ __forceinline__ void mi_glds4(const void * gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds));
+}
+// LDS byte address of a __shared__ location (the low 32 bits of its flat address), wave-uniform
+__device__ __forceinline__ uint32_t mi_lds_addr(const void * p) {
+    return (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (uintptr_t) p);
+}
+
+// DI: the next stage's DMAs interleaved with the MFMA steps (else issued at the step's start).
+template <int TYPE, bool DI>
+__global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
+    MI_MMX_MEMBER(grp);
+    using F = XFmt<TYPE>;
+    static_assert(!F::Q5, "Q4_K only");
+    constexpr int NP = F::NP;
+    constexpr int BM = 128, BN = 64;
+    constexpr int XB = 8 * BN * 32;           // activation quants of one superblock
+    constexpr int UB = BN * 32;               // U halves
+    constexpr int WB = BM * F::BS;            // raw weight blocks
+    constexpr int DB = BN * 4;                // d_a
+    constexpr int HB = XB + UB + WB + DB;     // one K half of a stage: [X | U | W | d_a]
+    constexpr int SB = 2 * HB;                // a stage
+    constexpr int NPIECE = (XB + UB + WB) / 1024;  // 1-KB DMA pieces per half (36)
+    static_assert((XB + UB + WB) % 1024 == 0 && (2 * NPIECE) % 8 == 0, "whole pieces, evenly dealt");
+    constexpr int NI = 2 * NPIECE / 8;        // pieces per wave and stage (9)
+    constexpr int SINK = 2 * SB;              // d_a DMAs of waves 2-7 land here
+    __shared__ __attribute__((aligned(16))) char lds[2 * SB + DB];
+
+    const int tid = (int) threadIdx.x;
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int rw = w & 3, kh = w >> 2;
+    const int64_t ncols = act.ncols;
+    const int S = (int) (K / 256);
+    const int gs = cfold_gs(S);
+    const int SK = cfold_split(S);            // superblocks of the low half (>= those of the high)
+    const int64_t nrt = (N + BM - 1) / BM;
+    const int64_t n0 = (mmx_tile % nrt) * BM, c0 = (mmx_tile / nrt) * BN;
+    const int nrows = (int) std::min<int64_t>(BM, N - n0);
+    auto col_of = [&](int c) { return (uint32_t) std::min<int64_t>(c0 + c, ncols - 1); };
+
+    // ---- staging: piece q = w + 8 i of a stage (half q / NPIECE, piece t = q % NPIECE of the half):
+    // a wave-uniform global base and superblock stride, a per-lane 32-bit offset
+    const char * pbase[NI];
+    uint32_t pstride[NI], poff[NI], pdst[NI];
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        const int q = w + 8 * i, hf = q / NPIECE, t = q % NPIECE;
+        pdst[i] = (uint32_t) (hf * HB + 1024 * t);
+        if (t < 16) {  // activation quants: step kk, 32-column group cg
+            const int kk = t >> 1, cg = t & 1, col = 32 * cg + (lane >> 1);
+            pbase[i] = (const char *) act.xq + (size_t) kk * ncols * 32;
+            pstride[i] = 8 * (uint32_t) ncols * 32;
+            poff[i] = col_of(col) * 32 + 16 * ((lane & 1) ^ ((lane >> 5) & 1));
+        } else if (t < 18) {  // U halves
+            const int col = 32 * (t - 16) + (lane >> 1);
+            pbase[i] = (const char *) act.xu;
+            pstride[i] = (uint32_t) ncols * 32;
+            poff[i] = col_of(col) * 32 + 16 * ((lane & 1) ^ ((lane >> 5) & 1));
+        } else {  // raw weight blocks: 1 KB of the [128 rows][BS] image
+            const int o = 1024 * (t - 18) + 16 * lane, row = o / F::BS;
+            pbase[i] = (const char *) W + (size_t) n0 * nb01;
+            pstride[i] = F::BS;
+            poff[i] = (uint32_t) (std::min(row, nrows - 1) * nb01 + o % F::BS);
+        }
+    }
+    const uint32_t doff = col_of(lane) * 4;
+    // stage u: superblock u of the low half, SK + u of the high half (clamped: a high half shorter
+    // than the low one re-reads its last superblock, whose terms are not folded)
+    // piece i < NI of stage u into buffer buf; i == NI: d_a (wave 0 the low half's, wave 1 the high
+    // half's, the others into the sink)
+    auto stage_piece = [&](int u, int buf, int i) {
+        char * sbuf = lds + buf * SB;
+        if (i < NI) {
+            const int hf = (w + 8 * i) / NPIECE;
+            const int sb = std::min(hf ? SK + u : u, S - 1);
+            const char * src = pbase[i] + (size_t) sb * pstride[i] + poff[i];
+            mi_glds16(src, mi_lds_addr(sbuf + pdst[i]));
+        } else {
+            const int sb = std::min(w == 1 ? SK + u : u, S - 1);
+            const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
+            char * dd = w < 2 ? sbuf + w * HB + XB + UB + WB : lds + SINK;
+            mi_glds4(src, mi_lds_addr(dd));
+        }
+    };
+    auto stage_dma = [&](int u, int buf) {
+#pragma unroll
+        for (int i = 0; i <= NI; i++) stage_piece(u, buf, i);
+    };
+    auto stage_wait = [] { asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+    // ---- compute: rows n0 + 32 rw + r of half kh; tiles ct = columns 32 ct ..
+    const uint32_t xoff0 = (uint32_t) (r * 32 + 16 * (h ^ ((r >> 4) & 1)));  // tile 0; tile 1 at + 1024
+    constexpr uint32_t kQs = 16;
+    const uint32_t woff = (uint32_t) (kh * HB + XB + UB + (32 * rw + r) * F::BS);
+    const int sb_end = kh ? S : SK;
+    f32x16 y[2] = {f32x16(-0.0f), f32x16(-0.0f)}, gsum[2] = {};
+
+    auto step = [&](int buf, int sb, auto && hook) {
+        const char * base = lds + buf * SB;
+        const char * hb = base + kh * HB;
+        const char * wr = base + woff;
+        const uint4 hdr = *(const uint4 *) wr;
+        uint4 q4[4];
+#pragma unroll
+        for (int p = 0; p < 4; p++) q4[p] = *(const uint4 *) (wr + kQs + 32 * p + 16 * h);
+        const uint32_t w0 = hdr.y, w2 = hdr.w;
+        const uint32_t sca = w0 & 0x3F3F3F3Fu;
+        const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
+        i32x16 acc[2][NP];
+        uint32_t lo[4], hi[4];
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const i32x4 xa0 = *(const i32x4 *) (hb + kk * (BN * 32) + xoff0);
+            const i32x4 xa1 = *(const i32x4 *) (hb + kk * (BN * 32) + 1024 + xoff0);
+            if ((kk & 1) == 0) {
+                const uint4 q = q4[kk >> 1];
+                const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    lo[e] = qv[e] & 0x0F0F0F0Fu;
+                    hi[e] = (qv[e] >> 4) & 0x0F0F0F0Fu;
+                }
+            }
+            const uint32_t scw = kk < 4 ? sca : scb;
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                const uint32_t f = __builtin_amdgcn_ubfe(scw, 8 * (kk & 3) + 3 * p, 3);
+                const uint32_t * v = (kk & 1) ? hi : lo;
+                const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+                acc[0][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa0, b, kk == 0 ? i32x16{} : acc[0][p], 0, 0, 0);
+                acc[1][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa1, b, kk == 0 ? i32x16{} : acc[1][p], 0, 0, 0);
+            }
+            hook(kk);
+        }
+        // the combine: U on the f16 MFMA (A = [S & 63, S >> 6] of the lane's column, B = [m, 64 m]
+        // of its row), then mmqx_term per element, folded into this half's sum
+        const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
+        const uint32_t ma = hdr.z & 0x3F3F3F3Fu;
+        const uint32_t mb = ((hdr.w >> 4) & 0x0F0F0F0Fu) | ((hdr.z >> 2) & 0x30303030u);
+        const uint32_t mw = h ? mb : ma;
+        half8 mu;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t m = (mw >> (8 * q)) & 0xFF;
+            mu[2 * q] = (_Float16) (float) m;
+            mu[2 * q + 1] = (_Float16) (float) (64 * m);
+        }
+        const bool fold = sb < sb_end;  // wave-uniform
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            const half8 xu = *(const half8 *) (hb + XB + 1024 * ct + xoff0);
+            const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
+            const float * dal = (const float *) (hb + XB + UB + WB) + 32 * ct;
+            f32x16 tv;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const float2 d2 = *(const float2 *) &dal[8 * (j >> 1) + 4 * h + 2 * (j & 1)];
+                const float dav[2] = {d2.x, d2.y};
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const int el = 2 * j + e;
+                    const int T = (acc[ct][1][el] << F::SHIFT) + acc[ct][0][el];
+                    tv[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
+                }
+            }
+            if (fold) {
+                // one half's fold: groups end at multiples of gs, y = y + g (the high half's
+                // first group lands exactly on y = -0)
+                const int pos = sb % gs;
+                if (pos == 0) {
+                    asm volatile("" ::: "memory");
+                    gsum[ct] = f32x16(-0.0f);
+                }
+                gsum[ct] = gsum[ct] + tv;
+                if (pos == gs - 1 || sb == S - 1) {
+                    asm volatile("" ::: "memory");
+                    y[ct] = y[ct] + gsum[ct];
+                }
+            }
+        }
+    };
+
+    stage_dma(0, 0);
+    stage_wait();
+    for (int u = 0; u < SK; u++) {
+        // the next stage's DMAs (past the end: clamped re-reads into the idle buffer)
+        if constexpr (DI) {  // one piece behind each 32-deep step's MFMAs, the rest after the last
+            step(u & 1, (kh ? SK : 0) + u, [&](int kk) {
+                if (kk < 7) {
+                    stage_piece(u + 1, (u + 1) & 1, kk);
+                } else {
+#pragma unroll
+                    for (int i = 7; i <= NI; i++) stage_piece(u + 1, (u + 1) & 1, i);
+                }
+            });
+        } else {  // all at the step's start
+            stage_dma(u + 1, (u + 1) & 1);
+            step(u & 1, (kh ? SK : 0) + u, [](int) {});
+        }
+        stage_wait();
+    }
+
+    // the halves meet: waves 4-7 leave their sums in LDS (the stage buffers are idle: every DMA
+    // has landed and every wave has passed the last barrier), waves 0-3 add and store
+    f32x16 * ex = (f32x16 *) lds;
+    if (kh) {
+        ex[(rw * 2 + 0) * 64 + lane] = y[0];
+        ex[(rw * 2 + 1) * 64 + lane] = y[1];
+    }
+    mi_lds_barrier();
+    if (kh) return;
+    const int64_t n = n0 + 32 * rw + r;
+    if (n >= N) return;
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) {
+        const f32x16 yv = y[ct] + ex[(rw * 2 + ct) * 64 + lane];  // cfold_end: lo + hi
+        // element el: prompt column c0 + 32 ct + (el & 3) + 8 (el >> 2) + 4 h
+#pragma unroll
+        for (int el = 0; el < 16; el++) {
+            const int64_t c = c0 + 32 * ct + (el & 3) + 8 * (el >> 2) + 4 * h;
+            if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = yv[el];
+        }
     }
 }
 
@@ -2152,8 +2313,9 @@ __global__ __launch_bounds__(1024) void k_mmqd1(mi_mmx_group g) {
     for (int o = 64 * w + lane; o < 1024; o += 64 * S) {
         const int lo = o >> 4, el = o & 15;
         const float * src = red + (size_t) lo * 16 + el;
-        float y = 0.0f, gsum = 0.0f;
-        for (int v = 0; v < ((ABL & 4) ? 1 : S); v++) cfold(gsum, y, src[(size_t) v * 64 * 16], v, gs, S);
+        float y = -0.0f, ylo = -0.0f, gsum = 0.0f;
+        for (int v = 0; v < ((ABL & 4) ? 1 : S); v++) cfold(gsum, y, ylo, src[(size_t) v * 64 * 16], v, gs, S);
+        y = cfold_end(ylo, y);
         if (ABL & 4) y = gsum;
         // element el of lane lo = prompt column c0 + (el & 3) + 8 (el >> 2) + 4 (lo >> 5), row n0 + lo % 32
         const int64_t n = n0 + (lo & 31);
@@ -2271,15 +2433,16 @@ __global__ __launch_bounds__(1024) void k_mmqd16(mi_mmx_group grp) {
     }
     mi_lds_barrier();
     if (w != 0) return;
-    float4 y = {}, gsum = {};
+    float4 y = {-0.0f, -0.0f, -0.0f, -0.0f}, lo = y, gsum = {};
     const int gs = cfold_gs(S);
     for (int v = 0; v < S; v++) {
         const float4 t4 = *(const float4 *) (red + ((size_t) v * 64 + lane) * 4);
-        cfold(gsum.x, y.x, t4.x, v, gs, S);
-        cfold(gsum.y, y.y, t4.y, v, gs, S);
-        cfold(gsum.z, y.z, t4.z, v, gs, S);
-        cfold(gsum.w, y.w, t4.w, v, gs, S);
+        cfold(gsum.x, y.x, lo.x, t4.x, v, gs, S);
+        cfold(gsum.y, y.y, lo.y, t4.y, v, gs, S);
+        cfold(gsum.z, y.z, lo.z, t4.z, v, gs, S);
+        cfold(gsum.w, y.w, lo.w, t4.w, v, gs, S);
     }
+    y = make_float4(cfold_end(lo.x, y.x), cfold_end(lo.y, y.y), cfold_end(lo.z, y.z), cfold_end(lo.w, y.w));
     const int64_t n = n0 + i;
     if (n >= N) return;
     const float yv[4] = {y.x, y.y, y.z, y.w};
@@ -2449,10 +2612,10 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         else hipLaunchKernelGGL((k_mmqx<13, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, g);
         return;
     }
-    if (g_mi_tuning.mmq_long == 2) {  // weights dequantized in registers, 128 x 64 tiles of 8 waves
-        const dim3 gridr((unsigned) mmx_deal(g, 128, 64));
-        if (type == 12) hipLaunchKernelGGL((k_mmqr<12, 2, 18>), gridr, dim3(512), 0, s, g);
-        else hipLaunchKernelGGL((k_mmqr<13, 1, 16>), gridr, dim3(512), 0, s, g);
+    if ((g_mi_tuning.mmq_long == 2 || g_mi_tuning.mmq_long == 6) && type == 12) {  // K split over wave pairs, 128 x 64 tiles (k_mmqt; 6: DMAs at step start)
+        const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
+        if (g_mi_tuning.mmq_long == 2) hipLaunchKernelGGL((k_mmqt<12, true>), gridt, dim3(512), 0, s, g);
+        else hipLaunchKernelGGL((k_mmqt<12, false>), gridt, dim3(512), 0, s, g);
         return;
     }
     if (g_mi_tuning.mmq_long >= 3) {  // + shared operands staged in LDS (4: rolled loop, 5: + deferred combine)

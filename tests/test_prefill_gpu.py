@@ -140,8 +140,8 @@ def test_prefill_edge_values(rt, backend):
 @pytest.mark.parametrize("B", [72, 13])
 def test_prefill_kernels_bit_equal(rt, backend, tname, B):
     """Every prefill kernel shares the canonical combine (exact T and U per superblock, terms
-    combined in the cfold order: 4 contiguous superblock groups, each left-folded, then the group
-    sums left-folded), so any kernel choice gives the same bits: k_mmqp (the default for <= 128
+    combined in the cfold order: 8 contiguous superblock groups, each left-folded; groups 0-3 and
+    4-7 left-folded separately, then added), so any kernel choice gives the same bits: k_mmqp (the default for <= 128
     columns), k_mmqd1 (variant bit 2048), k_mmqx (full- and half-width workgroups) and, for <= 16
     columns, k_mmqd16 (the default there; 16 x 16 tiles on the 16x16x64 MFMA). Q4_0 / Q8_0:
     k_mmq0p (32 x 32 tiles, <= 64 columns) and k_mmq0x (weights staged per 64 x 128 workgroup)."""
@@ -155,7 +155,7 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
     else:
         variants = [0, 2048, 1 << 27, 128 | 131072, 128 | 65536, 128 | 131072 | (1 << 28)] + ([1 << 21] if B <= 16 else [])
     # long-prompt kernels forced onto these shapes (variant bits 128 | 131072, mmq_long): k_mmqw (1),
-    # k_mmqr (2, weights dequantized in registers), k_mmqs (3 chunked, 4 rolled, 5 deferred combine)
+    # k_mmqt (2, K split over wave pairs; Q4_K), k_mmqs (3 chunked, 4 rolled, 5 deferred combine)
     longs = [(128 | 131072, L) for L in (1, 2, 3, 4, 5)] if tname in ("q4_K", "q5_K") else []
     outs = {}
     try:
@@ -172,6 +172,29 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
     assert rel_err(outs[0], ref) <= EXACT_TOL
     for v in variants[1:]:
         assert np.array_equal(outs[v].view(np.uint32), outs[0].view(np.uint32)), (v, rel_err(outs[v], outs[0]))
+
+
+@pytest.mark.parametrize("K,N,B", [(256, 64, 130), (1280, 96, 257), (3072, 200, 200), (11008, 256, 136), (4096, 4096, 512)])
+def test_split_k_prefill_bit_equal(rt, backend, K, N, B):
+    """k_mmqt (mmq_long 2: the two K halves of the canonical order on two waves, met in LDS) on
+    ragged shapes: one superblock (empty high half), S = 5 (a one-superblock high half), S = 12,
+    S = 43 (a high half shorter than the low: idle steps), ragged rows and columns; bit-identical to
+    the default kernel and within the exact-path tolerance of the oracle."""
+    t = orc.Q4_K
+    w = synth.uniform(K + 3 * N, K * N)
+    x = synth.uniform(K + 5 * B, K * B)
+    wq = orc.quantize(t, w, K)
+    try:
+        base = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
+        assert rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", 128 | 131072)
+        assert rt.ggml_backend_mi355x_set_tuning(b"mmq_long", 2)
+        y = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
+    finally:
+        rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", 0)
+        rt.ggml_backend_mi355x_set_tuning(b"mmq_long", 0)
+    assert np.array_equal(y.view(np.uint32), base.view(np.uint32)), rel_err(y, base)
+    if K * N * B <= 4096 * 4096 * 64:
+        assert rel_err(y, orc.mul_mat(t, wq, K, N, x, B)) <= EXACT_TOL
 
 
 @pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q4_0", "q8_0"])
