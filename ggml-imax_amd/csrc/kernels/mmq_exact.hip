@@ -1224,8 +1224,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
 // with their two 16-byte halves swapped for columns 16-31 of a 32-column group (the ds_read_b128
 // lane groups then hit 64 distinct banks). Same operands and canonical combine (mmqx_term,
 // cfold_vec) as every kernel of this file: bit-identical. CH > 0: K in straight-line chunks of CH
-// superblocks; 0: a rolled loop of step pairs; -1: rolled, each superblock's combine deferred under
-// the next one's MFMAs.
+// superblocks; 0: a rolled loop of step pairs.
 template <int TYPE, int CH>
 __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
@@ -1412,54 +1411,9 @@ __global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
         for (int j = 0; j < 8; j++) comb_slice(buf, acc, c, j);
         cfold_vec(gsum, y, ylo, c.tv, sb, gs, S);
     };
-    // deferred: superblock sb's MFMAs with the combine of sb - 1 (accumulators accp, buffer buf ^ 1)
-    // interleaved, one pair of elements per 32-deep step; returns with sb's accumulators in accc
-    auto compute_defer = [&](int buf, int sb, i32x16 (&accc)[NP], const i32x16 (&accp)[NP], bool prev) {
-        Comb c;
-        if (prev) comb_begin(buf ^ 1, c);
-        mfma_sb(buf, accc, [&](int kk) {
-            if (prev) comb_slice(buf ^ 1, accp, c, kk);
-        });
-        if (prev) cfold_vec(gsum, y, ylo, c.tv, sb - 1, gs, S);
-    };
-    auto finish_defer = [&](int buf, int sb, const i32x16 (&accp)[NP]) {
-        Comb c;
-        comb_begin(buf, c);
-#pragma unroll
-        for (int j = 0; j < 8; j++) comb_slice(buf, accp, c, j);
-        cfold_vec(gsum, y, ylo, c.tv, sb, gs, S);
-    };
-
     Stg st0, st1;  // (two variables, not an array: a register pair the unrolled steps alternate)
-    static_assert(CH % 2 == 0 || CH == -1, "staging registers alternate");
-    if constexpr (CH == -1) {
-        // rolled + deferred combine: superblock sb's combine runs under sb + 1's MFMAs (two
-        // accumulator sets, alternating with the step parity). The buffer a deferred combine reads
-        // (sb's) is restaged only at the end of step sb + 1, after the combine.
-        i32x16 acc0[NP], acc1[NP];
-        stage_load(st0, 0);
-        stage_load(st1, 1);
-        stage_store(st0, 0);
-        mi_lds_barrier();
-        // superblock 0 (no previous), then pairs (odd, even) so every slot index is static
-        stage_load(st0, 2);
-        compute_defer(0, 0, acc0, acc1, false);
-        stage_store(st1, 1);
-        mi_lds_barrier();
-        for (int sb = 1; sb < S - 1; sb += 2) {
-            stage_load(st1, sb + 2);
-            compute_defer(1, sb, acc1, acc0, true);
-            stage_store(st0, 0);
-            mi_lds_barrier();
-            stage_load(st0, sb + 3);
-            compute_defer(0, sb + 1, acc0, acc1, true);
-            stage_store(st1, 1);
-            mi_lds_barrier();
-        }
-        // S even: the last superblock S - 1 is odd (buffer 1)
-        compute_defer(1, S - 1, acc1, acc0, true);
-        finish_defer(1, S - 1, acc1);
-    } else if constexpr (CH == 0) {
+    static_assert(CH % 2 == 0, "staging registers alternate");
+    if constexpr (CH == 0) {
         // rolled: two steps per iteration, no branch in the body (S even, host-checked; requests
         // past the end are clamped re-reads), so the compiler's vmcnt bookkeeping across the back
         // edge stays exact and the code stays small
@@ -2618,13 +2572,9 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         else hipLaunchKernelGGL((k_mmqt<12, false>), gridt, dim3(512), 0, s, g);
         return;
     }
-    if (g_mi_tuning.mmq_long >= 3) {  // + shared operands staged in LDS (4: rolled loop, 5: + deferred combine)
+    if (g_mi_tuning.mmq_long == 3 || g_mi_tuning.mmq_long == 4) {  // shared operands staged in LDS (4: rolled loop)
         const dim3 gridr((unsigned) mmx_deal(g, 128, 64));
-        const bool rolled = g_mi_tuning.mmq_long >= 4 && (K / 256) % 2 == 0;
-        if (rolled && g_mi_tuning.mmq_long == 5) {
-            if (type == 12) hipLaunchKernelGGL((k_mmqs<12, -1>), gridr, dim3(512), 0, s, g);
-            else hipLaunchKernelGGL((k_mmqs<13, -1>), gridr, dim3(512), 0, s, g);
-        } else if (rolled) {
+        if (g_mi_tuning.mmq_long == 4 && (K / 256) % 2 == 0) {
             if (type == 12) hipLaunchKernelGGL((k_mmqs<12, 0>), gridr, dim3(512), 0, s, g);
             else hipLaunchKernelGGL((k_mmqs<13, 0>), gridr, dim3(512), 0, s, g);
         } else {

@@ -4,7 +4,7 @@
 set -eo pipefail
 OUT=gpurun_out/${1:-r04c}; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-PF_SINGLE=0 PF_R=16 PF_TYPES=${PF_TYPES:-q4_K} PF_LONG=${PF_LONG:-1,4,5} MMQ_VARIANTS=0 timeout -k 10 300 python3 -u tools/prefill_bench.py 512 2>&1 | grep --line-buffered -v amdgpu.ids | tee $OUT/pf_long.txt
+PF_SINGLE=0 PF_R=16 PF_TYPES=${PF_TYPES:-q4_K} PF_LONG=${PF_LONG:-1,2,4} MMQ_VARIANTS=0 timeout -k 10 300 python3 -u tools/prefill_bench.py 512 2>&1 | grep --line-buffered -v amdgpu.ids | tee $OUT/pf_long.txt
 PF_SINGLE=1 PF_R=16 PF_TYPES=f16 MMQ_VARIANTS=0,131072 timeout -k 10 300 python3 -u tools/prefill_bench.py 64 32 2>&1 | grep --line-buffered -v amdgpu.ids | tee $OUT/pf_f16.txt
 timeout -k 10 300 python -u -m pytest tests/test_mul_mat_gpu.py -x -q --timeout 200 --timeout-method thread -m gpu -k "f16 or float" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -2 $OUT/pytest.log

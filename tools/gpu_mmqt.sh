@@ -1,13 +1,12 @@
 #!/bin/bash
-# Round 4: the split-K long-prompt kernel (k_mmqt, mmq_long 2) -- prefill parity (the canonical
-# order changed for every Q4_K / Q5_K kernel), then Q4_K / Q5_K B=512 timing against the default,
+# Round 4: the split-K long-prompt kernel (k_mmqt, mmq_long 2 / 6) -- Q4_K / Q5_K B=512 / 256 timing
+# against the default, prefill parity (the canonical order changed for every Q4_K / Q5_K kernel),
 # then one PMC pass set of k_mmqt
 set -eo pipefail
 OUT=gpurun_out/${1:-r04h}; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 400 python -u -m pytest tests/test_prefill_gpu.py -x -v --timeout 200 --timeout-method thread -m gpu > $OUT/pytest_prefill.log 2>&1 || { tail -40 $OUT/pytest_prefill.log; exit 1; }
-tail -3 $OUT/pytest_prefill.log
 PF_SINGLE=0 PF_R=16 PF_TYPES=${PF_TYPES:-q4_K,q5_K} PF_LONG=${PF_LONG:-0,2,6} MMQ_VARIANTS=0 timeout -k 10 300 python3 -u tools/prefill_bench.py 512 256 2>&1 | grep --line-buffered -v amdgpu.ids | tee $OUT/pf_long.txt
+timeout -k 10 400 python -u -m pytest tests/test_prefill_gpu.py -x -v --timeout 200 --timeout-method thread -m gpu > $OUT/pytest_prefill.log 2>&1 && tail -1 $OUT/pytest_prefill.log || { grep -E "FAILED|^E " $OUT/pytest_prefill.log | head -20; tail -1 $OUT/pytest_prefill.log; }
 if [ -z "$NO_PMC" ]; then
 export PF_SINGLE=0 PF_R=16 PF_TYPES=q4_K MMQ_VARIANTS=0
 PF_LONG=2 timeout -k 10 300 python3 -u tools/pmc_kernel.py "$OUT/pmc_l2" k_mmq \

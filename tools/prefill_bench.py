@@ -14,7 +14,7 @@ sp = lib.ggml_backend_mi355x_get_stream(be)
 Bs = [int(b) for b in sys.argv[1:]] or [512, 64]
 refs = {}
 VARS = [int(v) for v in os.environ.get("MMQ_VARIANTS", "0").split(",")]
-# PF_LONG: mmq_long settings to compare (Q4_K / Q5_K past 128 columns: 1 k_mmqw, 2 k_mmqt, 3-5 k_mmqs)
+# PF_LONG: mmq_long settings to compare (Q4_K / Q5_K past 128 columns: 1 k_mmqw, 2 k_mmqt, 3-4 k_mmqs, 6 k_mmqt DMAs at step start)
 LONGS = [int(v) for v in os.environ.get("PF_LONG", "0").split(",")]
 VARS = [(v, l) for v in VARS for l in LONGS]
 # PF_MMV_BLOCKS: decode GEMV grid targets to compare (0 = automatic)
