@@ -2566,9 +2566,12 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         else hipLaunchKernelGGL((k_mmqx<13, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, g);
         return;
     }
-    if ((g_mi_tuning.mmq_long == 2 || g_mi_tuning.mmq_long == 6) && type == 12) {  // K split over wave pairs, 128 x 64 tiles (k_mmqt; 6: DMAs at step start)
+    // Q4_K: K split over wave pairs, 128 x 64 tiles (k_mmqt, the default; mmq_long 6: its DMAs at
+    // the step start; B=512 33.4 vs 36.6 us for k_mmqw, B=256 18.5 vs 19.7, profiles/r04i_pf_long_mmqt.txt)
+    const int lng = g_mi_tuning.mmq_long;
+    if ((lng == 0 || lng == 2 || lng == 6) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
-        if (g_mi_tuning.mmq_long == 2) hipLaunchKernelGGL((k_mmqt<12, true>), gridt, dim3(512), 0, s, g);
+        if (lng != 6) hipLaunchKernelGGL((k_mmqt<12, true>), gridt, dim3(512), 0, s, g);
         else hipLaunchKernelGGL((k_mmqt<12, false>), gridt, dim3(512), 0, s, g);
         return;
     }

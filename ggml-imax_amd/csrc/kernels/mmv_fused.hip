@@ -113,21 +113,7 @@ __device__ __forceinline__ void quantize_slice(float4 v4, int lane, const lds_ac
 
 // ------------------------------------------------------------------ weight formats
 
-// NT: weight loads with the nontemporal hint (the guide's nt-weights: once-read streams land
-// sooner); the weights of a GEMV are read exactly once per launch
-typedef unsigned mi_u32x4 __attribute__((ext_vector_type(4)));
-template <bool NT>
-__device__ __forceinline__ uint4 wld16(const uint8_t * p) {
-    if constexpr (NT) return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const mi_u32x4 *) p));
-    else return *(const uint4 *) p;
-}
-template <bool NT>
-__device__ __forceinline__ uint32_t wld4(const uint8_t * p) {
-    if constexpr (NT) return __builtin_nontemporal_load((const uint32_t *) p);
-    else return *(const uint32_t *) p;
-}
-
-template <bool Q5, bool NT = false>
+template <bool Q5>
 struct FmtKQ {
     static constexpr int QKA = 256;  // activation block
     static constexpr int ITEM = 64;  // elements per item
@@ -142,12 +128,12 @@ struct FmtKQ {
         const uint32_t s = (uint32_t) item >> 2, j = (uint32_t) item & 3;
         const uint32_t blk = s * BS;
         const uint32_t qp = blk + (Q5 ? 48 : 16) + 32 * j;
-        r.hdr = wld16<NT>(row + blk);
-        r.qa = wld16<NT>(row + qp);
-        r.qb = wld16<NT>(row + qp + 16);
+        r.hdr = *(const uint4 *) (row + blk);
+        r.qa = *(const uint4 *) (row + qp);
+        r.qb = *(const uint4 *) (row + qp + 16);
         if constexpr (Q5) {
-            r.ha = wld16<NT>(row + blk + 16);
-            r.hb = wld16<NT>(row + blk + 32);
+            r.ha = *(const uint4 *) (row + blk + 16);
+            r.hb = *(const uint4 *) (row + blk + 32);
         }
     }
     template <int NC>
@@ -316,7 +302,7 @@ struct FmtKQ {
 
 // Q4_0 (18 B) / Q8_0 (34 B) blocks: 2-byte aligned. Load the dwords covering the quants
 // (aligned down) and re-align with v_alignbyte; d is a separate 2-byte load.
-template <bool Q8, bool NT = false>
+template <bool Q8>
 struct FmtQ0 {
     static constexpr int QKA = 32;
     static constexpr int ITEM = 32;
@@ -335,7 +321,7 @@ struct FmtQ0 {
         r.off = blk & 2;
         const uint32_t base = blk - r.off;
 #pragma unroll
-        for (int i = 0; i <= NQ; i++) r.w[i] = wld4<NT>(row + base + 4 * i);  // 256 B tail slack
+        for (int i = 0; i <= NQ; i++) r.w[i] = *(const uint32_t *) (row + base + 4 * i);  // 256 B tail slack
     }
     template <int NC>
     __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
@@ -434,8 +420,7 @@ struct FmtQ0 {
 // Q4_0 in pairs of blocks (tree order only): an item is 2 blocks = 36 B, 4-byte aligned, so 9
 // dword loads cover it with no slack, the second block's quants are whole dwords (only the
 // first's need v_alignbyte), and a K = 4096 row is one item per lane.
-template <bool NT = false>
-struct FmtQ0PairT {
+struct FmtQ0Pair {
     static constexpr int QKA = 32;
     static constexpr int ITEM = 64;
     struct Regs {
@@ -444,7 +429,7 @@ struct FmtQ0PairT {
     __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item) {
         const uint8_t * p = row + (uint32_t) item * 36;
 #pragma unroll
-        for (int i = 0; i < 9; i++) r.w[i] = wld4<NT>(p + 4 * i);
+        for (int i = 0; i < 9; i++) r.w[i] = *(const uint32_t *) (p + 4 * i);
     }
     template <int NC>
     __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
@@ -479,7 +464,6 @@ struct FmtQ0PairT {
     }
 };
 
-using FmtQ0Pair = FmtQ0PairT<false>;
 
 // ------------------------------------------------------------------ the streaming kernel
 
@@ -792,6 +776,17 @@ int resident_blocks(const void * fn, size_t lds) {
     return n;
 }
 
+static int mi_cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        (void) hipGetDevice(&dev);
+        n = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    }
+    return n;
+}
+
 template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO = false>
 void launch_one(mi_mmv_group g, hipStream_t s) {
     const size_t act = lds_bytes<F::QKA>(NC, g.K);
@@ -827,7 +822,12 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
             attr_set = true;
         }
     }
-    const int target = g_mi_tuning.mmv_blocks > 0 ? g_mi_tuning.mmv_blocks : resident_blocks(fn, lds);
+    // automatic grid: the resident workgroup count, split over the members. A lone member at
+    // K >= 4096 gets one workgroup per CU instead: every workgroup quantizes the whole activation
+    // in its prologue, so at 4 rows per workgroup that redundant work dominates (Q4_K 4096^2 alone
+    // in its graph 7.96 -> 6.57 us, profiles/r04e_pf_single_blocks.txt)
+    int target = g_mi_tuning.mmv_blocks > 0 ? g_mi_tuning.mmv_blocks : resident_blocks(fn, lds);
+    if (g_mi_tuning.mmv_blocks <= 0 && g.n == 1 && g.K >= 4096) target = std::min(target, mi_cu_count());
     int bpm = target / g.n;
     if (bpm < 1) bpm = 1;
     int64_t rows = (g.N + bpm - 1) / bpm;
@@ -932,33 +932,19 @@ static void mi_mul_mat_q_fused_launch(mi_mmv_group & g, hipStream_t s) {
     // variant 0 = per-type default, from interleaved A/B runs on MI355X (tools/mmv_tune.py):
     // prefetch depth 2 for Q4_K / Q8_0 / Q4_0 (Q4_0 in block pairs: 4096 x 11008 5.34 -> 5.58
     // TB/s), depth 1 for Q5_K (fewer VGPRs, more waves)
-    // variant + 100: nontemporal weight loads (A/B)
+    // (Nontemporal weight loads -- the guide's nt-weights -- measured 30-37 % SLOWER on every
+    // shape, profiles/r04g_nt_ab.txt: removed.)
     int variant = g_mi_tuning.mmv_variant;
-    const bool nt = variant >= 100;
-    variant %= 100;
     if (variant == 0) variant = (g.type == 12 || g.type == 8) ? 21 : (g.type == 2 ? 22 : 11);
     switch (g.type) {
-        case 12:
-            if (nt) launch_stream_ord<FmtKQ<false, true>>(g, variant, s);
-            else launch_stream_ord<FmtKQ<false>>(g, variant, s);
-            break;
-        case 13:
-            if (nt) launch_stream_ord<FmtKQ<true, true>>(g, variant, s);
-            else launch_stream_ord<FmtKQ<true>>(g, variant, s);
-            break;
+        case 12: launch_stream_ord<FmtKQ<false>>(g, variant, s); break;
+        case 13: launch_stream_ord<FmtKQ<true>>(g, variant, s); break;
         case 2:
             // tree order: pairs of blocks per item (variant % 10 == 1: single blocks)
-            if (!mi_mmv_order() && variant % 10 != 1) {
-                if (nt) launch_stream_nc<FmtQ0PairT<true>, false>(g, variant, s);
-                else launch_stream_nc<FmtQ0Pair, false>(g, variant, s);
-            } else {
-                launch_stream_ord<FmtQ0<false>>(g, variant, s);
-            }
+            if (!mi_mmv_order() && variant % 10 != 1) launch_stream_nc<FmtQ0Pair, false>(g, variant, s);
+            else launch_stream_ord<FmtQ0<false>>(g, variant, s);
             break;
-        case 8:
-            if (nt) launch_stream_ord<FmtQ0<true, true>>(g, variant, s);
-            else launch_stream_ord<FmtQ0<true>>(g, variant, s);
-            break;
+        case 8: launch_stream_ord<FmtQ0<true>>(g, variant, s); break;
         default: break;
     }
 }

@@ -20,7 +20,8 @@ LIB_DIR = os.path.join(PKG_ROOT, "lib")
 # GGML_MI355X_CORE_LIB: an alternative build of the host runtime (the sanitizer build of
 # `make -C ggml-imax_amd sanitize`, run by tools/sanitize.sh)
 CORE_LIB = os.environ.get("GGML_MI355X_CORE_LIB") or os.path.join(LIB_DIR, "libggml_core.so")
-BACKEND_LIB = os.path.join(LIB_DIR, "libggml_mi355x.so")
+# GGML_MI355X_BACKEND_LIB: an alternative build of the backend (A/B builds, e.g. `make abpk`)
+BACKEND_LIB = os.environ.get("GGML_MI355X_BACKEND_LIB") or os.path.join(LIB_DIR, "libggml_mi355x.so")
 GPT2_LIB = os.path.join(LIB_DIR, "libgpt2_mi355x.so")
 
 # enum ggml_type (include/ggml/ggml.h:348-381)
