@@ -1507,8 +1507,14 @@ __device__ __forceinline__ uint32_t mi_lds_addr(const void * p) {
     return (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (uintptr_t) p);
 }
 
-// DI: the next stage's DMAs interleaved with the MFMA steps (else issued at the step's start).
-template <int TYPE, bool DI>
+// SKEW: the high-half waves fold superblock u's terms while the low-half waves run superblock
+// u + 1's MFMAs (and the other way round), so the two waves of a SIMD -- w and w + 4, the two halves
+// of the same rows -- alternate between the matrix pipe and the VALU instead of running the same
+// phase in lock step after every barrier. The high half's combine operands (its rows' block headers,
+// the U halves and d_a of its superblock) then live in a ring of three LDS slots, written by the
+// stage's DMAs and read one step later, after the double-buffered stage they came with has been
+// restaged.
+template <int TYPE, bool SKEW>
 __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -1524,8 +1530,10 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     constexpr int NPIECE = (XB + UB + WB) / 1024;  // 1-KB DMA pieces per half (36)
     static_assert((XB + UB + WB) % 1024 == 0 && (2 * NPIECE) % 8 == 0, "whole pieces, evenly dealt");
     constexpr int NI = 2 * NPIECE / 8;        // pieces per wave and stage (9)
-    constexpr int SINK = 2 * SB;              // d_a DMAs of waves 2-7 land here
-    __shared__ __attribute__((aligned(16))) char lds[2 * SB + DB];
+    constexpr int RS = BM * 16 + UB + DB;     // SKEW ring slot: [headers | U halves | d_a] of the high half
+    constexpr int RING = 2 * SB;
+    constexpr int SINK = RING + (SKEW ? 3 * RS : 0);  // d_a DMAs of waves 2-7 land here
+    __shared__ __attribute__((aligned(16))) char lds[SINK + DB];
 
     const int tid = (int) threadIdx.x;
     const int lane = tid & 63;
@@ -1542,14 +1550,26 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     auto col_of = [&](int c) { return (uint32_t) std::min<int64_t>(c0 + c, ncols - 1); };
 
     // ---- staging: piece q = w + 8 i of a stage (half q / NPIECE, piece t = q % NPIECE of the half):
-    // a wave-uniform global base and superblock stride, a per-lane 32-bit offset
-    const char * pbase[NI];
-    uint32_t pstride[NI], poff[NI], pdst[NI];
+    // a wave-uniform global base and superblock stride, a per-lane 32-bit offset. SKEW: the high
+    // half's U pieces go to the ring slot, and waves 0 and 1 move its rows' 16-byte headers there
+    // too (pieces 72, 73: 64 rows each).
+    constexpr int NX = SKEW ? 1 : 0;          // extra pieces per wave (waves 0, 1)
+    const char * pbase[NI + NX];
+    uint32_t pstride[NI + NX], poff[NI + NX], pdst[NI + NX];
+    bool pring[NI + NX];
 #pragma unroll
-    for (int i = 0; i < NI; i++) {
+    for (int i = 0; i < NI + NX; i++) {
         const int q = w + 8 * i, hf = q / NPIECE, t = q % NPIECE;
         pdst[i] = (uint32_t) (hf * HB + 1024 * t);
-        if (t < 16) {  // activation quants: step kk, 32-column group cg
+        pring[i] = false;
+        if (i == NI) {  // SKEW: header piece q - 72 (waves 0, 1; the others re-read it into the sink)
+            const int row = 64 * (w & 1) + lane;
+            pbase[i] = (const char *) W + (size_t) n0 * nb01;
+            pstride[i] = F::BS;
+            poff[i] = (uint32_t) (std::min(row, nrows - 1) * nb01);
+            pdst[i] = (uint32_t) (1024 * (w & 1));
+            pring[i] = true;
+        } else if (t < 16) {  // activation quants: step kk, 32-column group cg
             const int kk = t >> 1, cg = t & 1, col = 32 * cg + (lane >> 1);
             pbase[i] = (const char *) act.xq + (size_t) kk * ncols * 32;
             pstride[i] = 8 * (uint32_t) ncols * 32;
@@ -1559,6 +1579,10 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
             pbase[i] = (const char *) act.xu;
             pstride[i] = (uint32_t) ncols * 32;
             poff[i] = col_of(col) * 32 + 16 * ((lane & 1) ^ ((lane >> 5) & 1));
+            if (SKEW && hf == 1) {
+                pdst[i] = (uint32_t) (BM * 16 + 1024 * (t - 16));
+                pring[i] = true;
+            }
         } else {  // raw weight blocks: 1 KB of the [128 rows][BS] image
             const int o = 1024 * (t - 18) + 16 * lane, row = o / F::BS;
             pbase[i] = (const char *) W + (size_t) n0 * nb01;
@@ -1568,26 +1592,28 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     }
     const uint32_t doff = col_of(lane) * 4;
     // stage u: superblock u of the low half, SK + u of the high half (clamped: a high half shorter
-    // than the low one re-reads its last superblock, whose terms are not folded)
-    // piece i < NI of stage u into buffer buf; i == NI: d_a (wave 0 the low half's, wave 1 the high
-    // half's, the others into the sink)
-    auto stage_piece = [&](int u, int buf, int i) {
-        char * sbuf = lds + buf * SB;
-        if (i < NI) {
-            const int hf = (w + 8 * i) / NPIECE;
+    // than the low one re-reads its last superblock, whose terms are not folded) into buffer u & 1
+    // (and ring slot u % 3). Piece i < NI + NX; i == NI + NX: d_a (wave 0 the low half's, wave 1
+    // the high half's, the others into the sink).
+    auto stage_piece = [&](int u, int i) {
+        char * sbuf = lds + (u & 1) * SB;
+        char * rslot = lds + RING + (u % 3) * RS;
+        if (i < NI + NX) {
+            const int hf = i == NI ? 1 : (w + 8 * i) / NPIECE;
             const int sb = std::min(hf ? SK + u : u, S - 1);
             const char * src = pbase[i] + (size_t) sb * pstride[i] + poff[i];
-            mi_glds16(src, mi_lds_addr(sbuf + pdst[i]));
+            char * dd = (i == NI && w >= 2) ? lds + SINK : (pring[i] ? rslot : sbuf) + pdst[i];
+            mi_glds16(src, mi_lds_addr(dd));
         } else {
             const int sb = std::min(w == 1 ? SK + u : u, S - 1);
             const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
-            char * dd = w < 2 ? sbuf + w * HB + XB + UB + WB : lds + SINK;
+            char * dd = w >= 2 ? lds + SINK : (SKEW && w == 1) ? rslot + BM * 16 + UB : sbuf + w * HB + XB + UB + WB;
             mi_glds4(src, mi_lds_addr(dd));
         }
     };
-    auto stage_dma = [&](int u, int buf) {
+    auto stage_dma = [&](int u) {
 #pragma unroll
-        for (int i = 0; i <= NI; i++) stage_piece(u, buf, i);
+        for (int i = 0; i <= NI + NX; i++) stage_piece(u, i);
     };
     auto stage_wait = [] { asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
@@ -1597,8 +1623,10 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     const uint32_t woff = (uint32_t) (kh * HB + XB + UB + (32 * rw + r) * F::BS);
     const int sb_end = kh ? S : SK;
     f32x16 y[2] = {f32x16(-0.0f), f32x16(-0.0f)}, gsum[2] = {};
+    i32x16 acc[2][NP];
 
-    auto step = [&](int buf, int sb, auto && hook) {
+    // superblock MFMAs from stage buffer buf into acc; `hook(kk)` after step kk's MFMAs
+    auto mfma = [&](int buf, auto && hook) {
         const char * base = lds + buf * SB;
         const char * hb = base + kh * HB;
         const char * wr = base + woff;
@@ -1609,7 +1637,6 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         const uint32_t w0 = hdr.y, w2 = hdr.w;
         const uint32_t sca = w0 & 0x3F3F3F3Fu;
         const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
-        i32x16 acc[2][NP];
         uint32_t lo[4], hi[4];
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) {
@@ -1635,8 +1662,12 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
             }
             hook(kk);
         }
-        // the combine: U on the f16 MFMA (A = [S & 63, S >> 6] of the lane's column, B = [m, 64 m]
-        // of its row), then mmqx_term per element, folded into this half's sum
+    };
+    // the combine of superblock sb from acc: U on the f16 MFMA (A = [S & 63, S >> 6] of the lane's
+    // column from xup, B = [m, 64 m] of its row from the header at hdrp), then mmqx_term per element
+    // (d_a from dal), folded into this half's sum
+    auto combine = [&](const char * hdrp, const char * xup, const float * dal, int sb) {
+        const uint4 hdr = *(const uint4 *) hdrp;
         const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
         const uint32_t ma = hdr.z & 0x3F3F3F3Fu;
         const uint32_t mb = ((hdr.w >> 4) & 0x0F0F0F0Fu) | ((hdr.z >> 2) & 0x30303030u);
@@ -1651,13 +1682,12 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         const bool fold = sb < sb_end;  // wave-uniform
 #pragma unroll
         for (int ct = 0; ct < 2; ct++) {
-            const half8 xu = *(const half8 *) (hb + XB + 1024 * ct + xoff0);
+            const half8 xu = *(const half8 *) (xup + 1024 * ct);
             const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
-            const float * dal = (const float *) (hb + XB + UB + WB) + 32 * ct;
             f32x16 tv;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                const float2 d2 = *(const float2 *) &dal[8 * (j >> 1) + 4 * h + 2 * (j & 1)];
+                const float2 d2 = *(const float2 *) &dal[32 * ct + 8 * (j >> 1) + 4 * h + 2 * (j & 1)];
                 const float dav[2] = {d2.x, d2.y};
 #pragma unroll
                 for (int e = 0; e < 2; e++) {
@@ -1682,26 +1712,37 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
             }
         }
     };
+    auto combine_stage = [&](int buf, int sb) {  // operands from the stage buffer
+        const char * hb = lds + buf * SB + kh * HB;
+        combine(lds + buf * SB + woff, hb + XB + xoff0, (const float *) (hb + XB + UB + WB), sb);
+    };
+    auto combine_ring = [&](int u, int sb) {  // SKEW, high half: operands from ring slot u % 3
+        const char * rs = lds + RING + (u % 3) * RS;
+        combine(rs + (32 * rw + r) * 16, rs + BM * 16 + xoff0, (const float *) (rs + BM * 16 + UB), sb);
+    };
 
-    stage_dma(0, 0);
+    const bool late = SKEW && kh;  // wave-uniform: this wave folds one step late
+    const int sb0 = kh ? SK : 0;
+    stage_dma(0);
     stage_wait();
     for (int u = 0; u < SK; u++) {
-        // the next stage's DMAs (past the end: clamped re-reads into the idle buffer)
-        if constexpr (DI) {  // one piece behind each 32-deep step's MFMAs, the rest after the last
-            step(u & 1, (kh ? SK : 0) + u, [&](int kk) {
-                if (kk < 7) {
-                    stage_piece(u + 1, (u + 1) & 1, kk);
-                } else {
+        if (late && u > 0) combine_ring(u - 1, sb0 + u - 1);
+        __builtin_amdgcn_sched_barrier(0);  // (keeps the two phases' registers apart)
+        // the next stage's DMAs (past the end: clamped re-reads into the idle buffer), one piece
+        // behind each 32-deep step's MFMAs, the rest after the last
+        mfma(u & 1, [&](int kk) {
+            if (kk < 7) {
+                stage_piece(u + 1, kk);
+            } else {
 #pragma unroll
-                    for (int i = 7; i <= NI; i++) stage_piece(u + 1, (u + 1) & 1, i);
-                }
-            });
-        } else {  // all at the step's start
-            stage_dma(u + 1, (u + 1) & 1);
-            step(u & 1, (kh ? SK : 0) + u, [](int) {});
-        }
+                for (int i = 7; i <= NI + NX; i++) stage_piece(u + 1, i);
+            }
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        if (!late) combine_stage(u & 1, sb0 + u);
         stage_wait();
     }
+    if (late) combine_ring(SK - 1, sb0 + SK - 1);
 
     // the halves meet: waves 4-7 leave their sums in LDS (the stage buffers are idle: every DMA
     // has landed and every wave has passed the last barrier), waves 0-3 add and store
@@ -2566,12 +2607,13 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         else hipLaunchKernelGGL((k_mmqx<13, false, 0, 2, 0, 4>), grid4, dim3(256), 0, s, g);
         return;
     }
-    // Q4_K: K split over wave pairs, 128 x 64 tiles (k_mmqt, the default; mmq_long 6: its DMAs at
-    // the step start; B=512 33.4 vs 36.6 us for k_mmqw, B=256 18.5 vs 19.7, profiles/r04i_pf_long_mmqt.txt)
+    // Q4_K: K split over wave pairs, 128 x 64 tiles (k_mmqt, the default; B=512 33.4 vs 36.6 us for
+    // k_mmqw, B=256 18.5 vs 19.7, profiles/r04i_pf_long_mmqt.txt; its DMAs all at the step start
+    // instead of one behind each MFMA step: 37.1 us). mmq_long 7: the skewed halves.
     const int lng = g_mi_tuning.mmq_long;
-    if ((lng == 0 || lng == 2 || lng == 6) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
+    if ((lng == 0 || lng == 2 || lng == 7) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
-        if (lng != 6) hipLaunchKernelGGL((k_mmqt<12, true>), gridt, dim3(512), 0, s, g);
+        if (lng == 7) hipLaunchKernelGGL((k_mmqt<12, true>), gridt, dim3(512), 0, s, g);
         else hipLaunchKernelGGL((k_mmqt<12, false>), gridt, dim3(512), 0, s, g);
         return;
     }
