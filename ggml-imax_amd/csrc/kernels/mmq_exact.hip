@@ -1507,14 +1507,11 @@ __device__ __forceinline__ uint32_t mi_lds_addr(const void * p) {
     return (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (uintptr_t) p);
 }
 
-// SKEW: the high-half waves fold superblock u's terms while the low-half waves run superblock
-// u + 1's MFMAs (and the other way round), so the two waves of a SIMD -- w and w + 4, the two halves
-// of the same rows -- alternate between the matrix pipe and the VALU instead of running the same
-// phase in lock step after every barrier. The high half's combine operands (its rows' block headers,
-// the U halves and d_a of its superblock) then live in a ring of three LDS slots, written by the
-// stage's DMAs and read one step later, after the double-buffered stage they came with has been
-// restaged.
-template <int TYPE, bool SKEW>
+// ABL (diagnostic builds only, results invalid): 8 s_memtime stamps of waves 0 and 4 of workgroups 0
+// and 97 into dst as uint64 [2][2][80] (0 start, 1 after the prologue, 2 + 4 u + {0 step start, 1
+// after the MFMA steps, 2 after the combine, 3 after the DMA wait}); 1 no weight DMAs after the
+// prologue, 2 no combine, 4 no DMAs at all after the prologue (profiles/r04l_mmqt_stamps.txt).
+template <int TYPE, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -1530,9 +1527,7 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     constexpr int NPIECE = (XB + UB + WB) / 1024;  // 1-KB DMA pieces per half (36)
     static_assert((XB + UB + WB) % 1024 == 0 && (2 * NPIECE) % 8 == 0, "whole pieces, evenly dealt");
     constexpr int NI = 2 * NPIECE / 8;        // pieces per wave and stage (9)
-    constexpr int RS = BM * 16 + UB + DB;     // SKEW ring slot: [headers | U halves | d_a] of the high half
-    constexpr int RING = 2 * SB;
-    constexpr int SINK = RING + (SKEW ? 3 * RS : 0);  // d_a DMAs of waves 2-7 land here
+    constexpr int SINK = 2 * SB;              // d_a DMAs of waves 2-7 land here
     __shared__ __attribute__((aligned(16))) char lds[SINK + DB];
 
     const int tid = (int) threadIdx.x;
@@ -1550,26 +1545,14 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     auto col_of = [&](int c) { return (uint32_t) std::min<int64_t>(c0 + c, ncols - 1); };
 
     // ---- staging: piece q = w + 8 i of a stage (half q / NPIECE, piece t = q % NPIECE of the half):
-    // a wave-uniform global base and superblock stride, a per-lane 32-bit offset. SKEW: the high
-    // half's U pieces go to the ring slot, and waves 0 and 1 move its rows' 16-byte headers there
-    // too (pieces 72, 73: 64 rows each).
-    constexpr int NX = SKEW ? 1 : 0;          // extra pieces per wave (waves 0, 1)
-    const char * pbase[NI + NX];
-    uint32_t pstride[NI + NX], poff[NI + NX], pdst[NI + NX];
-    bool pring[NI + NX];
+    // a wave-uniform global base and superblock stride, a per-lane 32-bit offset
+    const char * pbase[NI];
+    uint32_t pstride[NI], poff[NI], pdst[NI];
 #pragma unroll
-    for (int i = 0; i < NI + NX; i++) {
+    for (int i = 0; i < NI; i++) {
         const int q = w + 8 * i, hf = q / NPIECE, t = q % NPIECE;
         pdst[i] = (uint32_t) (hf * HB + 1024 * t);
-        pring[i] = false;
-        if (i == NI) {  // SKEW: header piece q - 72 (waves 0, 1; the others re-read it into the sink)
-            const int row = 64 * (w & 1) + lane;
-            pbase[i] = (const char *) W + (size_t) n0 * nb01;
-            pstride[i] = F::BS;
-            poff[i] = (uint32_t) (std::min(row, nrows - 1) * nb01);
-            pdst[i] = (uint32_t) (1024 * (w & 1));
-            pring[i] = true;
-        } else if (t < 16) {  // activation quants: step kk, 32-column group cg
+        if (t < 16) {  // activation quants: step kk, 32-column group cg
             const int kk = t >> 1, cg = t & 1, col = 32 * cg + (lane >> 1);
             pbase[i] = (const char *) act.xq + (size_t) kk * ncols * 32;
             pstride[i] = 8 * (uint32_t) ncols * 32;
@@ -1579,10 +1562,6 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
             pbase[i] = (const char *) act.xu;
             pstride[i] = (uint32_t) ncols * 32;
             poff[i] = col_of(col) * 32 + 16 * ((lane & 1) ^ ((lane >> 5) & 1));
-            if (SKEW && hf == 1) {
-                pdst[i] = (uint32_t) (BM * 16 + 1024 * (t - 16));
-                pring[i] = true;
-            }
         } else {  // raw weight blocks: 1 KB of the [128 rows][BS] image
             const int o = 1024 * (t - 18) + 16 * lane, row = o / F::BS;
             pbase[i] = (const char *) W + (size_t) n0 * nb01;
@@ -1592,30 +1571,42 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     }
     const uint32_t doff = col_of(lane) * 4;
     // stage u: superblock u of the low half, SK + u of the high half (clamped: a high half shorter
-    // than the low one re-reads its last superblock, whose terms are not folded) into buffer u & 1
-    // (and ring slot u % 3). Piece i < NI + NX; i == NI + NX: d_a (wave 0 the low half's, wave 1
-    // the high half's, the others into the sink).
+    // than the low one re-reads its last superblock, whose terms are not folded) into buffer u & 1.
+    // Piece i < NI; i == NI: d_a (wave 0 the low half's, wave 1 the high half's, the others into the
+    // sink).
     auto stage_piece = [&](int u, int i) {
+        if constexpr ((ABL & 4) != 0) if (u > 0) return;
+        if constexpr ((ABL & 1) != 0) if (u > 0 && i < NI && (w + 8 * i) % NPIECE >= 18) return;
         char * sbuf = lds + (u & 1) * SB;
-        char * rslot = lds + RING + (u % 3) * RS;
-        if (i < NI + NX) {
-            const int hf = i == NI ? 1 : (w + 8 * i) / NPIECE;
+        if (i < NI) {
+            const int hf = (w + 8 * i) / NPIECE;
             const int sb = std::min(hf ? SK + u : u, S - 1);
             const char * src = pbase[i] + (size_t) sb * pstride[i] + poff[i];
-            char * dd = (i == NI && w >= 2) ? lds + SINK : (pring[i] ? rslot : sbuf) + pdst[i];
-            mi_glds16(src, mi_lds_addr(dd));
+            mi_glds16(src, mi_lds_addr(sbuf + pdst[i]));
         } else {
             const int sb = std::min(w == 1 ? SK + u : u, S - 1);
             const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
-            char * dd = w >= 2 ? lds + SINK : (SKEW && w == 1) ? rslot + BM * 16 + UB : sbuf + w * HB + XB + UB + WB;
+            char * dd = w >= 2 ? lds + SINK : sbuf + w * HB + XB + UB + WB;
             mi_glds4(src, mi_lds_addr(dd));
         }
     };
     auto stage_dma = [&](int u) {
 #pragma unroll
-        for (int i = 0; i <= NI + NX; i++) stage_piece(u, i);
+        for (int i = 0; i <= NI; i++) stage_piece(u, i);
     };
-    auto stage_wait = [] { asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    auto stamp = [&](int slot) {
+        if constexpr ((ABL & 8) != 0) {
+            const int wsel = blockIdx.x == 0 ? 0 : blockIdx.x == 97 ? 1 : -1;
+            if (wsel >= 0 && (w & 3) == 0 && lane == 0 && slot < 80)
+                ((uint64_t *) dst)[(wsel * 2 + (w >> 2)) * 80 + slot] = __builtin_amdgcn_s_memtime();
+        }
+    };
+    int stamp_slot = 0;
+    auto stage_wait = [&] {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(stamp_slot);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
 
     // ---- compute: rows n0 + 32 rw + r of half kh; tiles ct = columns 32 ct ..
     const uint32_t xoff0 = (uint32_t) (r * 32 + 16 * (h ^ ((r >> 4) & 1)));  // tile 0; tile 1 at + 1024
@@ -1667,6 +1658,10 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     // column from xup, B = [m, 64 m] of its row from the header at hdrp), then mmqx_term per element
     // (d_a from dal), folded into this half's sum
     auto combine = [&](const char * hdrp, const char * xup, const float * dal, int sb) {
+        if constexpr ((ABL & 2) != 0) {  // timing ablation: no combine (keep the accumulators alive)
+            if (acc[0][0][0] == 0x7fffffff && acc[1][1][5] == 0x7fffffff) y[0][0] += 1.0f;
+            return;
+        }
         const uint4 hdr = *(const uint4 *) hdrp;
         const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
         const uint32_t ma = hdr.z & 0x3F3F3F3Fu;
@@ -1716,18 +1711,14 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         const char * hb = lds + buf * SB + kh * HB;
         combine(lds + buf * SB + woff, hb + XB + xoff0, (const float *) (hb + XB + UB + WB), sb);
     };
-    auto combine_ring = [&](int u, int sb) {  // SKEW, high half: operands from ring slot u % 3
-        const char * rs = lds + RING + (u % 3) * RS;
-        combine(rs + (32 * rw + r) * 16, rs + BM * 16 + xoff0, (const float *) (rs + BM * 16 + UB), sb);
-    };
-
-    const bool late = SKEW && kh;  // wave-uniform: this wave folds one step late
     const int sb0 = kh ? SK : 0;
+    stamp(0);
     stage_dma(0);
+    stamp_slot = 1;
     stage_wait();
     for (int u = 0; u < SK; u++) {
-        if (late && u > 0) combine_ring(u - 1, sb0 + u - 1);
-        __builtin_amdgcn_sched_barrier(0);  // (keeps the two phases' registers apart)
+        stamp(2 + 4 * u);
+        stamp_slot = 5 + 4 * u;
         // the next stage's DMAs (past the end: clamped re-reads into the idle buffer), one piece
         // behind each 32-deep step's MFMAs, the rest after the last
         mfma(u & 1, [&](int kk) {
@@ -1735,14 +1726,21 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
                 stage_piece(u + 1, kk);
             } else {
 #pragma unroll
-                for (int i = 7; i <= NI + NX; i++) stage_piece(u + 1, i);
+                for (int i = 7; i <= NI; i++) stage_piece(u + 1, i);
             }
         });
-        __builtin_amdgcn_sched_barrier(0);
-        if (!late) combine_stage(u & 1, sb0 + u);
+        stamp(3 + 4 * u);
+        combine_stage(u & 1, sb0 + u);
+        stamp(4 + 4 * u);
         stage_wait();
     }
-    if (late) combine_ring(SK - 1, sb0 + SK - 1);
+    if constexpr ((ABL & 8) != 0) {  // dst holds the stamps; keep the results alive
+        float t = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; i++) t += y[0][i] + y[1][i];
+        if (t == 1.2345e-30f) dst[8192 + threadIdx.x] = t;
+        return;
+    }
 
     // the halves meet: waves 4-7 leave their sums in LDS (the stage buffers are idle: every DMA
     // has landed and every wave has passed the last barrier), waves 0-3 add and store
@@ -2609,14 +2607,28 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     }
     // Q4_K: K split over wave pairs, 128 x 64 tiles (k_mmqt, the default; B=512 33.4 vs 36.6 us for
     // k_mmqw, B=256 18.5 vs 19.7, profiles/r04i_pf_long_mmqt.txt; its DMAs all at the step start
-    // instead of one behind each MFMA step: 37.1 us). mmq_long 7: the skewed halves.
+    // instead of one behind each MFMA step: 37.1 us; the high half folding one step late from a
+    // 3-slot LDS ring, so the two waves of a SIMD alternate MFMA and VALU phases: 38.7 us,
+    // profiles/r04k_mmqt_skew_ab.txt, r04m_mmqt_skew_stamps.txt -- both removed)
     const int lng = g_mi_tuning.mmq_long;
-    if ((lng == 0 || lng == 2 || lng == 7) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
+    if ((lng == 0 || lng == 2) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
-        if (lng == 7) hipLaunchKernelGGL((k_mmqt<12, true>), gridt, dim3(512), 0, s, g);
-        else hipLaunchKernelGGL((k_mmqt<12, false>), gridt, dim3(512), 0, s, g);
+        hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
         return;
     }
+#if MI_DIAG
+    if (lng >= 16 && lng < 24 && type == 12) {  // k_mmqt stamps (+ ablation bits lng - 16; results invalid)
+        const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
+        switch (lng - 16) {
+            case 1: hipLaunchKernelGGL((k_mmqt<12, 9>), gridt, dim3(512), 0, s, g); break;
+            case 2: hipLaunchKernelGGL((k_mmqt<12, 10>), gridt, dim3(512), 0, s, g); break;
+            case 4: hipLaunchKernelGGL((k_mmqt<12, 12>), gridt, dim3(512), 0, s, g); break;
+            case 6: hipLaunchKernelGGL((k_mmqt<12, 14>), gridt, dim3(512), 0, s, g); break;
+            default: hipLaunchKernelGGL((k_mmqt<12, 8>), gridt, dim3(512), 0, s, g); break;
+        }
+        return;
+    }
+#endif
     if (g_mi_tuning.mmq_long == 3 || g_mi_tuning.mmq_long == 4) {  // shared operands staged in LDS (4: rolled loop)
         const dim3 gridr((unsigned) mmx_deal(g, 128, 64));
         if (g_mi_tuning.mmq_long == 4 && (K / 256) % 2 == 0) {
