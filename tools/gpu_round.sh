@@ -27,6 +27,6 @@ find "$OUT/prof_gpt2" -name '*kernel_stats.csv' -exec cp {} "$OUT/gpt2_kernel_st
 cat "$OUT/gpt2_prof.log" | tail -4
 # GPT-2 per-kernel decode durations over the last tokens
 bash tools/gpt2_trace.sh "$TAG/gpt2_trace" 51 | tail -12
-# prefill GEMM counters (k_mmqx at B = 512): MFMA busy, VALU per MFMA, waits
-timeout -k 10 300 python tools/pmc_kernel.py "$OUT/pmc_mmqx" k_mmqx "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS;SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM GRBM_GUI_ACTIVE;SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM" -- python3 tools/prefill_bench.py 512 > "$OUT/mmqx_pmc.txt" 2>&1
-grep -E "MFMA|VALU" "$OUT/mmqx_pmc.txt" | head -6
+# prefill GEMM counters (k_mmqt, the Q4_K default at B = 512): MFMA busy, VALU per MFMA, waits
+timeout -k 10 300 python tools/pmc_kernel.py "$OUT/pmc_mmqt" k_mmqt "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS;SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM GRBM_GUI_ACTIVE;SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM" -- python3 tools/prefill_bench.py 512 > "$OUT/mmqt_pmc.txt" 2>&1
+grep -E "MFMA|VALU" "$OUT/mmqt_pmc.txt" | head -6
