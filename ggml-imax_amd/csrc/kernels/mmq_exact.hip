@@ -1502,6 +1502,25 @@ __device__ __forceinline__ void mi_glds4(const void * gsrc, uint32_t lds) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(gsrc), "s"(lds));
 }
+// The same through a buffer descriptor: per-lane 32-bit offset voff + wave-uniform soff (no
+// per-lane address arithmetic per load)
+// A raw buffer descriptor as four wave-uniform dwords (base, num_records; no stride, the flags of
+// __builtin_amdgcn_make_buffer_rsrc(..., 0x00020000)), so inline asm can take it as an SGPR quad.
+__device__ __forceinline__ i32x4 mi_rsrc(const void * base, uint32_t bytes) {
+    const uint64_t a = (uint64_t) (uintptr_t) base;
+    return i32x4{__builtin_amdgcn_readfirstlane((int) (uint32_t) a), __builtin_amdgcn_readfirstlane((int) ((uint32_t) (a >> 32) & 0xFFFF)),
+                 __builtin_amdgcn_readfirstlane((int) bytes), 0x00020000};
+}
+__device__ __forceinline__ void mi_blds16(i32x4 rs, uint32_t voff, uint32_t soff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds), "s"(soff));
+}
+__device__ __forceinline__ void mi_blds4(i32x4 rs, uint32_t voff, uint32_t soff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds), "s"(soff));
+}
 // LDS byte address of a __shared__ location (the low 32 bits of its flat address), wave-uniform
 __device__ __forceinline__ uint32_t mi_lds_addr(const void * p) {
     return (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (uintptr_t) p);
@@ -1511,7 +1530,9 @@ __device__ __forceinline__ uint32_t mi_lds_addr(const void * p) {
 // and 97 into dst as uint64 [2][2][80] (0 start, 1 after the prologue, 2 + 4 u + {0 step start, 1
 // after the MFMA steps, 2 after the combine, 3 after the DMA wait}); 1 no weight DMAs after the
 // prologue, 2 no combine, 4 no DMAs at all after the prologue (profiles/r04l_mmqt_stamps.txt).
-template <int TYPE, int ABL = 0>
+// BUF: the DMAs through buffer descriptors (SGPR superblock offsets) instead of per-lane 64-bit
+// addresses.
+template <int TYPE, int ABL = 0, bool BUF = false>
 __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -1570,6 +1591,13 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         }
     }
     const uint32_t doff = col_of(lane) * 4;
+    // BUF: descriptors of the activation quants, U halves, weight rows (this tile's) and d_a; piece
+    // i's byte offset = its per-lane part (poff) + a wave-uniform part (sbase + sb * pstride)
+    // (descriptors built at each use from uniform values: SGPR quads the asm can take)
+    auto xres = [&] { return mi_rsrc(act.xq, (uint32_t) (K * ncols)); };
+    auto ures = [&] { return mi_rsrc(act.xu, (uint32_t) (S * ncols * 32)); };
+    auto wres = [&] { return mi_rsrc(W + (size_t) n0 * nb01, (uint32_t) ((size_t) nrows * nb01)); };
+    auto dres = [&] { return mi_rsrc(act.xd, (uint32_t) (S * ncols * 4)); };
     // stage u: superblock u of the low half, SK + u of the high half (clamped: a high half shorter
     // than the low one re-reads its last superblock, whose terms are not folded) into buffer u & 1.
     // Piece i < NI; i == NI: d_a (wave 0 the low half's, wave 1 the high half's, the others into the
@@ -1579,15 +1607,29 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         if constexpr ((ABL & 1) != 0) if (u > 0 && i < NI && (w + 8 * i) % NPIECE >= 18) return;
         char * sbuf = lds + (u & 1) * SB;
         if (i < NI) {
-            const int hf = (w + 8 * i) / NPIECE;
+            const int q = w + 8 * i, hf = q / NPIECE, t = q % NPIECE;
             const int sb = std::min(hf ? SK + u : u, S - 1);
-            const char * src = pbase[i] + (size_t) sb * pstride[i] + poff[i];
-            mi_glds16(src, mi_lds_addr(sbuf + pdst[i]));
+            if constexpr (BUF) {
+                // wave-uniform: the kk offset of an activation piece, the superblock offset
+                const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(
+                    (int) ((t < 16 ? (uint32_t) (t >> 1) * (uint32_t) ncols * 32 : 0u) + (uint32_t) sb * pstride[i]));
+                const uint32_t ld = mi_lds_addr(sbuf + pdst[i]);
+                if (t < 16) mi_blds16(xres(), poff[i], so, ld);
+                else if (t < 18) mi_blds16(ures(), poff[i], so, ld);
+                else mi_blds16(wres(), poff[i], so, ld);
+            } else {
+                const char * src = pbase[i] + (size_t) sb * pstride[i] + poff[i];
+                mi_glds16(src, mi_lds_addr(sbuf + pdst[i]));
+            }
         } else {
             const int sb = std::min(w == 1 ? SK + u : u, S - 1);
-            const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
             char * dd = w >= 2 ? lds + SINK : sbuf + w * HB + XB + UB + WB;
-            mi_glds4(src, mi_lds_addr(dd));
+            if constexpr (BUF) {
+                mi_blds4(dres(), doff, (uint32_t) __builtin_amdgcn_readfirstlane((int) ((uint32_t) sb * (uint32_t) ncols * 4)), mi_lds_addr(dd));
+            } else {
+                const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
+                mi_glds4(src, mi_lds_addr(dd));
+            }
         }
     };
     auto stage_dma = [&](int u) {
@@ -2611,9 +2653,10 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     // 3-slot LDS ring, so the two waves of a SIMD alternate MFMA and VALU phases: 38.7 us,
     // profiles/r04k_mmqt_skew_ab.txt, r04m_mmqt_skew_stamps.txt -- both removed)
     const int lng = g_mi_tuning.mmq_long;
-    if ((lng == 0 || lng == 2) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
+    if ((lng == 0 || lng == 2 || lng == 5) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
-        hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
+        if (lng == 5) hipLaunchKernelGGL((k_mmqt<12, 0, true>), gridt, dim3(512), 0, s, g);  // buffer-descriptor DMAs (A/B)
+        else hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
         return;
     }
 #if MI_DIAG
