@@ -1531,8 +1531,10 @@ __device__ __forceinline__ uint32_t mi_lds_addr(const void * p) {
 // after the MFMA steps, 2 after the combine, 3 after the DMA wait}); 1 no weight DMAs after the
 // prologue, 2 no combine, 4 no DMAs at all after the prologue (profiles/r04l_mmqt_stamps.txt).
 // BUF: the DMAs through buffer descriptors (SGPR superblock offsets) instead of per-lane 64-bit
-// addresses.
-template <int TYPE, int ABL = 0, bool BUF = false>
+// addresses. SPLIT: the two column tiles' MFMAs in two passes over the dequantized planes (held in
+// registers), the first tile's combine interleaved with the second tile's MFMAs, so half of the
+// combine's VALU runs beside the matrix pipe instead of after it.
+template <int TYPE, int ABL = 0, bool BUF = false, bool SPLIT = false>
 __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -1753,6 +1755,97 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         const char * hb = lds + buf * SB + kh * HB;
         combine(lds + buf * SB + woff, hb + XB + xoff0, (const float *) (hb + XB + UB + WB), sb);
     };
+    // SPLIT: one whole step (MFMAs + combine) from stage buffer buf
+    auto fold_tile = [&](int ct, const f32x16 & tv, int sb) {
+        if (sb >= sb_end) return;  // wave-uniform
+        const int pos = sb % gs;
+        if (pos == 0) {
+            asm volatile("" ::: "memory");
+            gsum[ct] = f32x16(-0.0f);
+        }
+        gsum[ct] = gsum[ct] + tv;
+        if (pos == gs - 1 || sb == S - 1) {
+            asm volatile("" ::: "memory");
+            y[ct] = y[ct] + gsum[ct];
+        }
+    };
+    auto step_split = [&](int buf, int sb, auto && hook) {
+        const char * base = lds + buf * SB;
+        const char * hb = base + kh * HB;
+        const char * wr = base + woff;
+        const uint4 hdr = *(const uint4 *) wr;
+        uint4 q4[4];
+#pragma unroll
+        for (int p = 0; p < 4; p++) q4[p] = *(const uint4 *) (wr + kQs + 32 * p + 16 * h);
+        const uint32_t w0 = hdr.y, w2 = hdr.w;
+        const uint32_t sca = w0 & 0x3F3F3F3Fu;
+        const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
+        i32x4 bq[8][NP];
+        uint32_t lo[4], hi[4];
+        // pass 1: tile 0, dequantizing every plane fragment once
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const i32x4 xa0 = *(const i32x4 *) (hb + kk * (BN * 32) + xoff0);
+            if ((kk & 1) == 0) {
+                const uint4 q = q4[kk >> 1];
+                const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    lo[e] = qv[e] & 0x0F0F0F0Fu;
+                    hi[e] = (qv[e] >> 4) & 0x0F0F0F0Fu;
+                }
+            }
+            const uint32_t scw = kk < 4 ? sca : scb;
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                const uint32_t f = __builtin_amdgcn_ubfe(scw, 8 * (kk & 3) + 3 * p, 3);
+                const uint32_t * v = (kk & 1) ? hi : lo;
+                bq[kk][p] = i32x4{(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+                acc[0][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa0, bq[kk][p], kk == 0 ? i32x16{} : acc[0][p], 0, 0, 0);
+            }
+            hook(kk);
+        }
+        // the combine's row operands and tile 0's U
+        const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
+        const uint32_t ma = hdr.z & 0x3F3F3F3Fu;
+        const uint32_t mb = ((hdr.w >> 4) & 0x0F0F0F0Fu) | ((hdr.z >> 2) & 0x30303030u);
+        const uint32_t mw = h ? mb : ma;
+        half8 mu;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t m = (mw >> (8 * q)) & 0xFF;
+            mu[2 * q] = (_Float16) (float) m;
+            mu[2 * q + 1] = (_Float16) (float) (64 * m);
+        }
+        const float * dal = (const float *) (hb + XB + UB + WB);
+        auto terms = [&](int ct, const f32x16 & Uv, f32x16 & tv, int j) {  // elements 2 j, 2 j + 1
+            const float2 d2 = *(const float2 *) &dal[32 * ct + 8 * (j >> 1) + 4 * h + 2 * (j & 1)];
+            const float dav[2] = {d2.x, d2.y};
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int el = 2 * j + e;
+                const int T = (acc[ct][1][el] << F::SHIFT) + acc[ct][0][el];
+                tv[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
+            }
+        };
+        const f32x16 Uv0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8 *) (hb + XB + xoff0), mu, f32x16{}, 0, 0, 0);
+        // pass 2: tile 1 from the held planes, tile 0's terms between its MFMA steps
+        f32x16 tv0;
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const i32x4 xa1 = *(const i32x4 *) (hb + kk * (BN * 32) + 1024 + xoff0);
+#pragma unroll
+            for (int p = 0; p < NP; p++)
+                acc[1][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa1, bq[kk][p], kk == 0 ? i32x16{} : acc[1][p], 0, 0, 0);
+            terms(0, Uv0, tv0, kk);
+        }
+        fold_tile(0, tv0, sb);
+        const f32x16 Uv1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8 *) (hb + XB + 1024 + xoff0), mu, f32x16{}, 0, 0, 0);
+        f32x16 tv1;
+#pragma unroll
+        for (int j = 0; j < 8; j++) terms(1, Uv1, tv1, j);
+        fold_tile(1, tv1, sb);
+    };
     const int sb0 = kh ? SK : 0;
     stamp(0);
     stage_dma(0);
@@ -1763,17 +1856,24 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         stamp_slot = 5 + 4 * u;
         // the next stage's DMAs (past the end: clamped re-reads into the idle buffer), one piece
         // behind each 32-deep step's MFMAs, the rest after the last
-        mfma(u & 1, [&](int kk) {
+        auto dma_hook = [&](int kk) {
             if (kk < 7) {
                 stage_piece(u + 1, kk);
             } else {
 #pragma unroll
                 for (int i = 7; i <= NI; i++) stage_piece(u + 1, i);
             }
-        });
-        stamp(3 + 4 * u);
-        combine_stage(u & 1, sb0 + u);
-        stamp(4 + 4 * u);
+        };
+        if constexpr (SPLIT) {
+            step_split(u & 1, sb0 + u, dma_hook);
+            stamp(3 + 4 * u);
+            stamp(4 + 4 * u);
+        } else {
+            mfma(u & 1, dma_hook);
+            stamp(3 + 4 * u);
+            combine_stage(u & 1, sb0 + u);
+            stamp(4 + 4 * u);
+        }
         stage_wait();
     }
     if constexpr ((ABL & 8) != 0) {  // dst holds the stamps; keep the results alive
@@ -2653,9 +2753,10 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     // 3-slot LDS ring, so the two waves of a SIMD alternate MFMA and VALU phases: 38.7 us,
     // profiles/r04k_mmqt_skew_ab.txt, r04m_mmqt_skew_stamps.txt -- both removed)
     const int lng = g_mi_tuning.mmq_long;
-    if ((lng == 0 || lng == 2 || lng == 5) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
+    if ((lng == 0 || lng == 2 || lng == 5 || lng == 6) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
         if (lng == 5) hipLaunchKernelGGL((k_mmqt<12, 0, true>), gridt, dim3(512), 0, s, g);  // buffer-descriptor DMAs (A/B)
+        else if (lng == 6) hipLaunchKernelGGL((k_mmqt<12, 0, true, true>), gridt, dim3(512), 0, s, g);  // + split tiles (A/B)
         else hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
         return;
     }
