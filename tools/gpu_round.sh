@@ -15,7 +15,7 @@ fi
 timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-  python3 bench.py --steps 50 --warmup 10 --no-cpu --no-gpt2 > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+  python3 bench.py --steps 50 --warmup 10 --no-cpu --no-gpt2 --no-sweep > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 head -8 "$OUT/kernel_stats.csv" | cut -c1-200
 timeout -k 10 300 python tools/pmc_traffic.py --tag "$TAG" > "$OUT/pmc.log" 2>&1
