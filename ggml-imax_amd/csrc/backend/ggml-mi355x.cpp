@@ -2812,7 +2812,7 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.mmq_variant = value;
         return true;
     }
-    if (strcmp(name, "mmq_long") == 0 && value >= 0 && value <= 23) {  // (16-23: diagnostic builds only)
+    if (strcmp(name, "mmq_long") == 0 && value >= 0 && value <= 23) {  // (8-15 unused; 16-23: diagnostic builds only)
         g_mi_tuning.mmq_long = value;
         return true;
     }

@@ -1531,10 +1531,12 @@ __device__ __forceinline__ uint32_t mi_lds_addr(const void * p) {
 // after the MFMA steps, 2 after the combine, 3 after the DMA wait}); 1 no weight DMAs after the
 // prologue, 2 no combine, 4 no DMAs at all after the prologue (profiles/r04l_mmqt_stamps.txt).
 // BUF: the DMAs through buffer descriptors (SGPR superblock offsets) instead of per-lane 64-bit
-// addresses. SPLIT: the two column tiles' MFMAs in two passes over the dequantized planes (held in
+// addresses. SPLIT 1: the two column tiles' MFMAs in two passes over the dequantized planes (held in
 // registers), the first tile's combine interleaved with the second tile's MFMAs, so half of the
-// combine's VALU runs beside the matrix pipe instead of after it.
-template <int TYPE, int ABL = 0, bool BUF = false, bool SPLIT = false>
+// combine's VALU runs beside the matrix pipe instead of after it; 2: also the second tile's combine,
+// deferred into the next step's first pass (its operands -- exact T, U, d_a, d_w, dmin -- carried
+// across the barrier in registers).
+template <int TYPE, int ABL = 0, bool BUF = false, int SPLIT = 0>
 __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -1769,6 +1771,11 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
             y[ct] = y[ct] + gsum[ct];
         }
     };
+    // SPLIT 2: tile 1's combine operands of the previous step
+    i32x16 dT = {};
+    f32x16 dU = {}, dA = {}, dtv;
+    float ddw = 0.0f, ddm = 0.0f;
+    int dsb = -1;  // wave-uniform; -1: nothing pending
     auto step_split = [&](int buf, int sb, auto && hook) {
         const char * base = lds + buf * SB;
         const char * hb = base + kh * HB;
@@ -1804,6 +1811,15 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
                 acc[0][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa0, bq[kk][p], kk == 0 ? i32x16{} : acc[0][p], 0, 0, 0);
             }
             hook(kk);
+            if constexpr (SPLIT == 2) {  // the previous step's tile-1 terms 2 kk, 2 kk + 1
+                if (dsb >= 0) {
+#pragma unroll
+                    for (int e = 0; e < 2; e++) dtv[2 * kk + e] = mmqx_term(dT[2 * kk + e], dU[2 * kk + e], ddw, ddm, dA[2 * kk + e]);
+                }
+            }
+        }
+        if constexpr (SPLIT == 2) {
+            if (dsb >= 0) fold_tile(1, dtv, dsb);
         }
         // the combine's row operands and tile 0's U
         const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
@@ -1841,10 +1857,32 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         }
         fold_tile(0, tv0, sb);
         const f32x16 Uv1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8 *) (hb + XB + 1024 + xoff0), mu, f32x16{}, 0, 0, 0);
-        f32x16 tv1;
+        if constexpr (SPLIT == 2) {  // tile 1's operands into registers: its terms run in the next step
 #pragma unroll
-        for (int j = 0; j < 8; j++) terms(1, Uv1, tv1, j);
-        fold_tile(1, tv1, sb);
+            for (int j = 0; j < 8; j++) {
+                const float2 d2 = *(const float2 *) &dal[32 + 8 * (j >> 1) + 4 * h + 2 * (j & 1)];
+                dA[2 * j] = d2.x;
+                dA[2 * j + 1] = d2.y;
+            }
+#pragma unroll
+            for (int el = 0; el < 16; el++) dT[el] = (acc[1][1][el] << F::SHIFT) + acc[1][0][el];
+            dU = Uv1;
+            ddw = dw;
+            ddm = dm;
+            dsb = sb;
+        } else {
+            f32x16 tv1;
+#pragma unroll
+            for (int j = 0; j < 8; j++) terms(1, Uv1, tv1, j);
+            fold_tile(1, tv1, sb);
+        }
+    };
+    auto finish_split = [&] {  // SPLIT 2: the last step's tile-1 terms
+        if constexpr (SPLIT == 2) {
+#pragma unroll
+            for (int el = 0; el < 16; el++) dtv[el] = mmqx_term(dT[el], dU[el], ddw, ddm, dA[el]);
+            fold_tile(1, dtv, dsb);
+        }
     };
     const int sb0 = kh ? SK : 0;
     stamp(0);
@@ -1864,7 +1902,7 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
                 for (int i = 7; i <= NI; i++) stage_piece(u + 1, i);
             }
         };
-        if constexpr (SPLIT) {
+        if constexpr (SPLIT != 0) {
             step_split(u & 1, sb0 + u, dma_hook);
             stamp(3 + 4 * u);
             stamp(4 + 4 * u);
@@ -1876,6 +1914,7 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         }
         stage_wait();
     }
+    finish_split();
     if constexpr ((ABL & 8) != 0) {  // dst holds the stamps; keep the results alive
         float t = 0.0f;
 #pragma unroll
@@ -2753,10 +2792,11 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     // 3-slot LDS ring, so the two waves of a SIMD alternate MFMA and VALU phases: 38.7 us,
     // profiles/r04k_mmqt_skew_ab.txt, r04m_mmqt_skew_stamps.txt -- both removed)
     const int lng = g_mi_tuning.mmq_long;
-    if ((lng == 0 || lng == 2 || lng == 5 || lng == 6) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
+    if ((lng == 0 || lng == 2 || (lng >= 5 && lng <= 7)) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
         if (lng == 5) hipLaunchKernelGGL((k_mmqt<12, 0, true>), gridt, dim3(512), 0, s, g);  // buffer-descriptor DMAs (A/B)
-        else if (lng == 6) hipLaunchKernelGGL((k_mmqt<12, 0, true, true>), gridt, dim3(512), 0, s, g);  // + split tiles (A/B)
+        else if (lng == 6) hipLaunchKernelGGL((k_mmqt<12, 0, true, 1>), gridt, dim3(512), 0, s, g);  // + split tiles (A/B)
+        else if (lng == 7) hipLaunchKernelGGL((k_mmqt<12, 0, true, 2>), gridt, dim3(512), 0, s, g);  // + tile 1 deferred (A/B)
         else hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
         return;
     }

@@ -12,5 +12,5 @@ for spec in "q4_K 4096 4096 32 21:0,31:0,21:2048,31:2048" "q4_K 4096 11008 14 21
   echo "== $1 ${2}x${3} R=$4" | tee -a $OUT/sweep.txt
   timeout -k 10 150 python3 -u tools/mmv_tune.py --variants $5 --rounds 9 --type $1 --K $2 --N $3 --rotate $4 2>&1 | grep -v amdgpu.ids | tee -a $OUT/sweep.txt
 done
-PF_SINGLE=0 PF_R=16 PF_TYPES=q4_K PF_LONG=0,6,0,6 MMQ_VARIANTS=0 timeout -k 10 300 python3 -u tools/prefill_bench.py 512 256 2>&1 | grep --line-buffered -v amdgpu.ids | tee $OUT/pf.txt
+PF_SINGLE=0 PF_R=16 PF_TYPES=q4_K PF_LONG=0,6,7,0,6,7 MMQ_VARIANTS=0 timeout -k 10 300 python3 -u tools/prefill_bench.py 512 256 2>&1 | grep --line-buffered -v amdgpu.ids | tee $OUT/pf.txt
 timeout -k 10 300 python -u -m pytest tests/test_prefill_gpu.py -x -q --timeout 200 --timeout-method thread -m gpu -k "split_k or bit_equal" > $OUT/pytest.log 2>&1 && tail -1 $OUT/pytest.log || { grep -E "FAILED|^E " $OUT/pytest.log | head -20; tail -1 $OUT/pytest.log; exit 1; }
