@@ -21,6 +21,8 @@
 // ggml_vec_dot_q4_K_q8_K (src/ggml-quants.c:7007-7502), ggml_vec_dot_q5_K_q8_K (:7833-8378),
 // ggml_vec_dot_q4_0_q8_0 (:3469-3874), ggml_vec_dot_q8_0_q8_0 (:4819+) up to summation order.
 
+#include <type_traits>
+
 #include "mi355x_common.h"
 #include "mi355x_kernels.h"
 
@@ -828,6 +830,9 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
     // in its graph 7.96 -> 6.57 us, profiles/r04e_pf_single_blocks.txt)
     int target = g_mi_tuning.mmv_blocks > 0 ? g_mi_tuning.mmv_blocks : resident_blocks(fn, lds);
     if (g_mi_tuning.mmv_blocks <= 0 && g.n == 1 && g.K >= 4096) target = std::min(target, mi_cu_count());
+    // Q5_K grouped launches: twice the resident count (smaller workgroups, a later tail; 4096 x 11008
+    // 5.56 -> 5.75 TB/s, r04r_gemv_sweep.txt)
+    else if (g_mi_tuning.mmv_blocks <= 0 && std::is_same<F, FmtKQ<true>>::value && !ORD && !PRO) target *= 2;
     int bpm = target / g.n;
     if (bpm < 1) bpm = 1;
     int64_t rows = (g.N + bpm - 1) / bpm;
@@ -933,9 +938,11 @@ static void mi_mul_mat_q_fused_launch(mi_mmv_group & g, hipStream_t s) {
     // prefetch depth 2 for Q4_K / Q8_0 / Q4_0 (Q4_0 in block pairs: 4096 x 11008 5.34 -> 5.58
     // TB/s), depth 1 for Q5_K (fewer VGPRs, more waves)
     // (Nontemporal weight loads -- the guide's nt-weights -- measured 30-37 % SLOWER on every
-    // shape, profiles/r04g_nt_ab.txt: removed.)
+    // shape, profiles/r04g_nt_ab.txt: removed.) Round-4 defaults from two interleaved sweeps on two
+    // boxes (profiles/r04p_gemv_sweep.txt, r04r_gemv_sweep.txt): Q4_K depth 3 (4096^2 +2..4 %,
+    // 4096 x 11008 +2..4 %), Q5_K depth 2 (+2 %), Q4_0 pairs depth 3 (+1..4 %), Q8_0 depth 1 (+1 %)
     int variant = g_mi_tuning.mmv_variant;
-    if (variant == 0) variant = (g.type == 12 || g.type == 8) ? 21 : (g.type == 2 ? 22 : 11);
+    if (variant == 0) variant = g.type == 12 ? 31 : g.type == 13 ? 21 : g.type == 2 ? 32 : 11;
     switch (g.type) {
         case 12: launch_stream_ord<FmtKQ<false>>(g, variant, s); break;
         case 13: launch_stream_ord<FmtKQ<true>>(g, variant, s); break;
