@@ -1209,274 +1209,19 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
     }
 }
 
-// ---- long prompts, shared operands staged in LDS, weights dequantized in registers: k_mmqs --------
-// (Round 4's first register-dequant kernel loaded every operand per wave straight from L2 -- the
-// activations 4x, the weights 2x per CU: ~123 KB per superblock step -- and measured 43.8 us at
-// B = 512, load-path bound, profiles/r04a_pf_long_mmqr.txt; removed.) Here the workgroup stages each
-// superblock's operands ONCE into LDS -- the activation quants of its 64 columns [8 steps][64][32]
-// (16 KB), their U halves and scales, and the raw weight blocks of its 128 rows (18 KB) -- and every
-// wave reads its fragments from LDS, then dequantizes its own 32 rows' planes in registers (k_mmqp's
-// step) and runs its 32 x 32 tile.
-// Pipeline: the staging loads of superblock s + 2 are issued as step s starts and written into
-// the free LDS buffer at its end (two steps of latency cover; double-buffered LDS, one barrier per
-// step that waits for LDS traffic only, mi_lds_barrier). Every staging load is a per-lane base plus
-// the superblock times a per-lane stride, with no branch around it. Activation fragments are stored
-// with their two 16-byte halves swapped for columns 16-31 of a 32-column group (the ds_read_b128
-// lane groups then hit 64 distinct banks). Same operands and canonical combine (mmqx_term,
-// cfold_vec) as every kernel of this file: bit-identical. CH > 0: K in straight-line chunks of CH
-// superblocks; 0: a rolled loop of step pairs.
-template <int TYPE, int CH>
-__global__ __launch_bounds__(512, 2) void k_mmqs(mi_mmx_group grp) {
-    MI_MMX_MEMBER(grp);
-    using F = XFmt<TYPE>;
-    constexpr int NP = F::NP;
-    constexpr int BM = 128, BN = 64;
-    constexpr int XB = 8 * BN * 32;           // activation quants of one superblock
-    constexpr int UB = BN * 32;               // U halves
-    constexpr int DB = BN * 4;                // d_a
-    constexpr int WB = BM * F::BS;            // raw weight blocks
-    constexpr int SB = XB + UB + DB + WB;     // one stage
-    constexpr int WCH = WB / 16;              // 16-byte weight chunks per stage (Q4_K 1152, Q5_K 1408)
-
-    const int tid = (int) threadIdx.x;
-    const int lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r = lane & 31, h = lane >> 5;
-    const int rw = w & 3, cw = w >> 2;
-    const int64_t ncols = act.ncols;
-    const int S = (int) (K / 256);
-    const int gs = cfold_gs(S);
-    const int64_t nrt = (N + BM - 1) / BM;
-    const int64_t n0 = (mmx_tile % nrt) * BM, c0 = (mmx_tile / nrt) * BN;
-    const int nrows = (int) std::min<int64_t>(BM, N - n0);
-
-    const uint32_t xstep = (uint32_t) ncols * 32;
-
-    // ---- staging: a stage is the concatenation [X 1024 | U 128 | d_a 16 | W WCH] of 16-byte chunks;
-    // thread t moves chunks t + 512 i (i < NLD). Every slot is a global load at a per-lane base +
-    // superblock x per-lane stride and an LDS store, with no branch (the compiler's vmcnt bookkeeping
-    // stays exact only on branch-free paths): slots past the end re-read the thread's first chunk and
-    // store into a 256-byte sink.
-    typedef __attribute__((address_space(1))) const i32x4 * gp_t;  // (native vectors: the HIP uint4
-    // class in a struct array kept the staging registers in scratch)
-    constexpr int NCH = 1024 + 128 + 16 + WCH;
-    constexpr int NLD = (NCH + 511) / 512;
-    constexpr int SINK = 2 * SB;                       // 256-byte sink after the two stages
-    __shared__ __attribute__((aligned(16))) char lds[2 * SB + 256];
-    const char * sbase[NLD];
-    uint32_t sstride[NLD], sdst[NLD];
-    auto col_of = [&](int c) { return std::min<int64_t>(c0 + c, ncols - 1); };
-#pragma unroll
-    for (int i = 0; i < NLD; i++) {
-        int q = tid + 512 * i;
-        const bool real = q < NCH;
-        if (!real) q = tid;  // re-read chunk tid (an activation chunk), store into the sink
-        if (q < 1024) {  // activation quants: step kk, column col, half
-            const int kk = q >> 7, col = (q & 127) >> 1, half = q & 1;
-            sbase[i] = (const char *) act.xq + ((int64_t) kk * ncols + col_of(col)) * 32 + 16 * half;
-            sstride[i] = 8 * xstep;
-            sdst[i] = (uint32_t) (kk * (BN * 32) + col * 32 + 16 * (half ^ ((col >> 4) & 1)));
-        } else if (q < 1024 + 128) {  // U halves
-            const int qq = q - 1024, col = qq >> 1, half = qq & 1;
-            sbase[i] = (const char *) act.xu + col_of(col) * 32 + 16 * half;
-            sstride[i] = (uint32_t) ncols * 32;
-            sdst[i] = (uint32_t) (XB + col * 32 + 16 * (half ^ ((col >> 4) & 1)));
-        } else if (q < 1024 + 128 + 16) {  // d_a of columns 4 qq .. 4 qq + 3
-            const int qq = q - 1024 - 128;
-            sbase[i] = (const char *) act.xd + col_of(4 * qq) * 4;
-            sstride[i] = (uint32_t) ncols * 4;
-            sdst[i] = (uint32_t) (XB + UB + 16 * qq);
-        } else {  // raw weight blocks: row, 16-byte chunk c of the row's superblock
-            const int qq = q - 1024 - 128 - 16;
-            const int row = qq / (F::BS / 16), c = qq % (F::BS / 16);
-            sbase[i] = (const char *) W + (n0 + std::min(row, nrows - 1)) * (int64_t) nb01 + 16 * c;
-            sstride[i] = F::BS;
-            sdst[i] = (uint32_t) (XB + UB + DB + row * F::BS + 16 * c);
-        }
-        if (!real) sdst[i] = (uint32_t) (SINK + 16 * (tid & 15));
-    }
-    struct Stg {
-        i32x4 v[NLD];
-    };
-    auto stage_load = [&](Stg & st, int sb) {
-        sb = std::min(sb, S - 1);
-#pragma unroll
-        for (int i = 0; i < NLD; i++) st.v[i] = *(gp_t) (sbase[i] + (uint32_t) sb * sstride[i]);
-    };
-    auto stage_store = [&](const Stg & st, int buf) {
-#pragma unroll
-        for (int i = 0; i < NLD; i++) {
-            const uint32_t d = sdst[i] >= (uint32_t) SINK ? sdst[i] : sdst[i] + (uint32_t) (buf * SB);
-            *(i32x4 *) (lds + d) = st.v[i];
-        }
-    };
-
-    // ---- compute role (every wave): rows n0 + 32 rw + r, columns c0 + 32 cw + 16-column groups
-    const int col = 32 * cw + r;
-    const uint32_t xoff = (uint32_t) (col * 32 + 16 * (h ^ ((col >> 4) & 1)));
-    constexpr uint32_t kQs = F::Q5 ? 48 : 16;
-    const uint32_t woff = (uint32_t) (XB + UB + DB + (32 * rw + r) * F::BS);
-    f32x16 y = f32x16(-0.0f), ylo = f32x16(-0.0f), gsum = {};
-
-    // The combine of a superblock reads its accumulators and its scales / U halves / mins from the
-    // LDS buffer it was computed from (still intact during the next step: a buffer is restaged only
-    // at the end of the step after its own). comb_slice does accumulator elements 2 j, 2 j + 1.
-    struct Comb {
-        f32x16 Uv, tv;
-        float dw, dm;
-    };
-    auto comb_begin = [&](int buf, Comb & c) {
-        const char * base = lds + buf * SB;
-        const uint4 hdr = *(const uint4 *) (base + woff);
-        c.dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF));
-        c.dm = mi_h2f((uint16_t) (hdr.x >> 16));
-        const uint32_t ma = hdr.z & 0x3F3F3F3Fu;
-        const uint32_t mb = ((hdr.w >> 4) & 0x0F0F0F0Fu) | ((hdr.z >> 2) & 0x30303030u);
-        const uint32_t mw = h ? mb : ma;
-        half8 mu;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t m = (mw >> (8 * q)) & 0xFF;
-            mu[2 * q] = (_Float16) (float) m;
-            mu[2 * q + 1] = (_Float16) (float) (64 * m);
-        }
-        const half8 xu = *(const half8 *) (base + XB + xoff);
-        // U on the f16 MFMA: A = [S & 63, S >> 6] of the lane's column, B = [m, 64 m] of its row
-        c.Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
-    };
-    auto comb_slice = [&](int buf, const i32x16 (&acc)[NP], Comb & c, int j) {
-        const float * dal = (const float *) (lds + buf * SB + XB + UB) + 32 * cw;
-        const float2 d2 = *(const float2 *) &dal[8 * (j >> 1) + 4 * h + 2 * (j & 1)];
-        const float dav[2] = {d2.x, d2.y};
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const int el = 2 * j + e;
-            int T = acc[NP - 1][el];
-#pragma unroll
-            for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
-            c.tv[el] = mmqx_term(T, c.Uv[el], c.dw, c.dm, dav[e]);
-        }
-    };
-    // superblock sb's MFMAs into acc from LDS buffer buf; `hook(kk)` runs after step kk's MFMAs (the
-    // deferred combine of the previous superblock interleaves there)
-    auto mfma_sb = [&](int buf, i32x16 (&acc)[NP], auto && hook) {
-        const char * base = lds + buf * SB;
-        const char * wr = base + woff;
-        const uint4 hdr = *(const uint4 *) wr;
-        uint4 q4[4], qh = {};
-#pragma unroll
-        for (int p = 0; p < 4; p++) q4[p] = *(const uint4 *) (wr + kQs + 32 * p + 16 * h);
-        if constexpr (F::Q5) qh = *(const uint4 *) (wr + 16 + 16 * h);
-        const uint32_t w0 = hdr.y, w2 = hdr.w;
-        const uint32_t sca = w0 & 0x3F3F3F3Fu;
-        const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
-        uint32_t lo[4], hi[4];
-#pragma unroll
-        for (int kk = 0; kk < 8; kk++) {
-            const i32x4 xa = *(const i32x4 *) (base + kk * (BN * 32) + xoff);
-            if ((kk & 1) == 0) {
-                const uint4 q = q4[kk >> 1];
-                const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    lo[e] = qv[e] & 0x0F0F0F0Fu;
-                    hi[e] = (qv[e] >> 4) & 0x0F0F0F0Fu;
-                }
-            }
-            uint32_t v[4];
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                v[e] = (kk & 1) ? hi[e] : lo[e];
-                if constexpr (F::Q5) {
-                    const uint32_t hb[4] = {qh.x, qh.y, qh.z, qh.w};
-                    v[e] |= ((hb[e] >> kk) & 0x01010101u) << 4;
-                }
-            }
-            const uint32_t scw = kk < 4 ? sca : scb;
-#pragma unroll
-            for (int p = 0; p < NP; p++) {
-                const uint32_t f = __builtin_amdgcn_ubfe(scw, 8 * (kk & 3) + (F::Q5 ? 2 * p : 3 * p), F::Q5 ? 2 : 3);
-                const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
-                acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa, b, kk == 0 ? i32x16{} : acc[p], 0, 0, 0);
-            }
-            hook(kk);
-        }
-    };
-    auto compute = [&](int buf, int sb) {
-        i32x16 acc[NP];
-        mfma_sb(buf, acc, [](int) {});
-        Comb c;
-        comb_begin(buf, c);
-#pragma unroll
-        for (int j = 0; j < 8; j++) comb_slice(buf, acc, c, j);
-        cfold_vec(gsum, y, ylo, c.tv, sb, gs, S);
-    };
-    Stg st0, st1;  // (two variables, not an array: a register pair the unrolled steps alternate)
-    static_assert(CH % 2 == 0, "staging registers alternate");
-    if constexpr (CH == 0) {
-        // rolled: two steps per iteration, no branch in the body (S even, host-checked; requests
-        // past the end are clamped re-reads), so the compiler's vmcnt bookkeeping across the back
-        // edge stays exact and the code stays small
-        stage_load(st0, 0);
-        stage_load(st1, 1);
-        stage_store(st0, 0);
-        mi_lds_barrier();
-        for (int sb = 0; sb < S; sb += 2) {
-            stage_load(st0, sb + 2);
-            compute(0, sb);
-            stage_store(st1, 1);
-            mi_lds_barrier();
-            stage_load(st1, sb + 3);
-            compute(1, sb + 1);
-            stage_store(st0, 0);
-            mi_lds_barrier();
-        }
-    } else
-    for (int c0k = 0; c0k < S; c0k += CH) {
-        // chunk prologue: superblocks c0k, c0k + 1 requested, the first stored
-        stage_load(st0, c0k);
-        stage_load(st1, c0k + 1);
-        stage_store(st0, 0);
-        mi_lds_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        // step u: `mine` held superblock c0k + u (stored last step) and now requests u + 2; `next`
-        // holds u + 1, stored into the buffer the previous step read
-        auto step = [&](Stg & mine, Stg & next, const int u) {
-            const int sb = c0k + u;
-            if (u + 2 < CH) stage_load(mine, sb + 2);
-            if (sb < S) compute(u & 1, sb);
-            if (u + 1 < CH) stage_store(next, (u + 1) & 1);
-            mi_lds_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-        };
-#pragma unroll
-        for (int u = 0; u < CH; u += 2) {
-            step(st0, st1, u);
-            step(st1, st0, u + 1);
-        }
-    }
-
-    y = ylo + y;  // cfold_end
-    // accumulator element el: prompt column c0 + 32 cw + (el & 3) + 8 (el >> 2) + 4 h, row n0 + 32 rw + r
-    const int64_t n = n0 + 32 * rw + r;
-    if (n >= N) return;
-#pragma unroll
-    for (int el = 0; el < 16; el++) {
-        const int64_t c = c0 + 32 * cw + (el & 3) + 8 * (el >> 2) + 4 * h;
-        if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = y[el];
-    }
-}
-
 // ---- long prompts, K split over wave pairs: k_mmqt ------------------------------------------------
-// k_mmqs dequantizes a wave's 32 weight rows once per 32 columns, and the dequantization is the
-// larger share of its VALU (~112 of ~300 instructions per 17 MFMAs). Here each wave runs 32 rows x 64
+// A kernel that stages the shared operands once per workgroup in LDS and dequantizes each wave's 32
+// weight rows in registers (round 4's k_mmqs: 38.6 us at B = 512, MFMA 26 % busy,
+// profiles/r04c_pf_long.txt, r04d_mmqs_*_pmc.txt; removed) dequantizes them once per 32 columns,
+// and the dequantization is the larger share of its VALU (~112 of ~300 instructions per 17 MFMAs). Here each wave runs 32 rows x 64
 // columns -- two 32 x 32 tiles per dequantized plane, 34 MFMAs per superblock -- and the 8 waves of
 // the 128-row x 64-column tile split K in two: waves 0-3 fold the low half of the canonical order
 // (superblocks [0, SK), groups 0..3), waves 4-7 the high half ([SK, S), groups 4..7), and the
 // halves meet once at the end in LDS (y = lo + hi: the canonical combine, bit-identical to every
 // kernel of this file). A stage holds one superblock of each half: per half the activation quants
 // [8 steps][64 columns][32] (16 KB, 16-byte halves swapped for columns 16-31 of a 32-column group,
-// as k_mmqs), the U halves (2 KB), the raw weight blocks of the 128 rows (18 KB) and d_a (256 B).
+// so the ds_read_b128 lane groups hit 64 distinct banks), the U halves (2 KB), the raw weight
+// blocks of the 128 rows (18 KB) and d_a (256 B).
 // Staging is LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write pass): a stage is
 // 72 one-KB wave-instructions, 9 per wave (each a per-lane source address, the destination
 // lane-linear), plus one 256-byte d_a DMA per half. The next stage's DMAs are issued as a step
@@ -2813,17 +2558,6 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         return;
     }
 #endif
-    if (g_mi_tuning.mmq_long == 3 || g_mi_tuning.mmq_long == 4) {  // shared operands staged in LDS (4: rolled loop)
-        const dim3 gridr((unsigned) mmx_deal(g, 128, 64));
-        if (g_mi_tuning.mmq_long == 4 && (K / 256) % 2 == 0) {
-            if (type == 12) hipLaunchKernelGGL((k_mmqs<12, 0>), gridr, dim3(512), 0, s, g);
-            else hipLaunchKernelGGL((k_mmqs<13, 0>), gridr, dim3(512), 0, s, g);
-        } else {
-            if (type == 12) hipLaunchKernelGGL((k_mmqs<12, 16>), gridr, dim3(512), 0, s, g);
-            else hipLaunchKernelGGL((k_mmqs<13, 16>), gridr, dim3(512), 0, s, g);
-        }
-        return;
-    }
     const dim3 grid((unsigned) mmx_deal(g, XBM, XBN));
     // warp-specialized k_mmqw (4 loader + 8 MFMA waves; Q4_K B=512 32.1 -> 31.2 us, Q5_K 46.2 ->
     // 43.8 us grouped, profiles/r03r_prefill_mmqw.txt) unless variant bit 2^28 asks for k_mmqx
