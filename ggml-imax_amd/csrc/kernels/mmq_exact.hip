@@ -1247,25 +1247,6 @@ __device__ __forceinline__ void mi_glds4(const void * gsrc, uint32_t lds) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(gsrc), "s"(lds));
 }
-// The same through a buffer descriptor: per-lane 32-bit offset voff + wave-uniform soff (no
-// per-lane address arithmetic per load)
-// A raw buffer descriptor as four wave-uniform dwords (base, num_records; no stride, the flags of
-// __builtin_amdgcn_make_buffer_rsrc(..., 0x00020000)), so inline asm can take it as an SGPR quad.
-__device__ __forceinline__ i32x4 mi_rsrc(const void * base, uint32_t bytes) {
-    const uint64_t a = (uint64_t) (uintptr_t) base;
-    return i32x4{__builtin_amdgcn_readfirstlane((int) (uint32_t) a), __builtin_amdgcn_readfirstlane((int) ((uint32_t) (a >> 32) & 0xFFFF)),
-                 __builtin_amdgcn_readfirstlane((int) bytes), 0x00020000};
-}
-__device__ __forceinline__ void mi_blds16(i32x4 rs, uint32_t voff, uint32_t soff, uint32_t lds) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds), "s"(soff));
-}
-__device__ __forceinline__ void mi_blds4(i32x4 rs, uint32_t voff, uint32_t soff, uint32_t lds) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds), "s"(soff));
-}
 // LDS byte address of a __shared__ location (the low 32 bits of its flat address), wave-uniform
 __device__ __forceinline__ uint32_t mi_lds_addr(const void * p) {
     return (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (uintptr_t) p);
@@ -1275,13 +1256,7 @@ __device__ __forceinline__ uint32_t mi_lds_addr(const void * p) {
 // and 97 into dst as uint64 [2][2][80] (0 start, 1 after the prologue, 2 + 4 u + {0 step start, 1
 // after the MFMA steps, 2 after the combine, 3 after the DMA wait}); 1 no weight DMAs after the
 // prologue, 2 no combine, 4 no DMAs at all after the prologue (profiles/r04l_mmqt_stamps.txt).
-// BUF: the DMAs through buffer descriptors (SGPR superblock offsets) instead of per-lane 64-bit
-// addresses. SPLIT 1: the two column tiles' MFMAs in two passes over the dequantized planes (held in
-// registers), the first tile's combine interleaved with the second tile's MFMAs, so half of the
-// combine's VALU runs beside the matrix pipe instead of after it; 2: also the second tile's combine,
-// deferred into the next step's first pass (its operands -- exact T, U, d_a, d_w, dmin -- carried
-// across the barrier in registers).
-template <int TYPE, int ABL = 0, bool BUF = false, int SPLIT = 0>
+template <int TYPE, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -1340,13 +1315,6 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         }
     }
     const uint32_t doff = col_of(lane) * 4;
-    // BUF: descriptors of the activation quants, U halves, weight rows (this tile's) and d_a; piece
-    // i's byte offset = its per-lane part (poff) + a wave-uniform part (sbase + sb * pstride)
-    // (descriptors built at each use from uniform values: SGPR quads the asm can take)
-    auto xres = [&] { return mi_rsrc(act.xq, (uint32_t) (K * ncols)); };
-    auto ures = [&] { return mi_rsrc(act.xu, (uint32_t) (S * ncols * 32)); };
-    auto wres = [&] { return mi_rsrc(W + (size_t) n0 * nb01, (uint32_t) ((size_t) nrows * nb01)); };
-    auto dres = [&] { return mi_rsrc(act.xd, (uint32_t) (S * ncols * 4)); };
     // stage u: superblock u of the low half, SK + u of the high half (clamped: a high half shorter
     // than the low one re-reads its last superblock, whose terms are not folded) into buffer u & 1.
     // Piece i < NI; i == NI: d_a (wave 0 the low half's, wave 1 the high half's, the others into the
@@ -1356,29 +1324,15 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         if constexpr ((ABL & 1) != 0) if (u > 0 && i < NI && (w + 8 * i) % NPIECE >= 18) return;
         char * sbuf = lds + (u & 1) * SB;
         if (i < NI) {
-            const int q = w + 8 * i, hf = q / NPIECE, t = q % NPIECE;
+            const int hf = (w + 8 * i) / NPIECE;
             const int sb = std::min(hf ? SK + u : u, S - 1);
-            if constexpr (BUF) {
-                // wave-uniform: the kk offset of an activation piece, the superblock offset
-                const uint32_t so = (uint32_t) __builtin_amdgcn_readfirstlane(
-                    (int) ((t < 16 ? (uint32_t) (t >> 1) * (uint32_t) ncols * 32 : 0u) + (uint32_t) sb * pstride[i]));
-                const uint32_t ld = mi_lds_addr(sbuf + pdst[i]);
-                if (t < 16) mi_blds16(xres(), poff[i], so, ld);
-                else if (t < 18) mi_blds16(ures(), poff[i], so, ld);
-                else mi_blds16(wres(), poff[i], so, ld);
-            } else {
-                const char * src = pbase[i] + (size_t) sb * pstride[i] + poff[i];
-                mi_glds16(src, mi_lds_addr(sbuf + pdst[i]));
-            }
+            const char * src = pbase[i] + (size_t) sb * pstride[i] + poff[i];
+            mi_glds16(src, mi_lds_addr(sbuf + pdst[i]));
         } else {
             const int sb = std::min(w == 1 ? SK + u : u, S - 1);
+            const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
             char * dd = w >= 2 ? lds + SINK : sbuf + w * HB + XB + UB + WB;
-            if constexpr (BUF) {
-                mi_blds4(dres(), doff, (uint32_t) __builtin_amdgcn_readfirstlane((int) ((uint32_t) sb * (uint32_t) ncols * 4)), mi_lds_addr(dd));
-            } else {
-                const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
-                mi_glds4(src, mi_lds_addr(dd));
-            }
+            mi_glds4(src, mi_lds_addr(dd));
         }
     };
     auto stage_dma = [&](int u) {
@@ -1502,133 +1456,6 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         const char * hb = lds + buf * SB + kh * HB;
         combine(lds + buf * SB + woff, hb + XB + xoff0, (const float *) (hb + XB + UB + WB), sb);
     };
-    // SPLIT: one whole step (MFMAs + combine) from stage buffer buf
-    auto fold_tile = [&](int ct, const f32x16 & tv, int sb) {
-        if (sb >= sb_end) return;  // wave-uniform
-        const int pos = sb % gs;
-        if (pos == 0) {
-            asm volatile("" ::: "memory");
-            gsum[ct] = f32x16(-0.0f);
-        }
-        gsum[ct] = gsum[ct] + tv;
-        if (pos == gs - 1 || sb == S - 1) {
-            asm volatile("" ::: "memory");
-            y[ct] = y[ct] + gsum[ct];
-        }
-    };
-    // SPLIT 2: tile 1's combine operands of the previous step
-    i32x16 dT = {};
-    f32x16 dU = {}, dA = {}, dtv;
-    float ddw = 0.0f, ddm = 0.0f;
-    int dsb = -1;  // wave-uniform; -1: nothing pending
-    auto step_split = [&](int buf, int sb, auto && hook) {
-        const char * base = lds + buf * SB;
-        const char * hb = base + kh * HB;
-        const char * wr = base + woff;
-        const uint4 hdr = *(const uint4 *) wr;
-        uint4 q4[4];
-#pragma unroll
-        for (int p = 0; p < 4; p++) q4[p] = *(const uint4 *) (wr + kQs + 32 * p + 16 * h);
-        const uint32_t w0 = hdr.y, w2 = hdr.w;
-        const uint32_t sca = w0 & 0x3F3F3F3Fu;
-        const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
-        i32x4 bq[8][NP];
-        uint32_t lo[4], hi[4];
-        // pass 1: tile 0, dequantizing every plane fragment once
-#pragma unroll
-        for (int kk = 0; kk < 8; kk++) {
-            const i32x4 xa0 = *(const i32x4 *) (hb + kk * (BN * 32) + xoff0);
-            if ((kk & 1) == 0) {
-                const uint4 q = q4[kk >> 1];
-                const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    lo[e] = qv[e] & 0x0F0F0F0Fu;
-                    hi[e] = (qv[e] >> 4) & 0x0F0F0F0Fu;
-                }
-            }
-            const uint32_t scw = kk < 4 ? sca : scb;
-#pragma unroll
-            for (int p = 0; p < NP; p++) {
-                const uint32_t f = __builtin_amdgcn_ubfe(scw, 8 * (kk & 3) + 3 * p, 3);
-                const uint32_t * v = (kk & 1) ? hi : lo;
-                bq[kk][p] = i32x4{(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
-                acc[0][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa0, bq[kk][p], kk == 0 ? i32x16{} : acc[0][p], 0, 0, 0);
-            }
-            hook(kk);
-            if constexpr (SPLIT == 2) {  // the previous step's tile-1 terms 2 kk, 2 kk + 1
-                if (dsb >= 0) {
-#pragma unroll
-                    for (int e = 0; e < 2; e++) dtv[2 * kk + e] = mmqx_term(dT[2 * kk + e], dU[2 * kk + e], ddw, ddm, dA[2 * kk + e]);
-                }
-            }
-        }
-        if constexpr (SPLIT == 2) {
-            if (dsb >= 0) fold_tile(1, dtv, dsb);
-        }
-        // the combine's row operands and tile 0's U
-        const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF)), dm = mi_h2f((uint16_t) (hdr.x >> 16));
-        const uint32_t ma = hdr.z & 0x3F3F3F3Fu;
-        const uint32_t mb = ((hdr.w >> 4) & 0x0F0F0F0Fu) | ((hdr.z >> 2) & 0x30303030u);
-        const uint32_t mw = h ? mb : ma;
-        half8 mu;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t m = (mw >> (8 * q)) & 0xFF;
-            mu[2 * q] = (_Float16) (float) m;
-            mu[2 * q + 1] = (_Float16) (float) (64 * m);
-        }
-        const float * dal = (const float *) (hb + XB + UB + WB);
-        auto terms = [&](int ct, const f32x16 & Uv, f32x16 & tv, int j) {  // elements 2 j, 2 j + 1
-            const float2 d2 = *(const float2 *) &dal[32 * ct + 8 * (j >> 1) + 4 * h + 2 * (j & 1)];
-            const float dav[2] = {d2.x, d2.y};
-#pragma unroll
-            for (int e = 0; e < 2; e++) {
-                const int el = 2 * j + e;
-                const int T = (acc[ct][1][el] << F::SHIFT) + acc[ct][0][el];
-                tv[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
-            }
-        };
-        const f32x16 Uv0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8 *) (hb + XB + xoff0), mu, f32x16{}, 0, 0, 0);
-        // pass 2: tile 1 from the held planes, tile 0's terms between its MFMA steps
-        f32x16 tv0;
-#pragma unroll
-        for (int kk = 0; kk < 8; kk++) {
-            const i32x4 xa1 = *(const i32x4 *) (hb + kk * (BN * 32) + 1024 + xoff0);
-#pragma unroll
-            for (int p = 0; p < NP; p++)
-                acc[1][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa1, bq[kk][p], kk == 0 ? i32x16{} : acc[1][p], 0, 0, 0);
-            terms(0, Uv0, tv0, kk);
-        }
-        fold_tile(0, tv0, sb);
-        const f32x16 Uv1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8 *) (hb + XB + 1024 + xoff0), mu, f32x16{}, 0, 0, 0);
-        if constexpr (SPLIT == 2) {  // tile 1's operands into registers: its terms run in the next step
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const float2 d2 = *(const float2 *) &dal[32 + 8 * (j >> 1) + 4 * h + 2 * (j & 1)];
-                dA[2 * j] = d2.x;
-                dA[2 * j + 1] = d2.y;
-            }
-#pragma unroll
-            for (int el = 0; el < 16; el++) dT[el] = (acc[1][1][el] << F::SHIFT) + acc[1][0][el];
-            dU = Uv1;
-            ddw = dw;
-            ddm = dm;
-            dsb = sb;
-        } else {
-            f32x16 tv1;
-#pragma unroll
-            for (int j = 0; j < 8; j++) terms(1, Uv1, tv1, j);
-            fold_tile(1, tv1, sb);
-        }
-    };
-    auto finish_split = [&] {  // SPLIT 2: the last step's tile-1 terms
-        if constexpr (SPLIT == 2) {
-#pragma unroll
-            for (int el = 0; el < 16; el++) dtv[el] = mmqx_term(dT[el], dU[el], ddw, ddm, dA[el]);
-            fold_tile(1, dtv, dsb);
-        }
-    };
     const int sb0 = kh ? SK : 0;
     stamp(0);
     stage_dma(0);
@@ -1647,19 +1474,12 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
                 for (int i = 7; i <= NI; i++) stage_piece(u + 1, i);
             }
         };
-        if constexpr (SPLIT != 0) {
-            step_split(u & 1, sb0 + u, dma_hook);
-            stamp(3 + 4 * u);
-            stamp(4 + 4 * u);
-        } else {
-            mfma(u & 1, dma_hook);
-            stamp(3 + 4 * u);
-            combine_stage(u & 1, sb0 + u);
-            stamp(4 + 4 * u);
-        }
+        mfma(u & 1, dma_hook);
+        stamp(3 + 4 * u);
+        combine_stage(u & 1, sb0 + u);
+        stamp(4 + 4 * u);
         stage_wait();
     }
-    finish_split();
     if constexpr ((ABL & 8) != 0) {  // dst holds the stamps; keep the results alive
         float t = 0.0f;
 #pragma unroll
@@ -2535,14 +2355,15 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     // k_mmqw, B=256 18.5 vs 19.7, profiles/r04i_pf_long_mmqt.txt; its DMAs all at the step start
     // instead of one behind each MFMA step: 37.1 us; the high half folding one step late from a
     // 3-slot LDS ring, so the two waves of a SIMD alternate MFMA and VALU phases: 38.7 us,
-    // profiles/r04k_mmqt_skew_ab.txt, r04m_mmqt_skew_stamps.txt -- both removed)
+    // profiles/r04k_mmqt_skew_ab.txt, r04m_mmqt_skew_stamps.txt; DMAs through buffer descriptors:
+    // no change, r04p_mmqt_buf_ab.txt; the two column tiles in two passes over held planes with
+    // tile 0's combine under tile 1's MFMAs: 36.4 vs 35.5 us, r04r_mmqt_split_ab.txt, and tile 1's
+    // combine deferred into the next step too: 36.9 vs 35.4 us, r04t_mmqt_split2_ab.txt -- all
+    // removed)
     const int lng = g_mi_tuning.mmq_long;
-    if ((lng == 0 || lng == 2 || (lng >= 5 && lng <= 7)) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
+    if ((lng == 0 || lng == 2) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
-        if (lng == 5) hipLaunchKernelGGL((k_mmqt<12, 0, true>), gridt, dim3(512), 0, s, g);  // buffer-descriptor DMAs (A/B)
-        else if (lng == 6) hipLaunchKernelGGL((k_mmqt<12, 0, true, 1>), gridt, dim3(512), 0, s, g);  // + split tiles (A/B)
-        else if (lng == 7) hipLaunchKernelGGL((k_mmqt<12, 0, true, 2>), gridt, dim3(512), 0, s, g);  // + tile 1 deferred (A/B)
-        else hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
+        hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
         return;
     }
 #if MI_DIAG

@@ -155,8 +155,8 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
     else:
         variants = [0, 2048, 1 << 27, 128 | 131072, 128 | 65536, 128 | 131072 | (1 << 28)] + ([1 << 21] if B <= 16 else [])
     # long-prompt kernels forced onto these shapes (variant bits 128 | 131072, mmq_long): k_mmqw (1),
-    # k_mmqt (2, K split over wave pairs, Q4_K; 5 its DMAs through buffer descriptors, 6 + split tiles, 7 + deferred tile-1 combine)
-    longs = [(128 | 131072, L) for L in (1, 2, 5, 6, 7)] if tname in ("q4_K", "q5_K") else []
+    # k_mmqt (2, K split over wave pairs, Q4_K)
+    longs = [(128 | 131072, L) for L in (1, 2)] if tname in ("q4_K", "q5_K") else []
     outs = {}
     try:
         for v in variants + longs:
