@@ -2184,6 +2184,20 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
         ctx->graph_stats[3]++;
         return mi_graph_launch_nodes(ctx, cgraph);
     }
+    // A topology whose graphs kept arriving with new kernel arguments and never replayed (a decode
+    // step through graph_compute: the KV length moves every call) launches directly: a capture costs
+    // a synchronous recording of every launch plus an update per call for nothing, where a direct
+    // launch overlaps host and device. Decided after kGraphMissDirect such captures in a row; the
+    // key and the preparation are then skipped too. Measured on main-batched.cpp's decode loop
+    // (bench gpt2_batched): 4.9 k tokens/s capturing every step vs 6.2-6.5 k direct.
+    const uint64_t topo = graph_topology(cgraph);
+    {
+        auto m = ctx->topo_misses.find(topo);
+        if (m != ctx->topo_misses.end() && m->second >= kGraphMissDirect) {
+            ctx->graph_stats[3]++;
+            return mi_graph_launch_nodes(ctx, cgraph);
+        }
+    }
     prepare_for_capture(ctx, cgraph);
     static thread_local std::vector<uint64_t> key;
     graph_key(ctx, cgraph, key);
@@ -2195,7 +2209,6 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
             return GGML_STATUS_SUCCESS;
         }
     }
-    const uint64_t topo = graph_topology(cgraph);
     auto seen = ctx->topo_launches.find(topo);
     if (seen == ctx->topo_launches.end() || seen->second < graph_min_launches()) {
         ctx->graph_stats[3]++;
@@ -2203,19 +2216,7 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
         ctx->topo_launches[topo] = ctx->last_launches;
         return st;
     }
-    // A topology whose graphs keep arriving with new kernel arguments and never replay (a decode
-    // step through graph_compute: the KV length moves every call) pays a synchronous capture and an
-    // update per call for nothing -- the host records every launch anyway, and the device cannot
-    // start until the capture ends, where a direct launch overlaps the two. After
-    // kGraphMissDirect such captures in a row the topology launches directly (a later exact-key
-    // hit resets the count). Measured on main-batched.cpp's decode loop: 4.9 k tokens/s captured
-    // vs 6.5 k direct (profiles/r04s_bench.json, gpt2_batched).
-    int & misses = ctx->topo_misses[topo];
-    if (misses >= kGraphMissDirect) {
-        ctx->graph_stats[3]++;
-        return mi_graph_launch_nodes(ctx, cgraph);
-    }
-    misses++;
+    ctx->topo_misses[topo]++;  // (reset by a replay of this topology)
     hipGraph_t graph = capture_pass(ctx, cgraph);
     if (!graph) {
         ctx->graph_stats[3]++;

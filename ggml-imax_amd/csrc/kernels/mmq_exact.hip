@@ -16,8 +16,9 @@
 //   * U: one v_mfma_f32_32x32x16_f16 per superblock with exact small integers: A = [m_j, 64 m_j]
 //     (<= 4032), B = [S_j & 63, S_j >> 6] where S_j = sum of 32 q8 (the activation quantizer
 //     writes these), so every product and partial sum is an integer < 2^24: exact.
-// The float combine per superblock and the combine order are fixed (mmqx_term, its terms
-// left-folded in superblock order) and shared by every kernel of this file, so column shards of a
+// The float combine per superblock and the combine order are fixed (mmqx_pre, then cfold: the
+// values scaled by d_a and summed in a fixed tree of superblock groups) and shared by every kernel
+// of this file, so column shards of a
 // prompt (prompt-sharded multi-GPU) give the same bits as the whole prompt, whichever kernel runs
 // them. Against the
 // reference CPU the only difference is the f32 combine order (reference: 8-lane partial chains
@@ -58,17 +59,24 @@ __device__ __forceinline__ uint32_t mulb(uint32_t x, uint32_t m) {
     return __builtin_bit_cast(uint32_t, a * b);
 }
 
-// the canonical per-superblock term (every kernel of the family uses exactly this); the terms of
-// an output are then left-folded in superblock order: y = term_0; y = y + term_1; ...
-__device__ __forceinline__ float mmqx_term(int T, float U, float dw, float dm, float da) {
-    const float t = __builtin_fmaf(-dm, U, dw * (float) T);
-    return __builtin_fmaf(da, t, 0.0f);
+// the canonical per-superblock value t = d_w T - dmin_w U (every kernel of the family computes
+// exactly this); the group sums then take da * t fused: g = fma(da, t, g) (cfold below)
+__device__ __forceinline__ float mmqx_pre(int T, float U, float dw, float dm) {
+    return __builtin_fmaf(-dm, U, dw * (float) T);
+}
+__device__ __forceinline__ f32x16 fma_vec(const f32x16 & a, const f32x16 & b, const f32x16 & c) {
+    f32x16 r;
+#pragma unroll
+    for (int i = 0; i < 16; i++) r[i] = __builtin_fmaf(a[i], b[i], c[i]);
+    return r;
 }
 
 // The canonical combine order of an output's superblock terms, shared by every kernel of this
 // file (so any column shard of a prompt gives the same bits whichever kernel computes it): the S
 // superblocks form kCfoldGroups contiguous groups of gs = ceil(S / kCfoldGroups) (the last ones
-// shorter or empty), each group's terms are left-folded from -0 (g = -0; g = g + t; ...); the sums
+// shorter or empty), each group's terms are accumulated in superblock order from -0 with the
+// activation scale fused in (g = -0; g = fma(d_a, t, g); ...: round-4 form, one VALU op per
+// element and superblock fewer than a separate product and sum); the sums
 // of groups 0..3 and of groups 4..7 are left-folded separately from -0 (lo = lo + g_0 ...; hi = hi +
 // g_4 ...) and y = lo + hi. (-0 + x == x for every float x, signed zeros and NaNs included, so an
 // empty half changes nothing.) The pipelined kernel (k_mmqp) gives each group to one of its waves,
@@ -78,12 +86,12 @@ constexpr int kCfoldHalf = kCfoldGroups / 2;  // first group of the high half
 __host__ __device__ constexpr int cfold_gs(int S) { return (S + kCfoldGroups - 1) / kCfoldGroups; }
 // first superblock of the high half
 __host__ __device__ constexpr int cfold_split(int S) { return kCfoldHalf * cfold_gs(S) < S ? kCfoldHalf * cfold_gs(S) : S; }
-// Sequential form: term t of superblock sb (terms arrive in superblock order); g, y, lo updated in
-// place, y and lo starting at -0: y folds the current half, lo receives the low half's sum when the
-// high half's first group ends. The result is cfold_end(lo, y).
-__device__ __forceinline__ void cfold(float & g, float & y, float & lo, float t, int sb, int gs, int S) {
+// Sequential form: value t and activation scale da of superblock sb (in superblock order); g, y,
+// lo updated in place, y and lo starting at -0: y folds the current half, lo receives the low
+// half's sum when the high half's first group ends. The result is cfold_end(lo, y).
+__device__ __forceinline__ void cfold(float & g, float & y, float & lo, float t, float da, int sb, int gs, int S) {
     const int pos = sb % gs;
-    g = pos == 0 ? t : g + t;
+    g = __builtin_fmaf(da, t, pos == 0 ? -0.0f : g);
     if (pos == gs - 1 || sb == S - 1) {
         if (sb / gs == kCfoldHalf) {
             lo = y;
@@ -97,13 +105,14 @@ __device__ __forceinline__ float cfold_end(float lo, float y) { return lo + y; }
 // the same for a whole accumulator (sb wave-uniform) without per-element selects; the resets are
 // uniform branches kept as branches (the empty asm stops their if-conversion into 16 v_cndmask
 // per superblock)
-__device__ __forceinline__ void cfold_vec(f32x16 & g, f32x16 & y, f32x16 & lo, const f32x16 & t, int sb, int gs, int S) {
+__device__ __forceinline__ void cfold_vec(f32x16 & g, f32x16 & y, f32x16 & lo, const f32x16 & t, const f32x16 & da, int sb, int gs, int S) {
     const int pos = sb % gs;
-    if (pos == 0) {
+    if (pos == 0) {  // a group's first value: da * t (bitwise fma(da, t, -0))
         asm volatile("" ::: "memory");
-        g = f32x16(-0.0f);
+        g = da * t;
+    } else {
+        g = fma_vec(da, t, g);
     }
-    g = g + t;
     if (pos == gs - 1 || sb == S - 1) {
         asm volatile("" ::: "memory");
         if (sb / gs == kCfoldHalf) {
@@ -118,13 +127,14 @@ __device__ __forceinline__ void cfold_vec(f32x16 & g, f32x16 & y, f32x16 & lo, c
 // (e.g. in the thread's own output locations) when the high half's first group ends; the result is
 // then unpark() + y if cfold_split(S) < S, else y
 template <typename Park>
-__device__ __forceinline__ void cfold_vec_park(f32x16 & g, f32x16 & y, const f32x16 & t, int sb, int gs, int S, Park && park) {
+__device__ __forceinline__ void cfold_vec_park(f32x16 & g, f32x16 & y, const f32x16 & t, const f32x16 & da, int sb, int gs, int S, Park && park) {
     const int pos = sb % gs;
-    if (pos == 0) {
+    if (pos == 0) {  // a group's first value: da * t (bitwise fma(da, t, -0))
         asm volatile("" ::: "memory");
-        g = f32x16(-0.0f);
+        g = da * t;
+    } else {
+        g = fma_vec(da, t, g);
     }
-    g = g + t;
     if (pos == gs - 1 || sb == S - 1) {
         asm volatile("" ::: "memory");
         if (sb / gs == kCfoldHalf) {
@@ -338,8 +348,7 @@ namespace {
 // the other LDS plane buffer, plus the row operands of the combine. Activations and weights arrive a stage ahead (vmcnt is in-order: every load is
 // consumed in the order it was issued, each with one stage of lead). Two waves per SIMD: while
 // one issues its MFMAs the other runs its dequantization / combine VALU.
-// Canonical combine order (shared by every kernel of this file): the superblock terms
-// (mmqx_term) left-folded in superblock order, y = term_0; y = y + term_1; ...
+// Canonical combine (shared by every kernel of this file): mmqx_pre per superblock, cfold's order.
 // NWV = 4: half-width workgroups (64 rows x 64 columns, 4 waves, each thread stages two rows), two
 // per CU, so one workgroup's barrier wait overlaps the other's MFMA steps.
 template <int TYPE, bool XCD, int ABL = 0, int LEAD = 4, int SCT = 0, int NWV = 8>
@@ -622,7 +631,7 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
 #pragma unroll
             for (int i = 0; i < 16; i++) {
                 float gg = gsum[i], yy = y[i], ll = -0.0f;  // (timing ablation: results invalid)
-                cfold(gg, yy, ll, (float) acc[0][i], sb, gs, S);
+                cfold(gg, yy, ll, (float) acc[0][i], 1.0f, sb, gs, S);
                 gsum[i] = gg;
                 y[i] = yy;
             }
@@ -650,10 +659,10 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
                     int T = acc[NP - 1][i];
 #pragma unroll
                     for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][i];
-                    tv[i] = mmqx_term(T, Uv[i], dw[e], dm[e], da);
+                    tv[i] = mmqx_pre(T, Uv[i], dw[e], dm[e]);
                 }
             }
-            cfold_vec_park(gsum, y, tv, sb, gs, S, park);
+            cfold_vec_park(gsum, y, tv, f32x16(da), sb, gs, S, park);
         }
         stamp(4 + 4 * sb);
         mi_lds_barrier();
@@ -697,7 +706,7 @@ __global__ __launch_bounds__(64 * NWV) void k_mmqx(mi_mmx_group g) {
 // and row operands. Every wave passes the same one barrier per stage. In k_mmqx each wave does its
 // MFMA steps, its share of the dequantization and the combine, and the barrier then waits for the
 // slowest; here the MFMA waves' stage is only MFMAs + combine. Same operands, same canonical combine
-// (mmqx_term, cfold_vec): bit-identical to k_mmqx.
+// (mmqx_pre, cfold_vec): bit-identical to k_mmqx.
 // ABL 8: timing stamps of MFMA wave 0 (workgroups 0 and 97) into dst, as k_mmqx (results invalid)
 template <int TYPE, int LEAD, int ABL = 0>
 __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
@@ -948,10 +957,10 @@ __global__ __launch_bounds__(768, 1) void k_mmqw(mi_mmx_group g) {
                 int T = acc[NP - 1][i2];
 #pragma unroll
                 for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][i2];
-                tv[i2] = mmqx_term(T, Uv[i2], dw[e], dm[e], da);
+                tv[i2] = mmqx_pre(T, Uv[i2], dw[e], dm[e]);
             }
         }
-        cfold_vec_park(gsum, y, tv, sb, gs, S, park);
+        cfold_vec_park(gsum, y, tv, f32x16(da), sb, gs, S, park);
         stamp(4 + 4 * sb);
         mi_lds_barrier();
         stamp(5 + 4 * sb);
@@ -1170,8 +1179,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
                         int T = acc[t][NP - 1][el];
 #pragma unroll
                         for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[t][p][el];
-                        const float term = mmqx_term(T, Uv[el], dw, dm, dav[e]);
-                        gsum[t][el] = gsum[t][el] + term;
+                        gsum[t][el] = __builtin_fmaf(dav[e], mmqx_pre(T, Uv[el], dw, dm), gsum[t][el]);
                     }
                 }
             }
@@ -1400,7 +1408,7 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         }
     };
     // the combine of superblock sb from acc: U on the f16 MFMA (A = [S & 63, S >> 6] of the lane's
-    // column from xup, B = [m, 64 m] of its row from the header at hdrp), then mmqx_term per element
+    // column from xup, B = [m, 64 m] of its row from the header at hdrp), then mmqx_pre per element
     // (d_a from dal), folded into this half's sum
     auto combine = [&](const char * hdrp, const char * xup, const float * dal, int sb) {
         if constexpr ((ABL & 2) != 0) {  // timing ablation: no combine (keep the accumulators alive)
@@ -1424,27 +1432,29 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         for (int ct = 0; ct < 2; ct++) {
             const half8 xu = *(const half8 *) (xup + 1024 * ct);
             const f32x16 Uv = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
-            f32x16 tv;
+            f32x16 tv, dv;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 const float2 d2 = *(const float2 *) &dal[32 * ct + 8 * (j >> 1) + 4 * h + 2 * (j & 1)];
-                const float dav[2] = {d2.x, d2.y};
+                dv[2 * j] = d2.x;
+                dv[2 * j + 1] = d2.y;
 #pragma unroll
                 for (int e = 0; e < 2; e++) {
                     const int el = 2 * j + e;
                     const int T = (acc[ct][1][el] << F::SHIFT) + acc[ct][0][el];
-                    tv[el] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
+                    tv[el] = mmqx_pre(T, Uv[el], dw, dm);
                 }
             }
             if (fold) {
                 // one half's fold: groups end at multiples of gs, y = y + g (the high half's
                 // first group lands exactly on y = -0)
                 const int pos = sb % gs;
-                if (pos == 0) {
+                if (pos == 0) {  // bitwise fma(dv, tv, -0)
                     asm volatile("" ::: "memory");
-                    gsum[ct] = f32x16(-0.0f);
+                    gsum[ct] = dv * tv;
+                } else {
+                    gsum[ct] = fma_vec(dv, tv, gsum[ct]);
                 }
-                gsum[ct] = gsum[ct] + tv;
                 if (pos == gs - 1 || sb == S - 1) {
                     asm volatile("" ::: "memory");
                     y[ct] = y[ct] + gsum[ct];
@@ -2039,8 +2049,9 @@ __global__ __launch_bounds__(1024) void k_mmqd1(mi_mmx_group g) {
             int T = acc[NP - 1][el];
 #pragma unroll
             for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][el];
-            term[e] = mmqx_term(T, Uv[el], dw, dm, dav[e]);
+            term[e] = mmqx_pre(T, Uv[el], dw, dm);
         }
+        (void) dav;
         *(float4 *) (mine + 4 * g) = make_float4(term[0], term[1], term[2], term[3]);
     }
     mi_lds_barrier();
@@ -2052,8 +2063,10 @@ __global__ __launch_bounds__(1024) void k_mmqd1(mi_mmx_group g) {
     for (int o = 64 * w + lane; o < 1024; o += 64 * S) {
         const int lo = o >> 4, el = o & 15;
         const float * src = red + (size_t) lo * 16 + el;
+        // d_a of superblock v for this output's column (the waves' da rows after the terms)
+        const float * dsrc = red + (size_t) S * 64 * 16 + ((el & 3) + 8 * (el >> 2) + 4 * (lo >> 5));
         float y = -0.0f, ylo = -0.0f, gsum = 0.0f;
-        for (int v = 0; v < ((ABL & 4) ? 1 : S); v++) cfold(gsum, y, ylo, src[(size_t) v * 64 * 16], v, gs, S);
+        for (int v = 0; v < ((ABL & 4) ? 1 : S); v++) cfold(gsum, y, ylo, src[(size_t) v * 64 * 16], dsrc[v * 32], v, gs, S);
         y = cfold_end(ylo, y);
         if (ABL & 4) y = gsum;
         // element el of lane lo = prompt column c0 + (el & 3) + 8 (el >> 2) + 4 (lo >> 5), row n0 + lo % 32
@@ -2166,8 +2179,9 @@ __global__ __launch_bounds__(1024) void k_mmqd16(mi_mmx_group grp) {
             int T = acc[NP - 1][e];
 #pragma unroll
             for (int p = NP - 2; p >= 0; p--) T = (T << F::SHIFT) + acc[p][e];
-            term[e] = mmqx_term(T, Uv[e], dw, dm, dav[e]);
+            term[e] = mmqx_pre(T, Uv[e], dw, dm);
         }
+        (void) dav;
         *(float4 *) mine = make_float4(term[0], term[1], term[2], term[3]);
     }
     mi_lds_barrier();
@@ -2176,10 +2190,11 @@ __global__ __launch_bounds__(1024) void k_mmqd16(mi_mmx_group grp) {
     const int gs = cfold_gs(S);
     for (int v = 0; v < S; v++) {
         const float4 t4 = *(const float4 *) (red + ((size_t) v * 64 + lane) * 4);
-        cfold(gsum.x, y.x, lo.x, t4.x, v, gs, S);
-        cfold(gsum.y, y.y, lo.y, t4.y, v, gs, S);
-        cfold(gsum.z, y.z, lo.z, t4.z, v, gs, S);
-        cfold(gsum.w, y.w, lo.w, t4.w, v, gs, S);
+        const float4 d4 = *(const float4 *) (red + (size_t) S * 64 * 4 + v * 16 + 4 * g);  // d_a of columns 4 g ..
+        cfold(gsum.x, y.x, lo.x, t4.x, d4.x, v, gs, S);
+        cfold(gsum.y, y.y, lo.y, t4.y, d4.y, v, gs, S);
+        cfold(gsum.z, y.z, lo.z, t4.z, d4.z, v, gs, S);
+        cfold(gsum.w, y.w, lo.w, t4.w, d4.w, v, gs, S);
     }
     y = make_float4(cfold_end(lo.x, y.x), cfold_end(lo.y, y.y), cfold_end(lo.z, y.z), cfold_end(lo.w, y.w));
     const int64_t n = n0 + i;
