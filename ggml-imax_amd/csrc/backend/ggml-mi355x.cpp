@@ -2161,7 +2161,7 @@ static int graph_min_launches() {
 }
 
 static constexpr size_t kGraphCacheEntries = 8;
-static constexpr int kGraphMissDirect = 6;
+static constexpr int kGraphMissDirect = 3;
 
 static void gcache_launch(mi_backend_ctx * ctx, mi_backend_ctx::gcache_entry & e) {
     MI_CHECK(hipGraphLaunch(e.exec, ctx->stream));
@@ -2187,7 +2187,7 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
     // A topology whose graphs kept arriving with new kernel arguments and never replayed (a decode
     // step through graph_compute: the KV length moves every call) launches directly: a capture costs
     // a synchronous recording of every launch plus an update per call for nothing, where a direct
-    // launch overlaps host and device. Decided after kGraphMissDirect such captures in a row; the
+    // launch overlaps host and device. Decided after kGraphMissDirect (3) such captures in a row; the
     // key and the preparation are then skipped too. Measured on main-batched.cpp's decode loop
     // (bench gpt2_batched): 4.9 k tokens/s capturing every step vs 6.2-6.5 k direct.
     const uint64_t topo = graph_topology(cgraph);

@@ -1,9 +1,8 @@
 #!/bin/bash
-# Round 4: quick parity of the fused canonical fold and the graph_compute rule
+# Round 4 quick check: graph-capture and GPT-2 GPU tests, then the bench without CPU legs or sweep
 set -eo pipefail
-OUT=gpurun_out/${1:-r04w}; mkdir -p $OUT
+OUT=gpurun_out/${1:-r04y}; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 400 python -u -m pytest tests/test_prefill_gpu.py tests/test_graphs_gpu.py -x -q --timeout 200 --timeout-method thread -m gpu > $OUT/pytest.log 2>&1 && tail -1 $OUT/pytest.log || { grep -E "FAILED|^E " $OUT/pytest.log | head -20; tail -1 $OUT/pytest.log; exit 1; }
-PF_SINGLE=0 PF_R=16 PF_TYPES=q4_K,q5_K MMQ_VARIANTS=0 PF_LONG=0,1 timeout -k 10 300 python3 -u tools/prefill_bench.py 512 64 2>&1 | grep --line-buffered -v amdgpu.ids | tee $OUT/pf.txt
-# one GEMV per graph: grid of 128 / 192 / 256 workgroups (0 = the automatic choice)
-PF_SINGLE=1 PF_R=32 PF_TYPES=q4_K PF_MMV_BLOCKS=0,128,192,256 timeout -k 10 300 python3 -u tools/prefill_bench.py 1 2>&1 | grep --line-buffered -v amdgpu.ids | tee $OUT/pf_single.txt
+timeout -k 10 400 python -u -m pytest tests/test_graphs_gpu.py tests/test_gpt2.py -x -q --timeout 200 --timeout-method thread -m gpu > $OUT/pytest.log 2>&1 && tail -1 $OUT/pytest.log || { grep -E "FAILED|^E " $OUT/pytest.log | head -20; tail -1 $OUT/pytest.log; exit 1; }
+timeout -k 10 400 python -u bench.py --no-cpu --no-sweep > $OUT/bench.json 2> $OUT/bench.err
+python3 -c "import json; d=json.load(open('$OUT/bench.json')); print(d['value'], d['roofline']['frac'], d['roofline']['traffic_source']['file'], d.get('gpt2_batched'))"
