@@ -20,6 +20,7 @@ oracle/_ref/libggml_ref.so, timed on this host -- rank 0, N=1 only) and a per-co
 from __future__ import annotations
 
 import argparse
+import ctypes
 import glob
 import json
 import os
@@ -254,12 +255,21 @@ def gpt2_batched_bench(lib, backend, n_parallel=8, n_steps=48):
             nxt = [int(v) for v in np.argmax(lg, axis=1)]
         return time.perf_counter() - t0
 
+    def stats():
+        a = (ctypes.c_int64 * 6)()
+        lib.ggml_backend_mi355x_graph_stats_ex(backend, a, 6)
+        return list(a)
+
     try:
+        run()  # untimed pass: first captures of each topology, allocator and cache warm-up
+        s0 = stats()
         dt = run()
+        s1 = stats()
         r = {"workload": f"{n_parallel} sequences sharing an 8-token prompt, {n_steps} batched decode steps (main-batched.cpp)",
              "decode_tokens_per_s": round(n_parallel * n_steps / dt, 1), "ms_per_step": round(dt / n_steps * 1e3, 4),
              "kernel_launches_per_step": lib.ggml_backend_mi355x_last_launch_count(backend),
-             "parity": "within 1e-3 of the reference CPU, bit-identical with mmv_order=1 (tests/test_gpt2.py batched tests)"}
+             "parity": "within 1e-3 of the reference CPU, bit-identical with mmv_order=1 (tests/test_gpt2.py batched tests)",
+             "graph_compute_calls": {"direct": s1[3] - s0[3], "replays": s1[4] - s0[4], "captures": s1[5] - s0[5]}}
         if hasattr(lib, "ggml_backend_mi355x_set_graph_capture"):
             lib.ggml_backend_mi355x_set_graph_capture(backend, False)
             try:
