@@ -2856,6 +2856,12 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     return false;
 }
 
+bool ggml_backend_mi355x_stamps_enable(size_t slots) { return mi_stamps_enable(slots); }
+void ggml_backend_mi355x_stamps_reset(void) { mi_stamps_reset(); }
+size_t ggml_backend_mi355x_stamps_read(uint64_t * words, size_t n, char * log, size_t log_size) {
+    return mi_stamps_read(words, n, log, log_size);
+}
+
 bool ggml_backend_mi355x_quantize_activations(ggml_backend_t backend, int vec_dot_type, const float * x, int64_t K,
                                               int64_t ncols, int8_t * qs, float * d, int16_t * s32) {
     MI_ASSERT(ggml_backend_is_mi355x(backend));

@@ -164,6 +164,7 @@ __global__ __launch_bounds__(512) void k_attn_proj(mi_attn_desc a, mi_attn_proj_
     constexpr int RPW = 512 / LPR;       // rows per workgroup
     extern __shared__ __attribute__((aligned(16))) float sm[];  // s[n_kv] | red[8][D + 8] | (16 B aligned) oh[D] f16
     __shared__ float shm[8];
+    MI_STAMP(p.stamps, 0);
     const int rb = blockIdx.x, h = blockIdx.y;
     const int c = threadIdx.x % LPR;
     const int64_t row = (int64_t) rb * RPW + threadIdx.x / LPR;
@@ -171,6 +172,7 @@ __global__ __launch_bounds__(512) void k_attn_proj(mi_attn_desc a, mi_attn_proj_
     const uint4 w = *(const uint4 *) (p.W + rc * p.nb01 + ((size_t) h * D + c * 8) * 2);
     const float e_bias = p.bias[rc], e_res = p.resid[rc];  // requested before the attention too
     const float r = attn_head<D, KPG>(a, h, 0, sm, shm);
+    MI_STAMP(p.stamps, 1);  // the head's attention done
     uint16_t * oh = (uint16_t *) (sm + ((a.n_kv + 3) & ~3) + 8 * (D + 8));  // 16-byte aligned
     if (threadIdx.x < D) oh[threadIdx.x] = mi_f2h(r);
     __syncthreads();
@@ -183,6 +185,7 @@ __global__ __launch_bounds__(512) void k_attn_proj(mi_attn_desc a, mi_attn_proj_
     acc = group_sum<LPR>(acc);
     // head 0: (x + bias) + resid, the order of the unfused epilogue
     if (c == 0 && row < p.N) p.parts[(size_t) h * p.N + row] = h == 0 ? (acc + e_bias) + e_res : acc;
+    MI_STAMP(p.stamps, 7);
 }
 
 // out[i] = sum_h parts[h][i], in head order
@@ -223,8 +226,10 @@ void mi_attn_proj(const mi_attn_desc & a, const mi_attn_proj_desc & p, hipStream
     constexpr int RPW = 512 / (64 / 8);
     const dim3 grid((unsigned) ((p.N + RPW - 1) / RPW), (unsigned) a.H);
     const size_t lds = (size_t) (a.n_kv + 3 + 8 * (a.D + 8) + a.D) * sizeof(float);
-    if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_proj<64, 4>), grid, dim3(512), lds, s, a, p);
-    else hipLaunchKernelGGL((k_attn_proj<64, 8>), grid, dim3(512), lds, s, a, p);
+    mi_attn_proj_desc ps = p;
+    ps.stamps = mi_stamp_take("k_attn_proj", grid.x * grid.y);
+    if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_proj<64, 4>), grid, dim3(512), lds, s, a, ps);
+    else hipLaunchKernelGGL((k_attn_proj<64, 8>), grid, dim3(512), lds, s, a, ps);
 }
 
 void mi_sum_parts(float * out, const float * parts, int nparts, int64_t n, hipStream_t s) {

@@ -12,6 +12,21 @@
 
 #define MI_WAVE 64
 
+// Phase stamp of a diagnostic build: s_memrealtime (the chip-wide 100 MHz counter) of lane 0 of
+// the workgroup's first wave, written with a plain vector store into slot `slot` of the workgroup's
+// 8-slot record in `buf` (a buffer of its own, never an output). Compiled out of release builds.
+#if MI_DIAG
+#define MI_STAMP(buf, slot)                                                                                                \
+    do {                                                                                                                   \
+        if ((buf) && threadIdx.x == 0)                                                                                     \
+            (buf)[((size_t) blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();        \
+    } while (0)
+#else
+#define MI_STAMP(buf, slot) \
+    do {                    \
+    } while (0)
+#endif
+
 // Quantized weight blocks exactly as stored by ggml (src/ggml-common.h:144-300). Kernels read
 // them with aligned 16-byte loads where the block size allows (Q4_K 144 B, Q5_K 176 B).
 struct mi_block_q4_0 { uint16_t d; uint8_t qs[16]; };

@@ -101,8 +101,19 @@ struct mi_mmv_group {
         int mode = 0;  // 0 none, 1 norm, 2 rms_norm
     } pro;
     int pro_off = 0;   // set by the launcher: LDS byte offset of the normalized columns
+    uint64_t * stamps = nullptr;  // diagnostic builds: per-workgroup phase stamps (g_mi_stamp_dev)
     mi_mmv_member m[kMiMaxMembers];
 };
+// Diagnostic builds (make DIAG=1): when non-null, the decode kernels write s_memrealtime phase
+// stamps of wave 0 of every workgroup here (kMiStampSlots per workgroup); release builds never do
+extern uint64_t * g_mi_stamp_dev;
+constexpr int kMiStampSlots = 8;
+bool mi_stamps_enable(size_t slots);  // 0: off; false in release builds
+void mi_stamps_reset();
+// the next launch's stamp range (nullptr when off or full); logs "name nblocks offset"
+uint64_t * mi_stamp_take(const char * name, unsigned nblocks);
+// copies up to n stamp words and the log; returns the words written so far
+size_t mi_stamps_read(uint64_t * host, size_t n, char * log, size_t log_size);
 bool mi_mmv_fused_supported(int type, int64_t K, int64_t ncols);
 constexpr int64_t kMiMmvProMaxK = 768;  // norm prologue: the column is held in one wave's registers
 
@@ -258,6 +269,7 @@ struct mi_f16_epilogue {
         char * ptr = nullptr;
         size_t col_stride = 0;
     } copy[2];
+    uint64_t * stamps = nullptr;  // diagnostic builds: phase stamps (g_mi_stamp_dev)
 };
 // optional prologue: src1 = add(mul(norm|rms_norm(x, eps), g), b) computed in the kernel from x
 struct mi_norm_prologue {
@@ -315,6 +327,7 @@ struct mi_attn_proj_desc {
     const float * bias;   // [N]
     const float * resid;  // [N]
     float * parts;        // [H][N]
+    uint64_t * stamps = nullptr;  // diagnostic builds: phase stamps (g_mi_stamp_dev)
 };
 bool mi_attn_proj_supported(const mi_attn_desc & a, int64_t K, int64_t N, size_t nb01, const void * W);
 void mi_attn_proj(const mi_attn_desc & a, const mi_attn_proj_desc & p, hipStream_t s);

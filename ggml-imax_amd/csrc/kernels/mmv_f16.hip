@@ -178,6 +178,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
                                                   float * __restrict__ dst, size_t ycol, mi_f16_epilogue e, mi_norm_prologue pro,
                                                   int64_t kp, int rgs) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][kp] f16 (zero beyond K), then [waves][4][NC] f32
+    MI_STAMP(e.stamps, 0);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x >> 6) / rgs;
     const int grp = wid / nw, wave = wid % nw;  // row group, K slice
     const int m = lane & (kLpr - 1), rg = lane >> 4;
@@ -246,6 +247,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
         st.column((const float *) (x.base + c0 * x.nb1), K, kp, xs, (int64_t) JX * blockDim.x);
         for (int c = 1; c < nc; c++) st.column((const float *) (x.base + (c0 + c) * x.nb1), K, kp, xs + (size_t) c * kp, 0);
     }
+    MI_STAMP(e.stamps, 1);  // activations staged (normalized) by wave 0
     if (!priv) mi_lds_barrier();
 
     float acc[NC];
@@ -277,6 +279,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
         }
     }
 
+    MI_STAMP(e.stamps, 3);  // wave 0's dots done (its weights landed)
     // this wave's row totals in every lane of the row; lane m < nc holds column m
     float mine = 0.0f;
 #pragma unroll
@@ -308,6 +311,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
                 *(float *) (e.copy[k].ptr + col * e.copy[k].col_stride + (row - e.copy[k].row0) * sizeof(float)) = v;
         }
     }
+    MI_STAMP(e.stamps, 7);
 }
 
 // Tall matrices (lm_head, N = 50257): one column, rows in one register pass (K <= 128 U). A
@@ -320,6 +324,7 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
                                                        mi_src_cols x, float * __restrict__ dst, mi_f16_epilogue e,
                                                        mi_norm_prologue pro, int64_t kp) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [kp] f16
+    MI_STAMP(e.stamps, 0);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int m = lane & (kLpr - 1), rg = lane >> 4;
     const int64_t ngroups = (N + 3) / 4, stride = (int64_t) gridDim.x * 4;
@@ -355,6 +360,7 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
         st.column((const float *) x.base, K, kp, xs, (int64_t) 4 * blockDim.x);
     }
     mi_lds_barrier();
+    MI_STAMP(e.stamps, 2);
 
     for (; grp < ngroups; grp += stride) {
         uint4 nxt[U];
@@ -380,6 +386,7 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
         for (int u = 0; u < U; u++) cur[u] = nxt[u];
         eb = ebn;
     }
+    MI_STAMP(e.stamps, 7);
 }
 
 // The F16 GEMV of one column whose input is a norm chain over a value still held as partial sums
@@ -395,6 +402,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
                                                      float * __restrict__ dst, mi_f16_epilogue e, mi_norm_prologue pro, int64_t kp) {
     const int rw = blockDim.x >> 6;
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [rw][kp] f16 per wave, then [kp] f32 (the sum)
+    MI_STAMP(e.stamps, 0);
     float * xf = (float *) (xs + (size_t) rw * kp);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int m = lane & (kLpr - 1), rg = lane >> 4;
@@ -452,7 +460,9 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
             if (blockIdx.x == 0) *(float4 *) (pro.store + q4) = sum;
         }
     }
+    MI_STAMP(e.stamps, 1);  // parts landed and summed (wave 0)
     __syncthreads();
+    MI_STAMP(e.stamps, 2);
     float4 v[JM];
 #pragma unroll
     for (int j = 0; j < JM; j++) {
@@ -461,6 +471,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
     }
     uint16_t * xw = xs + (size_t) wid * kp;
     norm_store<JM, true>(v, pg, pb, K, kp, pro, xw, lane);
+    MI_STAMP(e.stamps, 4);  // normalized
 
     float acc = 0.0f;
 #pragma unroll
@@ -479,6 +490,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
                 *(float *) (e.copy[k].ptr + (row - e.copy[k].row0) * sizeof(float)) = r;
         }
     }
+    MI_STAMP(e.stamps, 7);
 }
 
 template <int NC, int U, bool ONE, int JM>
@@ -490,7 +502,9 @@ void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_c
     const size_t lds = (size_t) (priv ? ks : NC) * kp * sizeof(uint16_t) + (size_t) ks * rgs * 4 * NC * sizeof(float);
     const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
     const uint8_t * w = (const uint8_t *) W;
-#define MI_GEMV_F16(EP) hipLaunchKernelGGL((k_gemv_f16<NC, EP, U, ONE, JM>), grid, dim3(64 * ks * rgs), lds, s, w, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, kp, rgs)
+    mi_f16_epilogue es = e;
+    es.stamps = mi_stamp_take(JM ? "k_gemv_f16_norm" : "k_gemv_f16", grid.x * grid.y);
+#define MI_GEMV_F16(EP) hipLaunchKernelGGL((k_gemv_f16<NC, EP, U, ONE, JM>), grid, dim3(64 * ks * rgs), lds, s, w, nb01, K, N, x, xh, ncols, dst, ycol, es, pro, kp, rgs)
     switch (epi) {
         case 0: MI_GEMV_F16(0); break;
         case 1: MI_GEMV_F16(1); break;
@@ -561,7 +575,9 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         const size_t lds = (size_t) kp * sizeof(uint16_t);
         const int epi = e.gelu_table ? 3 : (e.bias ? 1 : 0);
         const uint8_t * w = (const uint8_t *) W;
-#define MI_GEMV_TALL(EP, JMV) hipLaunchKernelGGL((k_gemv_f16_tall<EP, 8, JMV>), grid, dim3(256), lds, s, w, nb01, K, N, x, dst, e, pro, kp)
+        mi_f16_epilogue es = e;
+        es.stamps = mi_stamp_take("k_gemv_f16_tall", grid.x);
+#define MI_GEMV_TALL(EP, JMV) hipLaunchKernelGGL((k_gemv_f16_tall<EP, 8, JMV>), grid, dim3(256), lds, s, w, nb01, K, N, x, dst, es, pro, kp)
         if (pro.mode) {
             if (epi == 0) MI_GEMV_TALL(0, 4); else if (epi == 1) MI_GEMV_TALL(1, 4); else MI_GEMV_TALL(3, 4);
         } else {
@@ -580,7 +596,9 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         const size_t lds = (size_t) rw * kp * sizeof(uint16_t) + (size_t) kp * sizeof(float);
         const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
         const uint8_t * w = (const uint8_t *) W;
-#define MI_GEMV_PS(EP, NPM, QPT) hipLaunchKernelGGL((k_gemv_f16_ps<EP, 8, 4, NPM, QPT>), grid, dim3(64 * rw), lds, s, w, nb01, K, N, dst, e, pro, kp)
+        mi_f16_epilogue es = e;
+        es.stamps = mi_stamp_take("k_gemv_f16_ps", grid.x);
+#define MI_GEMV_PS(EP, NPM, QPT) hipLaunchKernelGGL((k_gemv_f16_ps<EP, 8, 4, NPM, QPT>), grid, dim3(64 * rw), lds, s, w, nb01, K, N, dst, es, pro, kp)
 #define MI_GEMV_PS_E(NPM, QPT)                     \
         switch (epi) {                             \
             case 0: MI_GEMV_PS(0, NPM, QPT); break; \

@@ -31,7 +31,11 @@
 #include "cpu_order.h"
 #pragma clang fp contract(fast)
 
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+
+#include <string>
 
 static int env_int(const char * name, int def) {
     const char * v = getenv(name);
@@ -41,6 +45,63 @@ static int env_int(const char * name, int def) {
 // mmv_blocks == 0: size the grid from the kernel's residency (hipOccupancy...) per instance
 mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 0), env_int("GGML_MI355X_MMV_VARIANT", 0), env_int("GGML_MI355X_F16_VARIANT", 0), 0, env_int("GGML_MI355X_MMQ_VARIANT", 0), env_int("GGML_MI355X_ATTN_VARIANT", 0), env_int("GGML_MI355X_ATTN_ABL", 0), env_int("GGML_MI355X_MMV_ORDER", -1), env_int("GGML_MI355X_F16_WAVES", 0), env_int("GGML_MI355X_F16_RGS", 0), env_int("GGML_MI355X_F16_PS_WAVES", 0), env_int("GGML_MI355X_MMQ_LONG", 0)};
 thread_local int tl_mi_graph_order = 0;
+
+// ---- diagnostic phase stamps (make DIAG=1 builds; MI_STAMP in mi355x_common.h) ----
+// A device buffer of kMiStampSlots words per workgroup and launch; each instrumented launch takes
+// the next range (mi_stamp_take) and the host log records (kernel, workgroups, offset) so a tool
+// can rebuild the device timeline: per-launch first-start / last-end and per-workgroup phases.
+uint64_t * g_mi_stamp_dev = nullptr;
+static size_t g_mi_stamp_cap = 0, g_mi_stamp_cur = 0;
+static std::string g_mi_stamp_log;
+
+bool mi_stamps_enable(size_t slots) {
+#if MI_DIAG
+    if (g_mi_stamp_dev) (void) hipFree(g_mi_stamp_dev);
+    g_mi_stamp_dev = nullptr;
+    g_mi_stamp_cap = g_mi_stamp_cur = 0;
+    g_mi_stamp_log.clear();
+    if (slots == 0) return true;
+    if (hipMalloc(&g_mi_stamp_dev, slots * sizeof(uint64_t)) != hipSuccess) {
+        g_mi_stamp_dev = nullptr;
+        return false;
+    }
+    (void) hipMemset(g_mi_stamp_dev, 0, slots * sizeof(uint64_t));
+    g_mi_stamp_cap = slots;
+    return true;
+#else
+    (void) slots;
+    return false;  // release build: the kernels carry no stamps
+#endif
+}
+
+void mi_stamps_reset() {
+    g_mi_stamp_cur = 0;
+    g_mi_stamp_log.clear();
+}
+
+uint64_t * mi_stamp_take(const char * name, unsigned nblocks) {
+    if (!g_mi_stamp_dev) return nullptr;
+    const size_t need = (size_t) nblocks * kMiStampSlots;
+    if (g_mi_stamp_cur + need > g_mi_stamp_cap) return nullptr;
+    uint64_t * p = g_mi_stamp_dev + g_mi_stamp_cur;
+    char line[160];
+    snprintf(line, sizeof line, "%s %u %zu\n", name, nblocks, g_mi_stamp_cur);
+    g_mi_stamp_log += line;
+    g_mi_stamp_cur += need;
+    return p;
+}
+
+size_t mi_stamps_read(uint64_t * host, size_t n, char * log, size_t log_size) {
+    if (!g_mi_stamp_dev) return 0;
+    const size_t m = n < g_mi_stamp_cur ? n : g_mi_stamp_cur;
+    if (host && m) (void) hipMemcpy(host, g_mi_stamp_dev, m * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (log && log_size) {
+        const size_t k = g_mi_stamp_log.size() < log_size - 1 ? g_mi_stamp_log.size() : log_size - 1;
+        memcpy(log, g_mi_stamp_log.data(), k);
+        log[k] = 0;
+    }
+    return g_mi_stamp_cur;
+}
 
 namespace {
 
@@ -560,6 +621,7 @@ __device__ __forceinline__ void store_out(const mi_mmv_group & g, float * dst, i
 template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO>
 __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    MI_STAMP(g.stamps, 0);
     constexpr int NB = PD + 1;  // ring slots
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -653,7 +715,9 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
             }
         }
     }
+    MI_STAMP(g.stamps, 1);  // wave 0's activation slices loaded and quantized
     __syncthreads();
+    MI_STAMP(g.stamps, 2);  // every wave's
 
     // 3) stream: ring slot u holds row k0+u; refill it with row k0+u+PD right before using it
     //    (the last row again past the end: an L2 hit)
@@ -756,8 +820,10 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                 const float v = mi_wave_sum_u(acc[c]);
                 if (lane == 0 && c < ncols) store_out<PRO>(g, dst, c, row, v);
             }
+            if (k == 0) MI_STAMP(g.stamps, 3);  // first row reduced and stored
         }
     }
+    MI_STAMP(g.stamps, 7);
 }
 
 // Workgroups that fit on the chip at once for this kernel instance (all of them are launched
@@ -839,6 +905,7 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
     rows = (rows + 3) / 4 * 4;
     g.rows_per_block = rows;
     g.blocks_per_member = (int) ((g.N + rows - 1) / rows);
+    g.stamps = mi_stamp_take(ORD ? "k_mmv_stream_ord" : "k_mmv_stream", (unsigned) (g.blocks_per_member * g.n));
     hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL, TAIL, ORD, PRO>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds,
                        s, g);
 }

@@ -205,7 +205,8 @@ __device__ __forceinline__ float emb_elem(const mi_tensor_desc & a, int32_t r, i
 // id is still in flight (vmcnt retires in issue order).
 template <int TA, int TB>
 __global__ __launch_bounds__(256) void k_get_rows_add(mi_tensor_desc d, mi_tensor_desc a, mi_tensor_desc ia, mi_tensor_desc b,
-                                                      mi_tensor_desc ib, int ne0) {
+                                                      mi_tensor_desc ib, int ne0, uint64_t * st) {
+    MI_STAMP(st, 0);
     const int r = (int) blockIdx.y;
     const int32_t rb = *(const int32_t *) (ib.data + (size_t) r * ib.nb[0]);
     const int32_t ra = *(const int32_t *) (ia.data + (size_t) r * ia.nb[0]);
@@ -214,6 +215,7 @@ __global__ __launch_bounds__(256) void k_get_rows_add(mi_tensor_desc d, mi_tenso
         const float va = emb_elem<TA>(a, ra, c);
         *(float *) (d.data + (size_t) c * d.nb[0] + (size_t) r * d.nb[1]) = va + vb;
     }
+    MI_STAMP(st, 7);
 }
 
 __global__ __launch_bounds__(256) void k_diag_mask(mi_tensor_desc d, mi_tensor_desc a, int n_past, float value, int64_t n) {
@@ -470,12 +472,13 @@ static void launch_get_rows_add(const mi_tensor_desc & d, const mi_tensor_desc &
         ibc.data += r0 * ib.nb[0];
         dc.ne[1] = nr;
         const dim3 g((unsigned) std::min<int64_t>((ne0 + 1023) / 1024, 64), (unsigned) nr);
+        uint64_t * st = mi_stamp_take("k_get_rows_add", g.x * g.y);
         switch (b.type) {
-            case 2: hipLaunchKernelGGL((k_get_rows_add<TA, 2>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
-            case 8: hipLaunchKernelGGL((k_get_rows_add<TA, 8>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
-            case 12: hipLaunchKernelGGL((k_get_rows_add<TA, 12>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
-            case 13: hipLaunchKernelGGL((k_get_rows_add<TA, 13>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
-            default: hipLaunchKernelGGL((k_get_rows_add<TA, 0>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0); break;
+            case 2: hipLaunchKernelGGL((k_get_rows_add<TA, 2>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
+            case 8: hipLaunchKernelGGL((k_get_rows_add<TA, 8>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
+            case 12: hipLaunchKernelGGL((k_get_rows_add<TA, 12>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
+            case 13: hipLaunchKernelGGL((k_get_rows_add<TA, 13>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
+            default: hipLaunchKernelGGL((k_get_rows_add<TA, 0>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
         }
     }
 }

@@ -89,6 +89,17 @@ GGML_API bool ggml_backend_mi355x_set_tuning(const char * name, int value);
 GGML_API bool ggml_backend_mi355x_quantize_activations(ggml_backend_t backend, int vec_dot_type, const float * x,
                                                        int64_t K, int64_t ncols, int8_t * qs, float * d, int16_t * s32);
 
+// Device phase stamps (diagnostic builds, `make -C ggml-imax_amd diaglib`): with slots > 0 the
+// decode kernels (k_mmv_stream, the F16 GEMVs, k_attn_proj, k_get_rows_add) write s_memrealtime
+// stamps (100 MHz chip clock) of every workgroup's first wave into a device buffer of `slots` words,
+// 8 per workgroup and launch, in launch order; slots = 0 turns them off. Returns false in release
+// builds (whose kernels carry no stamps). _read copies up to n words into `words` and the launch
+// log ("kernel workgroups offset" lines) into `log`, and returns the number of words written since
+// the last _reset.
+GGML_API bool ggml_backend_mi355x_stamps_enable(size_t slots);
+GGML_API void ggml_backend_mi355x_stamps_reset(void);
+GGML_API size_t ggml_backend_mi355x_stamps_read(uint64_t * words, size_t n, char * log, size_t log_size);
+
 #ifdef __cplusplus
 }
 #endif
