@@ -2162,6 +2162,7 @@ static int graph_min_launches() {
 
 static constexpr size_t kGraphCacheEntries = 8;
 static constexpr int kGraphMissDirect = 3;
+static constexpr int kGraphRetry = 32;
 
 static void gcache_launch(mi_backend_ctx * ctx, mi_backend_ctx::gcache_entry & e) {
     MI_CHECK(hipGraphLaunch(e.exec, ctx->stream));
@@ -2190,12 +2191,19 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
     // launch overlaps host and device. Decided after kGraphMissDirect (3) such captures in a row; the
     // key and the preparation are then skipped too. Measured on main-batched.cpp's decode loop
     // (bench gpt2_batched): 4.9 k tokens/s capturing every step vs 6.2-6.5 k direct.
+    // The decision decays: every kGraphRetry-th direct run of such a topology looks its key up
+    // again, and a replay (a graph that does repeat) resets the count; set_graph_capture resets all.
     const uint64_t topo = graph_topology(cgraph);
+    bool direct_only = false;
     {
         auto m = ctx->topo_misses.find(topo);
         if (m != ctx->topo_misses.end() && m->second >= kGraphMissDirect) {
-            ctx->graph_stats[3]++;
-            return mi_graph_launch_nodes(ctx, cgraph);
+            m->second++;
+            if ((m->second - kGraphMissDirect) % kGraphRetry != 0) {
+                ctx->graph_stats[3]++;
+                return mi_graph_launch_nodes(ctx, cgraph);
+            }
+            direct_only = true;
         }
     }
     prepare_for_capture(ctx, cgraph);
@@ -2208,6 +2216,10 @@ static enum ggml_status mi_graph_compute(ggml_backend_t backend, ggml_cgraph * c
             gcache_launch(ctx, e);
             return GGML_STATUS_SUCCESS;
         }
+    }
+    if (direct_only) {
+        ctx->graph_stats[3]++;
+        return mi_graph_launch_nodes(ctx, cgraph);
     }
     auto seen = ctx->topo_launches.find(topo);
     if (seen == ctx->topo_launches.end() || seen->second < graph_min_launches()) {
@@ -2377,19 +2389,17 @@ static enum ggml_status mi_graph_plan_compute(ggml_backend_t backend, ggml_backe
 // (tests/test_gpt2.py::test_reference_quantized_gpt2_is_ulp_sensitive): such graphs run every decode
 // reduction in the reference CPU's order (bit-identical). Any other graph (F16 models, a mul_mat of
 // input data) keeps the tree order, within 1e-5 of the reference per op.
-// A split input of the reference scheduler is a NONE tensor holding a value another split computed:
-// ggml_backend_sched_split_graph creates it with ggml_dup_tensor_layout and names it
-// "<backend>#<source name>#<copy>" (ggml-backend.c:1498-1523), so it counts as computed here.
-static bool sched_split_copy(const ggml_tensor * t) {
-    const char * a = strchr(t->name, '#');
-    if (!a || a == t->name) return false;
-    const char * b = strrchr(t->name, '#');
-    if (b == a || b[1] == '\0') return false;
-    for (const char * c = b + 1; *c; c++) if (*c < '0' || *c > '9') return false;
-    return true;
-}
+// A split input of the reference scheduler is a NONE tensor holding a value another split computed
+// (ggml_backend_sched_split_graph creates it with ggml_dup_tensor_layout, ggml-backend.c:1498-1523).
+// It cannot be told from a true graph input by its own fields (flags are set only when n_copies > 1,
+// names may be truncated), but the graph says where it came from: the scheduler hands a backend
+// views of its splits (ggml_graph_view, ggml-backend.c:1549: size 0, no hash table), and a full
+// graph never holds such copies. So in a split view every NONE source counts as computed -- the
+// reference order, bit-identical either way -- and in a full graph as input.
+static bool sched_split_view(const ggml_cgraph * g) { return g->size == 0 && g->visited_hash_table.size == 0; }
 
 static int graph_decode_order(const ggml_cgraph * g) {
+    const bool view = sched_split_view(g);
     for (int i = 0; i < g->n_nodes; i++) {
         const ggml_tensor * n = g->nodes[i];
         if (n->op != GGML_OP_MUL_MAT || !ggml_is_quantized(n->src[0]->type)) continue;
@@ -2398,7 +2408,7 @@ static int graph_decode_order(const ggml_cgraph * g) {
                x->op == GGML_OP_TRANSPOSE) {
             x = x->view_src ? x->view_src : x->src[0];
         }
-        if (x->op != GGML_OP_NONE || sched_split_copy(x)) return 1;
+        if (x->op != GGML_OP_NONE || view) return 1;
     }
     return 0;
 }
@@ -2793,6 +2803,7 @@ void ggml_backend_mi355x_set_graph_capture(ggml_backend_t backend, bool enable) 
     auto * ctx = (mi_backend_ctx *) backend->context;
     ctx->graphs = enable;
     ctx->graph_fail_streak = 0;
+    ctx->topo_misses.clear();  // topologies switched to direct launch get captured again
 }
 
 void ggml_backend_mi355x_set_perf(ggml_backend_t backend, bool enable) {
@@ -2829,12 +2840,17 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.mmq_variant = value;
         return true;
     }
-    if (strcmp(name, "mmq_long") == 0 && value >= 0 && value <= 23) {  // (16-23: diagnostic builds only)
+    if (strcmp(name, "mmq_long") == 0 && ((value >= 0 && value <= 2) || (mi_diag_build() && value >= 16 && value <= 23))) {
+        // 0 auto, 1 k_mmqw, 2 k_mmqt; 16-23 k_mmqt stamps / ablations (diagnostic builds only)
         g_mi_tuning.mmq_long = value;
         return true;
     }
     if (strcmp(name, "mmv_order") == 0 && value >= -1 && value <= 1) {
         g_mi_tuning.mmv_order = value;
+        return true;
+    }
+    if (strcmp(name, "xfirst") == 0 && (value == 0 || value == 1)) {
+        g_mi_tuning.xfirst = value;
         return true;
     }
     if (strcmp(name, "f16_waves") == 0 && value >= 0) {

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(512) void k_attn_tree(mi_attn_desc a) {
 // projection's final output; the consumer (mi_sum_parts, or the next GEMV's norm prologue) adds
 // the H partials. Each workgroup of a head repeats that head's attention (K/V rows from L2).
 // Weights: D / 8 lanes per row, one 16-byte chunk each, requested before the attention.
-template <int D, int KPG>
+template <int D, int KPG, bool XF>
 __global__ __launch_bounds__(512) void k_attn_proj(mi_attn_desc a, mi_attn_proj_desc p) {
     constexpr int LPR = D / 8;           // lanes per weight row
     constexpr int RPW = 512 / LPR;       // rows per workgroup
@@ -169,9 +169,14 @@ __global__ __launch_bounds__(512) void k_attn_proj(mi_attn_desc a, mi_attn_proj_
     const int c = threadIdx.x % LPR;
     const int64_t row = (int64_t) rb * RPW + threadIdx.x / LPR;
     const int64_t rc = row < p.N ? row : p.N - 1;
-    const uint4 w = *(const uint4 *) (p.W + rc * p.nb01 + ((size_t) h * D + c * 8) * 2);
+    // the projection's weights: requested before the attention (their latency hidden under it), or
+    // with xfirst after it, so that the attention's q / K / V loads do not queue behind them
+    const uint8_t * wp = p.W + rc * p.nb01 + ((size_t) h * D + c * 8) * 2;
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (!XF) w = *(const uint4 *) wp;
     const float e_bias = p.bias[rc], e_res = p.resid[rc];  // requested before the attention too
     const float r = attn_head<D, KPG>(a, h, 0, sm, shm);
+    if constexpr (XF) w = *(const uint4 *) wp;
     MI_STAMP(p.stamps, 1);  // the head's attention done
     uint16_t * oh = (uint16_t *) (sm + ((a.n_kv + 3) & ~3) + 8 * (D + 8));  // 16-byte aligned
     if (threadIdx.x < D) oh[threadIdx.x] = mi_f2h(r);
@@ -228,8 +233,13 @@ void mi_attn_proj(const mi_attn_desc & a, const mi_attn_proj_desc & p, hipStream
     const size_t lds = (size_t) (a.n_kv + 3 + 8 * (a.D + 8) + a.D) * sizeof(float);
     mi_attn_proj_desc ps = p;
     ps.stamps = mi_stamp_take("k_attn_proj", grid.x * grid.y);
-    if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_proj<64, 4>), grid, dim3(512), lds, s, a, ps);
-    else hipLaunchKernelGGL((k_attn_proj<64, 8>), grid, dim3(512), lds, s, a, ps);
+    if (g_mi_tuning.xfirst) {
+        if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_proj<64, 4, true>), grid, dim3(512), lds, s, a, ps);
+        else hipLaunchKernelGGL((k_attn_proj<64, 8, true>), grid, dim3(512), lds, s, a, ps);
+    } else {
+        if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_proj<64, 4, false>), grid, dim3(512), lds, s, a, ps);
+        else hipLaunchKernelGGL((k_attn_proj<64, 8, false>), grid, dim3(512), lds, s, a, ps);
+    }
 }
 
 void mi_sum_parts(float * out, const float * parts, int nparts, int64_t n, hipStream_t s) {

@@ -110,6 +110,7 @@ extern uint64_t * g_mi_stamp_dev;
 constexpr int kMiStampSlots = 8;
 bool mi_stamps_enable(size_t slots);  // 0: off; false in release builds
 void mi_stamps_reset();
+bool mi_diag_build();  // this library's kernels were built with MI_DIAG (make diaglib)
 // the next launch's stamp range (nullptr when off or full); logs "name nblocks offset"
 uint64_t * mi_stamp_take(const char * name, unsigned nblocks);
 // copies up to n stamp words and the log; returns the words written so far
@@ -133,6 +134,7 @@ struct mi_tuning {
     int f16_rgs;      // fast F16 decode GEMV: row groups (4 rows) per workgroup (0 = automatic)
     int f16_ps_waves; // k_gemv_f16_ps (GEMV over summed partials): waves per workgroup, 2 / 4 / 8 (0 = automatic)
     int mmq_long;     // Q4_K / Q5_K prefill past 128 columns: 0 = automatic (Q4_K k_mmqt, Q5_K k_mmqw), 1 = k_mmqw, 2 = k_mmqt; 16-23 k_mmqt stamps (diagnostic builds)
+    int xfirst;       // lone decode GEMVs: activation loads issued and landed before the weight loads (1) or not (0)
 };
 extern mi_tuning g_mi_tuning;
 // the order of the graph being launched when mmv_order is -1 (set by the backend per graph)
@@ -270,6 +272,7 @@ struct mi_f16_epilogue {
         size_t col_stride = 0;
     } copy[2];
     uint64_t * stamps = nullptr;  // diagnostic builds: phase stamps (g_mi_stamp_dev)
+    int xfirst = 0;               // set by the launcher (g_mi_tuning.xfirst): activations landed before the weight loads
 };
 // optional prologue: src1 = add(mul(norm|rms_norm(x, eps), g), b) computed in the kernel from x
 struct mi_norm_prologue {

@@ -2296,7 +2296,23 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     // prompt's column shards give the whole prompt's bits whichever kernel runs them (variant bit
     // 128 forces k_mmqx, 16 the short-prompt kernels).
     const int var = g_mi_tuning.mmq_variant;
-    const bool direct = (var & 16) || (ncols <= 128 && !(var & 128));
+    // k_mmqx / k_mmqw park the low half of the canonical fold in their own output locations until
+    // the end: only plain device memory of this device may be used that way. An output in pinned
+    // host memory (host-staged logits) or on a peer device takes the pipelined 32 x 32 tiles, which
+    // store each element once (the same bits: the family's canonical combine).
+    bool dst_local = true;
+    for (int i = 0; i < g.n && dst_local; i++) {
+        hipPointerAttribute_t pa;
+        int dev = 0;
+        (void) hipGetDevice(&dev);
+        if (hipPointerGetAttributes(&pa, g.m[i].dst) != hipSuccess) {
+            (void) hipGetLastError();
+            dst_local = false;  // unknown to HIP: plain host memory
+        } else {
+            dst_local = pa.type == hipMemoryTypeDevice && pa.device == dev;
+        }
+    }
+    const bool direct = (var & 16) || (ncols <= 128 && !(var & 128)) || !dst_local;
     if (direct) {
         const int S = (int) (K / 256);
         const int64_t lim16 = (var & (1 << 22)) ? 128 : 16;  // bit 2^22: 16 x 16 tiles up to 128 columns

@@ -218,6 +218,8 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
         if (EPI >= 1) e_bias = e.bias[rc];
         if (EPI == 2) e_res = *(const float *) (e.resid + cc * e.resid_nb1 + rc * sizeof(float));
     }
+    // xfirst: the activation-side loads land before any weight load is queued behind them
+    if (e.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint4 cur[U];
 #pragma unroll
     for (int u = 0; u < U; u++) cur[u] = ld(u);
@@ -350,6 +352,7 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
     ColStager<4> st;
     if constexpr (JM > 0) norm_load<JM, GB>((const float *) x.base, K, lane, pro, pv, pg, pb);
     else st.load((const float *) x.base, K, 0);
+    if (e.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint4 cur[U];
     float eb = 0.0f;
     load_group(cur, eb, grp);
@@ -436,6 +439,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
         if (EPI >= 1) e_bias = e.bias[rc];
         if (EPI == 2) e_res = *(const float *) (e.resid + rc * sizeof(float));
     }
+    if (e.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint4 cur[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -504,6 +508,7 @@ void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_c
     const uint8_t * w = (const uint8_t *) W;
     mi_f16_epilogue es = e;
     es.stamps = mi_stamp_take(JM ? "k_gemv_f16_norm" : "k_gemv_f16", grid.x * grid.y);
+    es.xfirst = g_mi_tuning.xfirst;
 #define MI_GEMV_F16(EP) hipLaunchKernelGGL((k_gemv_f16<NC, EP, U, ONE, JM>), grid, dim3(64 * ks * rgs), lds, s, w, nb01, K, N, x, xh, ncols, dst, ycol, es, pro, kp, rgs)
     switch (epi) {
         case 0: MI_GEMV_F16(0); break;
@@ -577,6 +582,7 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         const uint8_t * w = (const uint8_t *) W;
         mi_f16_epilogue es = e;
         es.stamps = mi_stamp_take("k_gemv_f16_tall", grid.x);
+        es.xfirst = g_mi_tuning.xfirst;
 #define MI_GEMV_TALL(EP, JMV) hipLaunchKernelGGL((k_gemv_f16_tall<EP, 8, JMV>), grid, dim3(256), lds, s, w, nb01, K, N, x, dst, es, pro, kp)
         if (pro.mode) {
             if (epi == 0) MI_GEMV_TALL(0, 4); else if (epi == 1) MI_GEMV_TALL(1, 4); else MI_GEMV_TALL(3, 4);
@@ -598,6 +604,7 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         const uint8_t * w = (const uint8_t *) W;
         mi_f16_epilogue es = e;
         es.stamps = mi_stamp_take("k_gemv_f16_ps", grid.x);
+        es.xfirst = g_mi_tuning.xfirst;
 #define MI_GEMV_PS(EP, NPM, QPT) hipLaunchKernelGGL((k_gemv_f16_ps<EP, 8, 4, NPM, QPT>), grid, dim3(64 * rw), lds, s, w, nb01, K, N, dst, es, pro, kp)
 #define MI_GEMV_PS_E(NPM, QPT)                     \
         switch (epi) {                             \

@@ -1,0 +1,901 @@
+// mmv_fused_impl.h -- the streaming decode GEMV k_mmv_stream (see mmv_fused.hip for the design),
+// its weight-format policies and launchers. Included by one translation unit per weight format
+// (mmv_fused_q4k.hip, _q5k, _q40, _q80) so that the kernel instances compile in parallel; each
+// exports one mi_mmv_launch_* entry point that mmv_fused.hip's dispatcher calls.
+#pragma once
+
+#include <type_traits>
+
+#include "mi355x_common.h"
+#include "mi355x_kernels.h"
+
+// the norm prologue replays the CPU's rounding (cpu_order.h turns FMA contraction off); the rest
+// of this file keeps the default contraction
+#include "cpu_order.h"
+#pragma clang fp contract(fast)
+
+namespace {
+
+// ------------------------------------------------------------------ activations in LDS
+// layout per member: qs [NC][K] int8 | d [NC][K/QKA] f32 | s32 [NC][K/32] int16
+
+struct lds_act {
+    int8_t * qs;
+    float * d;
+    int16_t * s32;
+};
+
+template <int QKA>
+__device__ __forceinline__ lds_act lds_carve(uint8_t * lds, int NC, int64_t K) {
+    lds_act a;
+    a.qs = (int8_t *) lds;
+    a.d = (float *) (lds + NC * K);
+    a.s32 = (int16_t *) (lds + NC * K + NC * (K / QKA) * 4);
+    return a;
+}
+
+template <int QKA>
+__host__ __device__ constexpr size_t lds_bytes(int NC, int64_t K) {
+    return (size_t) NC * (K + (K / QKA) * 4 + (K / 32) * 2);
+}
+
+// reference-order scratch (per wave: rows x columns x F::ord_words), after the activations
+__host__ __device__ constexpr size_t ord_offset(size_t act) { return (act + 15) & ~(size_t) 15; }
+
+// one 256-element slice (four floats per lane) of column c into LDS
+template <int QKA>
+__device__ __forceinline__ void quantize_slice(float4 v4, int lane, const lds_act & a, int64_t K, int c, int sl) {
+    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+    int8_t * qs = a.qs + c * K + sl * 256;
+    if constexpr (QKA == 256) {
+        // Q8_K (quantize_row_q8_K_reference as the reference's gcc -mfma build rounds it)
+        uint32_t packed;
+        int sum32;
+        float dd;
+        mi_q8K_superblock(v, lane, packed, sum32, dd);
+        *(uint32_t *) (qs + lane * 4) = packed;
+        if ((lane & 7) == 0) a.s32[c * (K / 32) + sl * 8 + (lane >> 3)] = (int16_t) sum32;
+        if (lane == 0) a.d[c * (K / 256) + sl] = dd;
+    } else {
+        // Q8_0, AVX2 branch of quantize_row_q8_0 (src/ggml-quants.c:535-618): per 32-block
+        // amax, d = amax/127 -> fp16 (RNE), id = 127/amax, q = round-half-even(x*id).
+        // 8 lanes hold one block; max over the 8-lane group with DPP.
+        float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+        uint32_t ab = __float_as_uint(am);
+        ab = max(ab, (uint32_t) mi_dpp<MI_DPP_QP_1032>(0, (int) ab));
+        ab = max(ab, (uint32_t) mi_dpp<MI_DPP_QP_2301>(0, (int) ab));
+        ab = max(ab, (uint32_t) mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, (int) ab));
+        const float amax = __uint_as_float(ab);
+        const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+        uint32_t packed = 0;
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int q = (int) __builtin_rintf(__fmul_rn(v[i], id));
+            s += q;
+            packed |= ((uint32_t) (q & 0xFF)) << (8 * i);
+        }
+        s = mi_sum8(s);
+        *(uint32_t *) (qs + lane * 4) = packed;
+        if ((lane & 7) == 0) {
+            const int blk = sl * 8 + (lane >> 3);
+            a.d[c * (K / 32) + blk] = mi_h2f(mi_f2h(amax / 127.f));
+            a.s32[c * (K / 32) + blk] = (int16_t) s;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ weight formats
+
+template <bool Q5>
+struct FmtKQ {
+    static constexpr int QKA = 256;  // activation block
+    static constexpr int ITEM = 64;  // elements per item
+    static constexpr int BS = Q5 ? 176 : 144;
+    struct Regs {
+        uint4 hdr, qa, qb;
+        uint4 ha, hb;  // Q5 only
+    };
+    __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item) {
+        // row is wave-uniform and the lane offsets are 32-bit: scalar base + vector offset
+        // addressing, no per-lane 64-bit address arithmetic per row
+        const uint32_t s = (uint32_t) item >> 2, j = (uint32_t) item & 3;
+        const uint32_t blk = s * BS;
+        const uint32_t qp = blk + (Q5 ? 48 : 16) + 32 * j;
+        r.hdr = *(const uint4 *) (row + blk);
+        r.qa = *(const uint4 *) (row + qp);
+        r.qb = *(const uint4 *) (row + qp + 16);
+        if constexpr (Q5) {
+            r.ha = *(const uint4 *) (row + blk + 16);
+            r.hb = *(const uint4 *) (row + blk + 32);
+        }
+    }
+    template <int NC>
+    __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
+        const int s = item >> 2, j = item & 3;
+        const uint32_t q[8] = {r.qa.x, r.qa.y, r.qa.z, r.qa.w, r.qb.x, r.qb.y, r.qb.z, r.qb.w};
+        uint32_t qlo[8], qhi[8];
+        if constexpr (Q5) {
+            const uint32_t h[8] = {r.ha.x, r.ha.y, r.ha.z, r.ha.w, r.hb.x, r.hb.y, r.hb.z, r.hb.w};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = (q[i] & 0x0F0F0F0Fu) | (((h[i] >> (2 * j)) & 0x01010101u) << 4);
+                qhi[i] = ((q[i] >> 4) & 0x0F0F0F0Fu) | (((h[i] >> (2 * j + 1)) & 0x01010101u) << 4);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = q[i] & 0x0F0F0F0Fu;
+                qhi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
+            }
+        }
+        const float dw = mi_h2f((uint16_t) (r.hdr.x & 0xFFFF));
+        const float dmw = mi_h2f((uint16_t) (r.hdr.x >> 16));
+        // 6-bit scales / mins of sub-blocks 2j and 2j+1 (get_scale_min_k4,
+        // src/ggml-quants.c:1357-1365) without divergent branches: j is lane-dependent
+        const uint32_t sh = 16u * (uint32_t) (j & 1);
+        const uint32_t x0 = r.hdr.y >> sh, x1 = r.hdr.z >> sh, x2 = r.hdr.w >> sh;
+        int sc0, m0, sc1, m1;
+        if (j < 2) {  // sub-blocks 0..3: plain 6-bit fields (a select, both sides are cheap)
+            sc0 = (int) (x0 & 63);
+            sc1 = (int) ((x0 >> 8) & 63);
+            m0 = (int) (x1 & 63);
+            m1 = (int) ((x1 >> 8) & 63);
+        } else {      // sub-blocks 4..7: low 4 bits from bytes 8..11, high 2 bits from bytes 0..7
+            sc0 = (int) ((x2 & 0xF) | (((x0 >> 6) & 3) << 4));
+            sc1 = (int) (((x2 >> 8) & 0xF) | (((x0 >> 14) & 3) << 4));
+            m0 = (int) (((x2 >> 4) & 0xF) | (((x1 >> 6) & 3) << 4));
+            m1 = (int) (((x2 >> 12) & 0xF) | (((x1 >> 14) & 3) << 4));
+        }
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) s * 256 + 64 * j);
+            const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            const int alo[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const int ahi[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            int lo = 0, hi = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                lo = mi_dot4((int) qlo[i], alo[i], lo);
+                hi = mi_dot4((int) qhi[i], ahi[i], hi);
+            }
+            const int ss = *(const int *) (a.s32 + c * (K / 32) + s * 8 + 2 * j);
+            // sc*lo + sc*hi and m*bsum + m*bsum in f32 are exact (|.| < 2^24: 63*32*31*127 and
+            // 63*32*128 per term), i.e. (float) of the reference's int32 sums, without the
+            // quarter-rate 32-bit integer multiplies
+            const float sumi = fmaf((float) sc1, (float) hi, (float) sc0 * (float) lo);
+            const float summ = fmaf((float) m1, (float) (ss >> 16), (float) m0 * (float) (int) (int16_t) (ss & 0xFFFF));
+            acc[c] += a.d[c * (K / 256) + s] * (dw * sumi - dmw * summ);
+        }
+    }
+
+    // CPU order (see ord_* below): per item (superblock s, 64-group j) the reference's eight int32
+    // lanes l -- sc[2j] * (bytes 4l..4l+3 of the low nibbles . q8) + sc[2j+1] * (high nibbles) --
+    // summed over the superblock's four items (a DPP quad: items 4s..4s+3 sit on adjacent lanes),
+    // plus the mins lane m[2j] * bsum32[2j] + m[2j+1] * bsum32[2j+1]. Entry of superblock sb in the
+    // scratch: [0..7] the eight int32 sums, [8..11] the four mins lanes (Q5_K: [8] their sum),
+    // [12] d = y.d * x.d, [13] dmin = -(y.d * x.dmin).
+    template <int NC>
+    __device__ static __forceinline__ void dot_ord(const Regs & r, int item, int slot, const lds_act & a, int64_t K, int ncols,
+                                                   uint32_t * scr, int cs, int) {
+        const int s = item >> 2, j = item & 3;
+        const uint32_t q[8] = {r.qa.x, r.qa.y, r.qa.z, r.qa.w, r.qb.x, r.qb.y, r.qb.z, r.qb.w};
+        uint32_t qlo[8], qhi[8];
+        if constexpr (Q5) {
+            const uint32_t h[8] = {r.ha.x, r.ha.y, r.ha.z, r.ha.w, r.hb.x, r.hb.y, r.hb.z, r.hb.w};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = (q[i] & 0x0F0F0F0Fu) | (((h[i] >> (2 * j)) & 0x01010101u) << 4);
+                qhi[i] = ((q[i] >> 4) & 0x0F0F0F0Fu) | (((h[i] >> (2 * j + 1)) & 0x01010101u) << 4);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                qlo[i] = q[i] & 0x0F0F0F0Fu;
+                qhi[i] = (q[i] >> 4) & 0x0F0F0F0Fu;
+            }
+        }
+        const float dw = mi_h2f((uint16_t) (r.hdr.x & 0xFFFF));
+        const float dmw = mi_h2f((uint16_t) (r.hdr.x >> 16));
+        const uint32_t sh = 16u * (uint32_t) (j & 1);
+        const uint32_t x0 = r.hdr.y >> sh, x1 = r.hdr.z >> sh, x2 = r.hdr.w >> sh;
+        int sc0, m0, sc1, m1;
+        if (j < 2) {
+            sc0 = (int) (x0 & 63);
+            sc1 = (int) ((x0 >> 8) & 63);
+            m0 = (int) (x1 & 63);
+            m1 = (int) ((x1 >> 8) & 63);
+        } else {
+            sc0 = (int) ((x2 & 0xF) | (((x0 >> 6) & 3) << 4));
+            sc1 = (int) (((x2 >> 8) & 0xF) | (((x0 >> 14) & 3) << 4));
+            m0 = (int) (((x2 >> 4) & 0xF) | (((x1 >> 6) & 3) << 4));
+            m1 = (int) (((x2 >> 12) & 0xF) | (((x1 >> 14) & 3) << 4));
+        }
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) s * 256 + 64 * j);
+            const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            const int alo[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const int ahi[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            int v[8];
+#pragma unroll
+            for (int l = 0; l < 8; l++) {
+                // |products| < 2^23: the 24-bit multiplier is exact
+                v[l] = __mul24(sc0, mi_dot4((int) qlo[l], alo[l], 0)) + __mul24(sc1, mi_dot4((int) qhi[l], ahi[l], 0));
+                v[l] += mi_dpp<MI_DPP_QP_1032>(0, v[l]);
+                v[l] += mi_dpp<MI_DPP_QP_2301>(0, v[l]);
+            }
+            const int ss = *(const int *) (a.s32 + c * (K / 32) + s * 8 + 2 * j);
+            int pm = __mul24(m0, (int) (int16_t) (ss & 0xFFFF)) + __mul24(m1, ss >> 16);
+            if constexpr (Q5) {
+                pm += mi_dpp<MI_DPP_QP_1032>(0, pm);
+                pm += mi_dpp<MI_DPP_QP_2301>(0, pm);
+            }
+            uint32_t * e = scr + c * cs + (slot >> 2) * 16;
+            // lane j stores sums 2j and 2j+1 (all four lanes hold all eight after the quad sums),
+            // as floats (exact: |sum| < 2^24), i.e. the reference's _mm256_cvtepi32_ps
+            const int w0 = j == 0 ? v[0] : j == 1 ? v[2] : j == 2 ? v[4] : v[6];
+            const int w1 = j == 0 ? v[1] : j == 1 ? v[3] : j == 2 ? v[5] : v[7];
+            *(uint2 *) (e + 2 * j) = make_uint2(__float_as_uint((float) w0), __float_as_uint((float) w1));
+            if (!Q5 || j == 0) e[8 + j] = __float_as_uint((float) pm);
+            const float yd = a.d[c * (K / 256) + s];
+            if (j == 2) e[12] = __float_as_uint(yd * dw);
+            if (j == 3) e[13] = __float_as_uint(-(yd * dmw));
+        }
+    }
+    // one chain step per superblock: acc[l] = fma(d, (float) sumi[l], acc[l]) (the reference's
+    // _mm256_fmadd_ps) and the mins accumulator: Q4_K four lanes acc_m[k] = fma(dmin, prod[k],
+    // acc_m[k]) (_mm_fmadd_ps), Q5_K one scalar summs += dmin * hsum(prod) (contracted by the
+    // reference's -mfma build)
+    __device__ static __forceinline__ void chain(const uint32_t * scr, int l, int n_items, int, float & A, float & M) {
+        const float * e = (const float *) scr;
+        const int nsb = n_items >> 2;
+        const int lm = 8 + (Q5 ? 0 : (l & 3));
+        for (int sb = 0; sb < nsb; sb++, e += 16) {
+            A = fmaf(e[12], e[l], A);
+            M = fmaf(e[13], e[lm], M);
+        }
+    }
+    // scratch words per (row, column): one 16-word entry per superblock (+8: bank spread)
+    static int ord_words(int nitems, int & stride) {
+        stride = 0;
+        return 16 * (nitems / 4) + 8;
+    }
+    __device__ static __forceinline__ float finish(float A, float M) {
+        float z = A + __shfl_xor(A, 4, 8);
+        z = z + __shfl_xor(z, 2, 8);
+        z = z + __shfl_xor(z, 1, 8);
+        if constexpr (Q5) return z + M;
+        float m = M + __shfl_xor(M, 2, 8);
+        m = m + __shfl_xor(m, 1, 8);
+        return z + m;
+    }
+};
+
+// Q4_0 (18 B) / Q8_0 (34 B) blocks: 2-byte aligned. Load the dwords covering the quants
+// (aligned down) and re-align with v_alignbyte; d is a separate 2-byte load.
+template <bool Q8>
+struct FmtQ0 {
+    static constexpr int QKA = 32;
+    static constexpr int ITEM = 32;
+    static constexpr int BS = Q8 ? 34 : 18;
+    static constexpr int NQ = Q8 ? 8 : 4;  // quant dwords per block
+    struct Regs {
+        uint32_t w[NQ + 1];  // the dwords covering d and the quants
+        uint32_t off;        // byte offset of the block in w[0]: 0 or 2
+    };
+    __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item) {
+        // rows start 16-byte aligned (fused_mv_eligible), so the block's misalignment is a
+        // function of the item alone; dword loads only (a 16-bit load of d gets a zero-extend
+        // the compiler places right behind the load, which waits for it), on 32-bit lane offsets
+        // from the wave-uniform row pointer
+        const uint32_t blk = (uint32_t) item * BS;
+        r.off = blk & 2;
+        const uint32_t base = blk - r.off;
+#pragma unroll
+        for (int i = 0; i <= NQ; i++) r.w[i] = *(const uint32_t *) (row + base + 4 * i);  // 256 B tail slack
+    }
+    template <int NC>
+    __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
+        // d = bytes off..off+1 of w[0]; the quants start at byte off + 2
+        uint32_t t[NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; i++) t[i] = r.off ? r.w[i + 1] : __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], 2);
+        const uint32_t dbits = (r.off ? r.w[0] >> 16 : r.w[0]) & 0xFFFF;
+        const float dw = mi_h2f((uint16_t) dbits);
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 32);
+            const int4 a0 = p[0], a1 = p[1];
+            const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            int sumi = 0;
+            if constexpr (Q8) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) sumi = mi_dot4((int) t[i], av[i], sumi);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    sumi = mi_dot4((int) (t[i] & 0x0F0F0F0Fu), av[i], sumi);
+                    sumi = mi_dot4((int) ((t[i] >> 4) & 0x0F0F0F0Fu), av[i + 4], sumi);
+                }
+                sumi -= 8 * (int) a.s32[c * (K / 32) + item];  // (q - 8) * y
+            }
+            acc[c] += (float) sumi * (dw * a.d[c * (K / 32) + item]);
+        }
+    }
+
+    // CPU order: the reference's eight int32 lanes l of mul_sum_i8_pairs_float -- elements 4l..4l+3
+    // (Q4_0: low nibbles for l < 4, high nibbles of bytes 4(l-4).. for l >= 4, minus 8) -- and
+    // d = x.d * y.d, stored transposed: scratch [l][slot] (row stride 68 words), d at [8][slot].
+    template <int NC>
+    __device__ static __forceinline__ void dot_ord(const Regs & r, int item, int slot, const lds_act & a, int64_t K, int ncols,
+                                                   uint32_t * scr, int cs, int S) {
+        uint32_t t[NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; i++) t[i] = r.off ? r.w[i + 1] : __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], 2);
+        const uint32_t dbits = (r.off ? r.w[0] >> 16 : r.w[0]) & 0xFFFF;
+        const float dw = mi_h2f((uint16_t) dbits);
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 32);
+            const int4 a0 = p[0], a1 = p[1];
+            const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            uint32_t * e = scr + c * cs + slot;
+#pragma unroll
+            for (int l = 0; l < 8; l++) {
+                int q;
+                if constexpr (Q8) {
+                    q = mi_dot4((int) t[l], av[l], 0);
+                } else {
+                    const uint32_t nib = l < 4 ? (t[l] & 0x0F0F0F0Fu) : ((t[l - 4] >> 4) & 0x0F0F0F0Fu);
+                    q = mi_dot4((int) nib, av[l], mi_dot4((int) 0xF8F8F8F8u, av[l], 0));  // (q - 8) . y
+                }
+                e[l * S] = __float_as_uint((float) q);  // exact; _mm256_cvtepi32_ps
+            }
+            e[8 * S] = __float_as_uint(dw * a.d[c * (K / 32) + item]);
+        }
+    }
+    // acc[l] = fma(d_i, (float) q[i][l], acc[l]) over the blocks in order (_mm256_fmadd_ps)
+    __device__ static __forceinline__ void chain(const uint32_t * scr, int l, int n_items, int S, float & A, float & M) {
+        (void) M;
+        const float * q = (const float *) scr + l * S;
+        const float * d = (const float *) scr + 8 * S;
+        int i = 0;
+        for (; i + 4 <= n_items; i += 4) {
+            const float4 qq = *(const float4 *) (q + i);
+            const float4 dd = *(const float4 *) (d + i);
+            A = fmaf(dd.x, qq.x, A);
+            A = fmaf(dd.y, qq.y, A);
+            A = fmaf(dd.z, qq.z, A);
+            A = fmaf(dd.w, qq.w, A);
+        }
+        for (; i < n_items; i++) A = fmaf(d[i], q[i], A);
+    }
+    // scratch words per (row, column): 9 rows (8 lanes + d) of S >= nitems words; S = 4 (mod 32)
+    // keeps the eight lanes' 16-byte chain reads on distinct banks
+    static int ord_words(int nitems, int & stride) {
+        int S = (nitems + 3) & ~3;
+        while (S % 32 != 4) S += 4;
+        stride = S;
+        return 9 * S;
+    }
+    __device__ static __forceinline__ float finish(float A, float) {
+        // hsum_float_8: ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7))
+        float z = A + __shfl_xor(A, 4, 8);
+        z = z + __shfl_xor(z, 2, 8);
+        return z + __shfl_xor(z, 1, 8);
+    }
+};
+
+// Q4_0 in pairs of blocks (tree order only): an item is 2 blocks = 36 B, 4-byte aligned, so 9
+// dword loads cover it with no slack, the second block's quants are whole dwords (only the
+// first's need v_alignbyte), and a K = 4096 row is one item per lane.
+struct FmtQ0Pair {
+    static constexpr int QKA = 32;
+    static constexpr int ITEM = 64;
+    struct Regs {
+        uint32_t w[9];
+    };
+    __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item) {
+        const uint8_t * p = row + (uint32_t) item * 36;
+#pragma unroll
+        for (int i = 0; i < 9; i++) r.w[i] = *(const uint32_t *) (p + 4 * i);
+    }
+    template <int NC>
+    __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
+        // block 0: d = bytes 0..1, quants bytes 2..17; block 1: d = bytes 18..19, quants 20..35
+        uint32_t t0[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) t0[i] = __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], 2);
+        const float dw0 = mi_h2f((uint16_t) (r.w[0] & 0xFFFF));
+        const float dw1 = mi_h2f((uint16_t) (r.w[4] >> 16));
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 64);
+            const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            const int av0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const int av1[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            int s0 = 0, s1 = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                s0 = mi_dot4((int) (t0[i] & 0x0F0F0F0Fu), av0[i], s0);
+                s0 = mi_dot4((int) ((t0[i] >> 4) & 0x0F0F0F0Fu), av0[i + 4], s0);
+                s1 = mi_dot4((int) (r.w[i + 5] & 0x0F0F0F0Fu), av1[i], s1);
+                s1 = mi_dot4((int) ((r.w[i + 5] >> 4) & 0x0F0F0F0Fu), av1[i + 4], s1);
+            }
+            const uint32_t ss = *(const uint32_t *) (a.s32 + c * (K / 32) + 2 * item);  // both blocks' sums
+            s0 -= 8 * (int) (int16_t) (ss & 0xFFFF);
+            s1 -= 8 * (int) (int16_t) (ss >> 16);
+            const float2 da = *(const float2 *) (a.d + c * (K / 32) + 2 * item);
+            acc[c] += (float) s0 * (dw0 * da.x);
+            acc[c] += (float) s1 * (dw1 * da.y);
+        }
+    }
+};
+
+
+// ------------------------------------------------------------------ the streaming kernel
+
+// IPL = items per lane held in the prefetch ring (further items of long rows are loaded
+// in-line); PD = rows in flight ahead of the row being computed.
+// norm|rms_norm -> mul(g) -> add(b) of the group's activation columns into LDS (f32), by wave 0
+// with each column in registers -- the arithmetic of k_norm (ops.hip) and of the F16 GEMV's
+// prologue: certified double means, then every step rounded separately. norm_cols: a column's x,
+// g, b in registers (every load unconditional at a clamped index, then a select: a load under a
+// lane branch makes the compiler wait for it at the branch's join; absent g / b read x instead).
+struct norm_cols {
+    static constexpr int kJ = (int) (kMiMmvProMaxK / 64);
+    float v[kJ], gv[kJ], bv[kJ];
+};
+
+__device__ __forceinline__ void norm_cols_load(const mi_mmv_group & g, const char * X, int c, norm_cols & r) {
+    const int lane = threadIdx.x & 63;
+    const int64_t K = g.K;
+    const float * xc = (const float *) (X + c * g.xcol);
+    const float * gp = g.pro.g ? g.pro.g : xc;
+    const float * bp = g.pro.b ? g.pro.b : xc;
+#pragma unroll
+    for (int j = 0; j < norm_cols::kJ; j++) {
+        const int64_t k = (int64_t) j * 64 + lane;
+        const bool in = k < K;
+        const int64_t kc = in ? k : K - 1;
+        const float xv = xc[kc], gl = gp[kc], bl = bp[kc];
+        r.v[j] = in ? xv : 0.0f;
+        r.gv[j] = in && g.pro.g ? gl : 1.0f;
+        r.bv[j] = in && g.pro.b ? bl : 0.0f;
+    }
+}
+
+// r: column 0, already loaded (before the weight stream, so that vmcnt does not make it wait for
+// the weights); the other columns are loaded here
+__device__ void norm_prologue(const mi_mmv_group & g, const char * X, int ncols, float * xn, norm_cols & r) {
+    constexpr int kJ = norm_cols::kJ;
+    const int lane = threadIdx.x & 63;
+    const int64_t K = g.K;
+    for (int c = 0; c < ncols; c++) {
+        if (c > 0) norm_cols_load(g, X, c, r);
+        float scale;
+        if (g.pro.mode == 2) {
+            const float mean = wave_mean_cpu_order<true, kJ>(r.v, K);
+            scale = 1.0f / sqrtf(add_rn(mean, g.pro.eps));
+        } else {
+            const float mean = wave_mean_cpu_order<false, kJ>(r.v, K);
+#pragma unroll
+            for (int j = 0; j < kJ; j++) r.v[j] = sub_rn(r.v[j], mean);
+            const float variance = wave_mean_cpu_order<true, kJ>(r.v, K);
+            scale = 1.0f / sqrtf(add_rn(variance, g.pro.eps));
+        }
+#pragma unroll
+        for (int j = 0; j < kJ; j++) {
+            const int64_t k = (int64_t) j * 64 + lane;
+            if (k < K) {
+                float y = mul_rn(r.v[j], scale);
+                if (g.pro.g) y = mul_rn(y, r.gv[j]);
+                if (g.pro.b) y = add_rn(y, r.bv[j]);
+                xn[c * K + k] = y;
+            }
+        }
+    }
+}
+
+// one output element, through the graph's epilogue: + bias[row], then + resid or GELU (the fp16
+// table lookup of ggml_vec_gelu_f32 with its +-10 clamps), then the K/V-cache row copies -- each
+// step rounded as its own node would round it
+template <bool X>
+__device__ __forceinline__ void store_out(const mi_mmv_group & g, float * dst, int c, int row, float v) {
+    if constexpr (!X) {
+        *(float *) ((char *) dst + c * g.ycol + (size_t) row * sizeof(float)) = v;
+        return;
+    }
+    const mi_mmv_group::epilogue & e = g.epi;
+    if (e.bias) v = v + e.bias[row];
+    if (e.resid) v = v + *(const float *) (e.resid + c * e.resid_nb1 + (size_t) row * sizeof(float));
+    else if (e.gelu_table) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
+    *(float *) ((char *) dst + c * g.ycol + (size_t) row * sizeof(float)) = v;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (e.copy[k].ptr && row >= e.copy[k].row0 && row < e.copy[k].row1) {
+            *(float *) (e.copy[k].ptr + c * e.copy[k].col_stride + (size_t) (row - e.copy[k].row0) * sizeof(float)) = v;
+        }
+    }
+}
+
+// ORD: combine in the reference CPU's order (bit-identical results, see dot_ord / chain): each
+// 64-item chunk of a row leaves its per-item lane sums in the wave's LDS scratch, then lane
+// (column c, CPU lane l) runs the reference's sequential fma chain over the chunk.
+// PRO: the graph's norm prologue (g.pro) and store epilogue (g.epi) are compiled in
+// XF (lone members): the activation side first -- its loads issued and waited for before any weight
+// load, so they do not queue behind every workgroup's weight stream (phase stamps: with the weights
+// requested first, a lone Q4_K 4096^2 member's activations took 3.6 us to land and quantize,
+// profiles/r05b_lone_gemv_stamps.txt); the weights are then requested while the activations are
+// quantized (PRO: after the prologue's quantization)
+template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO, bool XF>
+__global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    MI_STAMP(g.stamps, 0);
+    constexpr int NB = PD + 1;  // ring slots
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int member = blockIdx.x / g.blocks_per_member;
+    const int rb = blockIdx.x - member * g.blocks_per_member;
+    const uint8_t * W = (const uint8_t *) g.m[member].W;
+    const char * X = g.m[member].X;
+    float * dst = g.m[member].dst;
+    const int64_t K = g.K;
+    const int nitems = (int) (K / F::ITEM);
+    const int ncols = g.ncols;
+    const lds_act act = lds_carve<F::QKA>(lds, NC, K);
+    uint32_t * scr = (uint32_t *) (lds + ord_offset(lds_bytes<F::QKA>(NC, K))) + wave * (g.ord_rows ? g.ord_rows : 1) * NC * g.ord_cs;
+
+    // 32-bit row bookkeeping (N < 2^31): scalar compares, no 64-bit VGPR temporaries in the loop
+    const int Nr = (int) g.N;
+    const int row_begin = rb * (int) g.rows_per_block;
+    const int row_end = row_begin + (int) g.rows_per_block < Nr ? row_begin + (int) g.rows_per_block : Nr;
+    const int nrows = row_end - row_begin > wave ? (row_end - row_begin - wave + 3) / 4 : 0;
+    auto wrow_of = [&](int k) {
+        const int r = row_begin + 4 * k + wave;
+        return W + (size_t) (r < Nr ? r : Nr - 1) * g.nb01;
+    };
+
+    // Every load of the ring is unconditional, with clamped row / item indices: a load under a
+    // branch makes the compiler merge the ring registers after it, and the merge copy waits for
+    // the load just issued (vmcnt(0)), which serialises the prefetch.
+    typename F::Regs ring[NB][IPL];
+    auto prefetch = [&](typename F::Regs (&slot)[IPL], int k) {
+        const uint8_t * wr = wrow_of(k);
+#pragma unroll
+        for (int i = 0; i < IPL; i++) {
+            const int item = lane + 64 * i;
+            F::load(slot[i], wr, item < nitems ? item : nitems - 1);
+        }
+    };
+    const int klast = nrows > 0 ? nrows - 1 : 0;
+
+    // 0) what the prologue reads first, requested before the weights (vmcnt retires in order: a
+    //    use of it would otherwise wait for the weight loads too): the norm prologue's first
+    //    column, g and b (wave 0), or the activation slices of the first quantization round
+    norm_cols nc0;
+    const int nsl = (int) (K / 256);
+    const int total = nsl * ncols;
+    float4 xfirst[4];
+    auto load_round = [&](float4 (&v)[4], const char * Xs, size_t xcs, int p0) {
+        // unconditional (clamped) loads: a predicated load makes hipcc wait vmcnt(0) per load
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = min(p0 + 4 * u, total - 1);
+            const int c = p / nsl, sl = p - c * nsl;
+            v[u] = *(const float4 *) (Xs + c * xcs + ((size_t) sl * 256 + lane * 4) * sizeof(float));
+        }
+    };
+    if constexpr (PRO) {
+        if (g.pro.mode && wave == 0) norm_cols_load(g, X, 0, nc0);
+    } else {
+        load_round(xfirst, X, g.xcol, wave);
+    }
+    if constexpr (XF && !PRO) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // 1) the first PD rows' weights in flight
+    if constexpr (!(XF && PRO)) {
+#pragma unroll
+        for (int u = 0; u < PD; u++) prefetch(ring[u], u < klast ? u : klast);
+    }
+
+    // 2) quantize the member's activation columns into LDS (wave w: 256-slices w, w+4, ...),
+    //    from the normalized columns when the graph's norm chain is fused in
+    const char * Xq = X;
+    size_t xcolq = g.xcol;
+    if (PRO && g.pro.mode) {
+        float * xn = (float *) (lds + g.pro_off);
+        if (wave == 0) norm_prologue(g, X, ncols, xn, nc0);
+        __syncthreads();
+        Xq = (const char *) xn;
+        xcolq = (size_t) K * sizeof(float);
+    }
+    {
+        for (int p0 = wave; p0 < total; p0 += 16) {
+            float4 v[4];
+            if (!PRO && p0 == wave) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = xfirst[u];
+            } else {
+                load_round(v, Xq, xcolq, p0);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = p0 + 4 * u;
+                if (p < total) {
+                    const int c = p / nsl, sl = p - c * nsl;
+                    quantize_slice<F::QKA>(v[u], lane, act, K, c, sl);
+                }
+            }
+        }
+    }
+    MI_STAMP(g.stamps, 1);  // wave 0's activation slices loaded and quantized
+    if constexpr (XF && PRO) {
+#pragma unroll
+        for (int u = 0; u < PD; u++) prefetch(ring[u], u < klast ? u : klast);
+    }
+    __syncthreads();
+    MI_STAMP(g.stamps, 2);  // every wave's
+
+    // 3) stream: ring slot u holds row k0+u; refill it with row k0+u+PD right before using it
+    //    (the last row again past the end: an L2 hit)
+    for (int k0 = 0; k0 < nrows; k0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; u++) {
+            const int k = k0 + u;
+            if (k >= nrows) break;  // wave-uniform
+            prefetch(ring[(u + PD) % NB], k + PD < klast ? k + PD : klast);
+            const int row = row_begin + 4 * k + wave;
+            if constexpr (ORD) {
+                const int R = g.ord_rows, cs = g.ord_cs, S = g.ord_s;
+                auto sync = [] {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_wave_barrier();
+                };
+                if (R == 0) {
+                    // rows too long for the scratch: one chain pass per 64-item chunk of the row
+                    const int cl = lane >> 3, ll = lane & 7;
+                    float A = 0.0f, M = 0.0f;
+                    auto chunk_done = [&](int base) {
+                        sync();
+                        if (cl < ncols && !g.abl) F::chain(scr + cl * cs, ll, min(64, nitems - base), S, A, M);
+                        sync();
+                    };
+#pragma unroll
+                    for (int i = 0; i < IPL; i++) {
+                        if (64 * i >= nitems) break;  // wave-uniform
+                        const int item = lane + 64 * i;
+                        if (item < nitems) F::template dot_ord<NC>(ring[u][i], item, lane, act, K, ncols, scr, cs, S);
+                        chunk_done(64 * i);
+                    }
+                    if constexpr (TAIL) {
+                        const uint8_t * wr = wrow_of(k);
+                        for (int base = 64 * IPL; base < nitems; base += 64) {
+                            const int item = base + lane;
+                            if (item < nitems) {
+                                typename F::Regs rr;
+                                F::load(rr, wr, item);
+                                F::template dot_ord<NC>(rr, item, lane, act, K, ncols, scr, cs, S);
+                            }
+                            chunk_done(base);
+                        }
+                    }
+                    const float v = F::finish(A, M);
+                    if (ll == 0 && cl < ncols) store_out<PRO>(g, dst, cl, row, v);
+                    continue;
+                }
+                // whole rows in the scratch: R rows' lane sums are collected, then one chain pass
+                // runs them all, lane = (row r, column c, CPU lane l), 8 * NC * R <= 64
+                const int slot = k % R;
+                uint32_t * srow = scr + slot * NC * cs;
+#pragma unroll
+                for (int i = 0; i < IPL; i++) {
+                    const int item = lane + 64 * i;
+                    if (item < nitems) F::template dot_ord<NC>(ring[u][i], item, item, act, K, ncols, srow, cs, S);
+                }
+                if constexpr (TAIL) {
+                    const uint8_t * wr = wrow_of(k);
+                    for (int item = lane + 64 * IPL; item < nitems; item += 64) {
+                        typename F::Regs rr;
+                        F::load(rr, wr, item);
+                        F::template dot_ord<NC>(rr, item, item, act, K, ncols, srow, cs, S);
+                    }
+                }
+                if (slot == R - 1 || k == nrows - 1) {  // wave-uniform
+                    sync();
+                    const int r = lane / (8 * NC), cl = (lane >> 3) % NC, ll = lane & 7;
+                    const bool mine = r <= slot && cl < ncols;
+                    float A = 0.0f, M = 0.0f;
+                    if (mine && !g.abl) F::chain(scr + (r * NC + cl) * cs, ll, nitems, S, A, M);
+                    const float v = F::finish(A, M);
+                    if (ll == 0 && mine) {
+                        store_out<PRO>(g, dst, cl, row_begin + 4 * (k - slot + r) + wave, v);
+                    }
+                    sync();
+                }
+                continue;
+            }
+            float acc[NC];
+#pragma unroll
+            for (int c = 0; c < NC; c++) acc[c] = 0.0f;
+#pragma unroll
+            for (int i = 0; i < IPL; i++) {
+                const int item = lane + 64 * i;
+                if (item < nitems) F::template dot<NC>(ring[u][i], item, act, K, ncols, acc);
+            }
+            if constexpr (TAIL) {
+                // items beyond the ring's IPL per lane, loaded in-line (long rows only: a loop
+                // with loads here makes the compiler drain vmcnt at the top of every row group)
+                const uint8_t * wr = wrow_of(k);
+                for (int item = lane + 64 * IPL; item < nitems; item += 64) {
+                    typename F::Regs rr;
+                    F::load(rr, wr, item);
+                    F::template dot<NC>(rr, item, act, K, ncols, acc);
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const float v = mi_wave_sum_u(acc[c]);
+                if (lane == 0 && c < ncols) store_out<PRO>(g, dst, c, row, v);
+            }
+            if (k == 0) MI_STAMP(g.stamps, 3);  // first row reduced and stored
+        }
+    }
+    MI_STAMP(g.stamps, 7);
+}
+
+// Workgroups that fit on the chip at once for this kernel instance (all of them are launched
+// in one wave, so no workgroup waits for another to retire). Speed only: nothing relies on
+// co-residency. Cached per kernel.
+int resident_blocks(const void * fn, size_t lds) {
+    struct entry { const void * fn; size_t lds; int n; };
+    static entry cache[64];
+    static int ncache = 0;
+    for (int i = 0; i < ncache; i++) if (cache[i].fn == fn && cache[i].lds == lds) return cache[i].n;
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    (void) hipGetDevice(&dev);
+    (void) hipGetDeviceProperties(&prop, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    const int n = per_cu * prop.multiProcessorCount;
+    if (ncache < 64) cache[ncache++] = entry{fn, lds, n};
+    return n;
+}
+
+static int mi_cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        (void) hipGetDevice(&dev);
+        n = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    }
+    return n;
+}
+
+template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO = false, bool XF = false>
+void launch_one(mi_mmv_group g, hipStream_t s) {
+    const size_t act = lds_bytes<F::QKA>(NC, g.K);
+    size_t lds = act;
+    if constexpr (ORD) {
+        // whole rows in the scratch when R >= 1 rows per wave fit a 36 KB budget (the kernel is
+        // VGPR-limited to ~4 workgroups per CU anyway), else one chunk of 64 items per wave
+        const int nitems = (int) (g.K / F::ITEM);
+        int S = 0;
+        const int cs = F::ord_words(nitems, S);
+        int R = (int) ((36 * 1024) / ((size_t) 4 * NC * cs * 4));
+        if (R > 8 / NC) R = 8 / NC;
+        if (R >= 1) {
+            g.ord_rows = R;
+            g.ord_cs = cs;
+            g.ord_s = S;
+        } else {
+            g.ord_rows = 0;
+            g.ord_cs = F::ord_words(64, S);
+            g.ord_s = S;
+        }
+        lds = ord_offset(act) + (size_t) 4 * (g.ord_rows ? g.ord_rows : 1) * NC * g.ord_cs * 4;
+    }
+    if (PRO && g.pro.mode) {
+        g.pro_off = (int) ord_offset(lds);
+        lds = (size_t) g.pro_off + (size_t) NC * g.K * sizeof(float);
+    }
+    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL, TAIL, ORD, PRO, XF>;
+    if (lds > 64 * 1024) {
+        static bool attr_set = false;  // per instance
+        if (!attr_set) {
+            (void) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_set = true;
+        }
+    }
+    // automatic grid: the resident workgroup count, split over the members. A lone member at
+    // K >= 4096 gets one workgroup per CU instead: every workgroup quantizes the whole activation
+    // in its prologue, so at 4 rows per workgroup that redundant work dominates (Q4_K 4096^2 alone
+    // in its graph 7.96 -> 6.57 us, profiles/r04e_pf_single_blocks.txt)
+    int target = g_mi_tuning.mmv_blocks > 0 ? g_mi_tuning.mmv_blocks : resident_blocks(fn, lds);
+    if (g_mi_tuning.mmv_blocks <= 0 && g.n == 1 && g.K >= 4096) target = std::min(target, mi_cu_count());
+    // Q5_K grouped launches: twice the resident count (smaller workgroups, a later tail; 4096 x 11008
+    // 5.56 -> 5.75 TB/s, r04r_gemv_sweep.txt)
+    else if (g_mi_tuning.mmv_blocks <= 0 && std::is_same<F, FmtKQ<true>>::value && !ORD && !PRO) target *= 2;
+    int bpm = target / g.n;
+    if (bpm < 1) bpm = 1;
+    int64_t rows = (g.N + bpm - 1) / bpm;
+    rows = (rows + 3) / 4 * 4;
+    g.rows_per_block = rows;
+    g.blocks_per_member = (int) ((g.N + rows - 1) / rows);
+    g.stamps = mi_stamp_take(ORD ? "k_mmv_stream_ord" : "k_mmv_stream", (unsigned) (g.blocks_per_member * g.n));
+    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL, TAIL, ORD, PRO, XF>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds,
+                       s, g);
+}
+
+template <class F, int NC, int PD, int IPL, bool ORD, bool XF = false>
+void launch_tail(const mi_mmv_group & g, hipStream_t s) {
+    if (g.K / F::ITEM > 64 * IPL) launch_one<F, NC, PD, IPL, true, ORD, false, XF>(g, s);
+    else launch_one<F, NC, PD, IPL, false, ORD, false, XF>(g, s);
+}
+
+template <class F, int NC, bool ORD>
+void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
+    const int items = (int) (g.K / F::ITEM);
+    const mi_mmv_group::epilogue & e = g.epi;
+    // lone members (a dependent layer's GEMV): activations first (XF), every row of a wave in flight
+    const bool xf = g.n == 1 && g_mi_tuning.xfirst;
+    if (g.pro.mode || e.bias || e.resid || e.gelu_table || e.copy[0].ptr || e.copy[1].ptr) {
+        // the graph's norm prologue and/or epilogue: instances of their own (prefetch depth 1) so
+        // that their registers and per-row branches do not weigh on the plain kernels
+        if (xf) {
+            if (items > 128) launch_one<F, NC, 2, 2, true, ORD, true, true>(g, s);
+            else if (items > 64) launch_one<F, NC, 2, 2, false, ORD, true, true>(g, s);
+            else launch_one<F, NC, 4, 1, false, ORD, true, true>(g, s);
+            return;
+        }
+        if (items > 128) launch_one<F, NC, 1, 2, true, ORD, true>(g, s);
+        else if (items > 64) launch_one<F, NC, 1, 2, false, ORD, true>(g, s);
+        else launch_one<F, NC, 1, 1, false, ORD, true>(g, s);
+        return;
+    }
+    if (items > 64) {
+        // two items per lane in the ring (Q4_0 / Q8_0 at K=4096)
+        if (xf) launch_tail<F, NC, 2, 2, ORD, true>(g, s);
+        else if (variant / 10 == 1) launch_tail<F, NC, 1, 2, ORD>(g, s);
+        else launch_tail<F, NC, 2, 2, ORD>(g, s);
+        return;
+    }
+    if (xf) {
+        launch_one<F, NC, 4, 1, false, ORD, false, true>(g, s);
+        return;
+    }
+    switch (variant / 10) {
+        case 1: launch_one<F, NC, 1, 1, false, ORD>(g, s); break;
+        case 3: launch_one<F, NC, 3, 1, false, ORD>(g, s); break;
+        default: launch_one<F, NC, 2, 1, false, ORD>(g, s); break;
+    }
+}
+
+template <class F, bool ORD>
+void launch_stream_nc(const mi_mmv_group & g, int variant, hipStream_t s) {
+    switch (g.ncols) {
+        case 1: launch_stream<F, 1, ORD>(g, variant, s); break;
+        case 2: launch_stream<F, 2, ORD>(g, variant, s); break;
+        case 3: case 4: launch_stream<F, 4, ORD>(g, variant, s); break;
+        default: launch_stream<F, 8, ORD>(g, variant, s); break;
+    }
+}
+
+template <class F>
+void launch_stream_ord(const mi_mmv_group & g, int variant, hipStream_t s) {
+    if (mi_mmv_order()) {
+        mi_mmv_group h = g;
+        h.abl = mi_mmv_order() == 2;
+        launch_stream_nc<F, true>(h, variant, s);
+    } else
+        launch_stream_nc<F, false>(g, variant, s);
+}
+
+
+} // namespace

@@ -237,3 +237,41 @@ def test_grouped_prefill_equals_single(rt, backend, tname, B):
     finally:
         rt.ggml_backend_buffer_free(buf)
         ctx.free()
+
+
+@pytest.mark.parametrize("tname", ["q5_K", "q4_K"])
+def test_long_prefill_into_host_memory(rt, backend, tname):
+    """A long prompt (> 128 columns, where k_mmqw / k_mmqx keep a partial sum in their own output
+    locations until the end) whose output lives in pinned host memory (the host buffer type, e.g.
+    host-staged logits): the backend picks a kernel that stores each output once; the result is
+    bit-identical to the same mul_mat into device memory."""
+    t = orc.TYPES_BY_NAME[tname]
+    K, N, B = 2048, 320, 160
+    wq = orc.quantize(t, synth.uniform(71, K * N), K)
+    x = synth.uniform(72, K * B)
+    dev_y = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
+    ovh = rt.ggml_tensor_overhead() * 8 + rt.ggml_graph_overhead()
+    cd, ch = G.Context(rt, ovh, no_alloc=True), G.Context(rt, ovh, no_alloc=True)
+    try:
+        w = rt.ggml_new_tensor_2d(cd.ctx, t, K, N)
+        xt = rt.ggml_new_tensor_2d(cd.ctx, G.GGML_TYPE_F32, K, B)
+        y = rt.ggml_mul_mat(ch.ctx, w, xt)  # the result tensor belongs to the host-buffer context
+        g = rt.ggml_new_graph(ch.ctx)
+        rt.ggml_build_forward_expand(g, y)
+        bd = rt.ggml_backend_alloc_ctx_tensors(cd.ctx, backend)
+        bh = rt.ggml_backend_alloc_ctx_tensors_from_buft(ch.ctx, rt.ggml_backend_mi355x_host_buffer_type())
+        assert bd and bh
+        try:
+            assert rt.ggml_backend_buffer_is_host(bh)
+            G.tensor_set(rt, w, wq)
+            G.tensor_set(rt, xt, x)
+            assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
+            host_y = G.tensor_get(rt, y)
+        finally:
+            rt.ggml_backend_buffer_free(bh)
+            rt.ggml_backend_buffer_free(bd)
+    finally:
+        ch.free()
+        cd.free()
+    assert np.array_equal(host_y.view(np.uint32), dev_y.view(np.uint32)), rel_err(host_y, dev_y)
+    assert rel_err(dev_y, orc.mul_mat(t, wq, K, N, x, B)) <= EXACT_TOL
