@@ -525,14 +525,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_DIST_BACKEND: the collective backend ("nccl" = RCCL, the default; "gloo" rehearses the
+    # multi-rank path with ranks sharing a GPU -- tests/test_bench_gpu.py runs 2 ranks on one device)
+    dist_backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count() if dist_backend == "gloo" else 0
+    device_index = local_rank % ndev if ndev else local_rank
     dist = None
+    coll_device = None  # where the timing collective's tensor lives (gloo: host)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(device_index)
+        if dist_backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
+            coll_device = torch.device("cuda", device_index)
 
     lib = G.runtime()
-    backend = G.mi355x_backend(lib, local_rank)
+    backend = G.mi355x_backend(lib, device_index)
     stream_ptr = lib.ggml_backend_mi355x_get_stream(backend)
     t = TYPE_NAMES[args.type]
     K, N, B, R = args.K, args.N, args.B, args.rotate
@@ -556,7 +566,7 @@ def main():
             wl.step()
         ev1.record(ext_stream)
 
-    dt = timed_region(run_steps, sync, dist, torch.device("cuda", local_rank) if dist else None)
+    dt = timed_region(run_steps, sync, dist, coll_device)
 
     ub = unit_bytes(t, K, N, B)
     value = R * ub * args.steps * world / dt / 1e9
@@ -676,7 +686,7 @@ def main():
             for _ in range(5):
                 w4.step()
 
-        dtp = timed_region(run_pf, sync, dist, torch.device("cuda", local_rank))
+        dtp = timed_region(run_pf, sync, dist, coll_device)
         result["prefill_sharded"] = {"workload": "8 x Q4_K 4096x4096 x B=512 per step, columns sharded over ranks",
                                      "columns_per_rank": cnt, "TFLOP/s": round(2.0 * 4096 * 4096 * 512 * 8 * 5 / dtp / 1e12, 2),
                                      "us_per_mul_mat": round(dtp / 5 / 8 * 1e6, 2)}
@@ -685,7 +695,9 @@ def main():
     if world > 1 and not args.no_sweep:
         # the optional tensor-split row path (RCCL): reported beside the main line, never fatal to it
         try:
-            result["prefill_rowsplit_rccl"] = rowsplit_prefill(lib, backend, dist, world, rank, torch.device("cuda", local_rank), torch)
+            if dist_backend != "nccl":
+                raise RuntimeError(f"the row-split leg exchanges device tensors over RCCL; collective backend is {dist_backend}")
+            result["prefill_rowsplit_rccl"] = rowsplit_prefill(lib, backend, dist, world, rank, coll_device, torch)
         except Exception as e:  # noqa: BLE001
             result["prefill_rowsplit_rccl"] = {"error": f"{type(e).__name__}: {e}"}
 

@@ -1852,10 +1852,53 @@ static int try_fuse_attn_proj(mi_backend_ctx * ctx, ggml_cgraph * g, int i, cons
     return k2;
 }
 
+// Quantized prompt mul_mats in a reference-order graph (mmv_order 1, or -1 resolved to 1: a quantized
+// model's graph): the int8-MFMA prefill GEMMs compute the reference's exact integer block sums but
+// fold them in their own canonical order, and since every layer re-quantizes its activations an ulp
+// there becomes a quant step (~1e-2 of max|logit|). Up to g_ord_prefill_cols columns such a mul_mat
+// runs instead as the reference-order decode GEMV (k_mmv_stream ORD: the CPU's vec_dot lane chains,
+// bit-identical) over chunks of 8 columns -- each chunk re-reads the weights, so longer prompts keep
+// the MFMA GEMM. GGML_MI355X_ORD_PREFILL_COLS / set_tuning("ord_prefill_cols", n); 0 turns it off.
+static int g_ord_prefill_cols = getenv("GGML_MI355X_ORD_PREFILL_COLS") ? atoi(getenv("GGML_MI355X_ORD_PREFILL_COLS")) : 64;
+
+static bool ord_prefill_chunked(const ggml_tensor * n) {
+    if (n->op != GGML_OP_MUL_MAT || mi_mmv_order() != 1 || is_split_tensor(n->src[0])) return false;
+    const ggml_tensor * a = n->src[0];
+    const ggml_tensor * b = n->src[1];
+    if (b->type != GGML_TYPE_F32 || b->ne[1] <= 8 || b->ne[1] > g_ord_prefill_cols) return false;
+    if (a->type != GGML_TYPE_Q4_K && a->type != GGML_TYPE_Q5_K && a->type != GGML_TYPE_Q4_0 && a->type != GGML_TYPE_Q8_0) return false;
+    if (!mi_mmv_fused_supported(a->type, a->ne[0], 8)) return false;
+    if (a->ne[2] != 1 || a->ne[3] != 1 || b->ne[2] != 1 || b->ne[3] != 1) return false;
+    if (a->nb[0] != ggml_type_size(a->type) || b->nb[0] != sizeof(float) || n->nb[0] != sizeof(float)) return false;
+    if (((uintptr_t) a->data | a->nb[1]) % 16 != 0 || ((uintptr_t) b->data | b->nb[1]) % 16 != 0 || n->nb[1] % sizeof(float)) return false;
+    return !overlaps(n, a) && !overlaps(n, b);
+}
+
+static void run_ord_prefill_chunks(mi_backend_ctx * ctx, ggml_tensor * n) {
+    const ggml_tensor * a = n->src[0];
+    const ggml_tensor * b = n->src[1];
+    for (int64_t c0 = 0; c0 < b->ne[1]; c0 += 8) {
+        mi_mmv_group g;
+        g.type = a->type;
+        g.n = 1;
+        g.ncols = (int) std::min<int64_t>(8, b->ne[1] - c0);
+        g.K = a->ne[0];
+        g.N = a->ne[1];
+        g.nb01 = a->nb[1];
+        g.xcol = b->nb[1];
+        g.ycol = n->nb[1];
+        g.m[0].W = a->data;
+        g.m[0].X = (const char *) b->data + c0 * b->nb[1];
+        g.m[0].dst = (float *) ((char *) n->data + c0 * n->nb[1]);
+        mi_mul_mat_q_fused(g, ctx->stream);
+        ctx->last_launches++;
+    }
+}
+
 // the activation kind of a MUL_MAT node that runs on an exact int8 prefill GEMM (Q4_K / Q5_K: 8,
 // Q4_0 / Q8_0: 9; > 8 plain columns), or -1
 static int prefill_mmx_kind(const ggml_tensor * n) {
-    if (n->op != GGML_OP_MUL_MAT || is_split_tensor(n->src[0])) return -1;
+    if (n->op != GGML_OP_MUL_MAT || is_split_tensor(n->src[0]) || ord_prefill_chunked(n)) return -1;
     const ggml_tensor * a = n->src[0], * b = n->src[1];
     if (b->type != GGML_TYPE_F32 || a->nb[0] != ggml_type_size(a->type) || b->nb[0] != sizeof(float) || n->nb[0] != sizeof(float)) return -1;
     if (a->ne[0] != b->ne[0]) return -1;
@@ -2523,6 +2566,10 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
                     i = run_fused_group(ctx, cgraph, i);
                     continue;
                 }
+                if (ord_prefill_chunked(node)) {
+                    run_ord_prefill_chunks(ctx, node);
+                    break;
+                }
                 const int lastg = run_prefill_group(ctx, cgraph, i);
                 if (lastg >= 0) {
                     i = lastg;
@@ -2849,7 +2896,11 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.mmv_order = value;
         return true;
     }
-    if (strcmp(name, "xfirst") == 0 && (value == 0 || value == 1)) {
+    if (strcmp(name, "ord_prefill_cols") == 0 && value >= 0) {
+        g_ord_prefill_cols = value;
+        return true;
+    }
+    if (strcmp(name, "xfirst") == 0 && value >= -1 && value <= 1) {
         g_mi_tuning.xfirst = value;
         return true;
     }

@@ -233,7 +233,7 @@ void mi_attn_proj(const mi_attn_desc & a, const mi_attn_proj_desc & p, hipStream
     const size_t lds = (size_t) (a.n_kv + 3 + 8 * (a.D + 8) + a.D) * sizeof(float);
     mi_attn_proj_desc ps = p;
     ps.stamps = mi_stamp_take("k_attn_proj", grid.x * grid.y);
-    if (g_mi_tuning.xfirst) {
+    if (g_mi_tuning.xfirst == 1) {  // (off by default, as the F16 GEMVs)
         if (a.n_kv <= 256) hipLaunchKernelGGL((k_attn_proj<64, 4, true>), grid, dim3(512), lds, s, a, ps);
         else hipLaunchKernelGGL((k_attn_proj<64, 8, true>), grid, dim3(512), lds, s, a, ps);
     } else {

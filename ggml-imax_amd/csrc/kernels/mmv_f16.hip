@@ -508,7 +508,7 @@ void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_c
     const uint8_t * w = (const uint8_t *) W;
     mi_f16_epilogue es = e;
     es.stamps = mi_stamp_take(JM ? "k_gemv_f16_norm" : "k_gemv_f16", grid.x * grid.y);
-    es.xfirst = g_mi_tuning.xfirst;
+    es.xfirst = g_mi_tuning.xfirst == 1;  // (off by default: GPT-2 decode 304 -> 316 us per token with it)
 #define MI_GEMV_F16(EP) hipLaunchKernelGGL((k_gemv_f16<NC, EP, U, ONE, JM>), grid, dim3(64 * ks * rgs), lds, s, w, nb01, K, N, x, xh, ncols, dst, ycol, es, pro, kp, rgs)
     switch (epi) {
         case 0: MI_GEMV_F16(0); break;
@@ -582,7 +582,7 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         const uint8_t * w = (const uint8_t *) W;
         mi_f16_epilogue es = e;
         es.stamps = mi_stamp_take("k_gemv_f16_tall", grid.x);
-        es.xfirst = g_mi_tuning.xfirst;
+        es.xfirst = g_mi_tuning.xfirst == 1;  // (off by default: GPT-2 decode 304 -> 316 us per token with it)
 #define MI_GEMV_TALL(EP, JMV) hipLaunchKernelGGL((k_gemv_f16_tall<EP, 8, JMV>), grid, dim3(256), lds, s, w, nb01, K, N, x, dst, es, pro, kp)
         if (pro.mode) {
             if (epi == 0) MI_GEMV_TALL(0, 4); else if (epi == 1) MI_GEMV_TALL(1, 4); else MI_GEMV_TALL(3, 4);
@@ -604,7 +604,7 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         const uint8_t * w = (const uint8_t *) W;
         mi_f16_epilogue es = e;
         es.stamps = mi_stamp_take("k_gemv_f16_ps", grid.x);
-        es.xfirst = g_mi_tuning.xfirst;
+        es.xfirst = g_mi_tuning.xfirst == 1;  // (off by default: GPT-2 decode 304 -> 316 us per token with it)
 #define MI_GEMV_PS(EP, NPM, QPT) hipLaunchKernelGGL((k_gemv_f16_ps<EP, 8, 4, NPM, QPT>), grid, dim3(64 * rw), lds, s, w, nb01, K, N, dst, es, pro, kp)
 #define MI_GEMV_PS_E(NPM, QPT)                     \
         switch (epi) {                             \

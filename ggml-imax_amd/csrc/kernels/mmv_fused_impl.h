@@ -843,8 +843,12 @@ template <class F, int NC, bool ORD>
 void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
     const int items = (int) (g.K / F::ITEM);
     const mi_mmv_group::epilogue & e = g.epi;
-    // lone members (a dependent layer's GEMV): activations first (XF), every row of a wave in flight
-    const bool xf = g.n == 1 && g_mi_tuning.xfirst;
+    // lone members (a dependent layer's GEMV): activations first (XF), every row of a wave in flight.
+    // Automatic (xfirst -1): from K = 2048 on, where the activation side (16 KB of f32 per workgroup
+    // at K = 4096, and its quantization) is the long pole -- lone Q4_K 4096^2 6.93 -> 6.11 us per
+    // graph, 3072 x 768 4.96 -> 4.57 us; at GPT-2's K = 768 the weights' latency would be exposed
+    // after the activations' (decode token 456 -> 475 us, profiles/r05c_xfirst_ab.txt)
+    const bool xf = g.n == 1 && (g_mi_tuning.xfirst == 1 || (g_mi_tuning.xfirst < 0 && g.K >= 2048));
     if (g.pro.mode || e.bias || e.resid || e.gelu_table || e.copy[0].ptr || e.copy[1].ptr) {
         // the graph's norm prologue and/or epilogue: instances of their own (prefetch depth 1) so
         // that their registers and per-row branches do not weigh on the plain kernels

@@ -63,3 +63,30 @@ def test_torch_view_and_rowsplit_leg():
     assert out["res"]["parity_ok"], out["res"]
     # ... and bit for bit the unsplit product
     assert out["same_as_direct"]
+
+
+def test_bench_two_ranks_rehearsal():
+    """bench.py's world > 1 branches end to end before the driver's 8-GPU run: two ranks launched by
+    torch.distributed.run as the driver launches them, sharing this box's one GPU over the gloo
+    collective backend (BENCH_DIST_BACKEND; RCCL refuses two ranks on one device). Checks the
+    barrier + max-over-ranks timing, the whole-job value (both ranks' units), and the config-5
+    prompt-sharded prefill leg (256 columns per rank); the RCCL row-split leg reports that it needs
+    RCCL instead of failing the line."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-gpt2",
+           "--no-cpu"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400, cwd=REPO)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["scaling"] == "weak"
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    pf = out["prefill_sharded"]
+    assert pf["columns_per_rank"] == 256 and pf["us_per_mul_mat"] > 0
+    assert "RCCL" in out["prefill_rowsplit_rccl"].get("error", "")

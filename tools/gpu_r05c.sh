@@ -17,5 +17,5 @@ for XF in 1 0; do
   GGML_MI355X_XFIRST=$XF timeout -k 10 200 python3 -u tools/stamps.py gpt2 q4_k 8 > "$OUT/gpt2_q4k_xf$XF.txt" 2>&1
   tail -3 "$OUT/gpt2_q4k_xf$XF.txt"
 done
-timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_mul_mat_gpu.py tests/test_gpt2.py tests/test_prefill_gpu.py -k "not full_size" > "$OUT/pytest.txt" 2>&1
+timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_mul_mat_gpu.py tests/test_gpt2.py tests/test_prefill_gpu.py tests/test_llama_block_gpu.py tests/test_bench_gpu.py -k "not full_size" > "$OUT/pytest.txt" 2>&1
 tail -5 "$OUT/pytest.txt"
