@@ -260,16 +260,25 @@ def gpt2_batched_bench(lib, backend, n_parallel=8, n_steps=48):
         lib.ggml_backend_mi355x_graph_stats_ex(backend, a, 6)
         return list(a)
 
+    def bstats():
+        a = (ctypes.c_int64 * 2)()
+        if hasattr(lib, "gpt2_batch_stats"):
+            lib.gpt2_batch_stats(m.m, a)
+        return list(a)
+
     try:
         run()  # untimed pass: first captures of each topology, allocator and cache warm-up
-        s0 = stats()
+        s0, b0 = stats(), bstats()
         dt = run()
-        s1 = stats()
+        s1, b1 = stats(), bstats()
         r = {"workload": f"{n_parallel} sequences sharing an 8-token prompt, {n_steps} batched decode steps (main-batched.cpp)",
              "decode_tokens_per_s": round(n_parallel * n_steps / dt, 1), "ms_per_step": round(dt / n_steps * 1e3, 4),
              "kernel_launches_per_step": lib.ggml_backend_mi355x_last_launch_count(backend),
              "parity": "within 1e-3 of the reference CPU, bit-identical with mmv_order=1 (tests/test_gpt2.py batched tests)",
-             "graph_compute_calls": {"direct": s1[3] - s0[3], "replays": s1[4] - s0[4], "captures": s1[5] - s0[5]}}
+             "graph_compute_calls": {"direct": s1[3] - s0[3], "replays": s1[4] - s0[4], "captures": s1[5] - s0[5]},
+             "steps": {"prebuilt_plan_launches": b1[0] - b0[0], "built_on_the_spot": b1[1] - b0[1],
+                       "note": "a step's graph is built, allocated and captured as a plan while the device runs the previous "
+                               "step; its inputs (tokens, positions, KQ mask) go in as one async copy"}}
         if hasattr(lib, "ggml_backend_mi355x_set_graph_capture"):
             lib.ggml_backend_mi355x_set_graph_capture(backend, False)
             try:

@@ -95,6 +95,18 @@ struct gpt2_model {
     };
     std::vector<kv_cell> cells;
     uint32_t kv_head = 0, kv_n = 0;
+    // batched decode inputs, host_io: one pinned staging block and one device block [tokens | pos |
+    // KQ mask] (one async copy per step; the graph's inputs are views of the device block), and the
+    // next step's graph built + allocated + planned while the device runs the current one
+    ggml_backend_buffer_type_t host_buft = nullptr;
+    ggml_context * ctx_bin = nullptr;
+    ggml_backend_buffer_t buf_bin_host = nullptr, buf_bin_dev = nullptr;
+    ggml_tensor * bin_host = nullptr, * bin_dev = nullptr;
+    ggml_cgraph * bnext_gf = nullptr;                 // prebuilt batched graph of (bnext_tokens, bnext_head)
+    int bnext_tokens = -1, bnext_head = -1;
+    ggml_backend_graph_plan_t bnext_plan = nullptr;
+    int64_t batch_plans = 0, batch_direct = 0;       // steps launched as a prebuilt plan / built on the spot
+    int batch_reserved = 0;                           // batch size the compute buffer is reserved for
 };
 
 namespace {
@@ -428,13 +440,22 @@ ggml_cgraph * build_graph_batched(gpt2_model & m, int n_tokens, int n_kv, int kv
     ggml_cgraph * gf = ggml_new_graph_custom(ctx, kMaxNodes, false);
 
     ggml_tensor * inp_tokens = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, n_tokens);
+    ggml_tensor * position = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, n_tokens);
+    ggml_tensor * KQ_mask = ggml_new_tensor_3d(ctx, GGML_TYPE_F32, n_kv, n_tokens, 1);
+    if (m.bin_dev) {
+        // placed in the persistent device input block [tokens | pos | mask] (one async copy per
+        // step; the graph allocator leaves tensors that already have memory alone)
+        char * base = (char *) m.bin_dev->data;
+        inp_tokens->data = base;
+        position->data = base + (size_t) n_tokens * 4;
+        KQ_mask->data = base + (size_t) 2 * n_tokens * 4;
+        inp_tokens->buffer = position->buffer = KQ_mask->buffer = m.buf_bin_dev;
+    }
     ggml_set_name(inp_tokens, "inp_tokens");
     ggml_set_input(inp_tokens);
-    ggml_tensor * position = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, n_tokens);
     ggml_set_name(position, "position");
     ggml_set_input(position);
     ggml_tensor * inpL = ggml_add(ctx, ggml_get_rows(ctx, m.wte, inp_tokens), ggml_get_rows(ctx, m.wpe, position));
-    ggml_tensor * KQ_mask = ggml_new_tensor_3d(ctx, GGML_TYPE_F32, n_kv, n_tokens, 1);
     ggml_set_name(KQ_mask, "KQ_mask");
     ggml_set_input(KQ_mask);
 
@@ -542,6 +563,7 @@ gpt2_model * gpt2_model_load_ex(const char * fname, ggml_backend_t backend, int 
         ggml_set_name(m->embd_in, "in/embd");
         ggml_set_name(m->pos_in, "in/position");
         ggml_set_name(m->logits_host, "out/logits");
+        m->host_buft = host_buft;
         m->buffer_input = ggml_backend_alloc_ctx_tensors_from_buft(m->ctx_in, host_buft);
         // the device reads these in place: a buffer the type fell back to (e.g. pageable memory,
         // another buffer type) will not do
@@ -640,6 +662,13 @@ void gpt2_model_free(gpt2_model * m) {
 #ifdef GPT2_WITH_SCHED
     if (m->sched) ggml_backend_sched_free((ggml_backend_sched_t) m->sched);
 #endif
+    if (m->bnext_plan) {
+        ggml_backend_synchronize(m->backend);
+        ggml_backend_graph_plan_free(m->backend, m->bnext_plan);
+    }
+    if (m->buf_bin_host) ggml_backend_buffer_free(m->buf_bin_host);
+    if (m->buf_bin_dev) ggml_backend_buffer_free(m->buf_bin_dev);
+    if (m->ctx_bin) ggml_free(m->ctx_bin);
     if (m->buffer_input) ggml_backend_buffer_free(m->buffer_input);
     if (m->ctx_in) ggml_free(m->ctx_in);
     if (m->buffer_pos) ggml_backend_buffer_free(m->buffer_pos);
@@ -676,6 +705,57 @@ void gpt2_kv_cache_seq_cp(gpt2_model * m, int32_t seq_src, int32_t seq_dst, int3
 // gpt2_decode (main-batched.cpp:854-968): the batch's tokens go into KV cells kv_head.., the graph
 // attends to cells [0, kv_head + n_tokens) through the host-built KQ mask (a cell is visible to a
 // token when it belongs to the token's sequence at a position <= the token's)
+// the batched path's prebuilt graph / plan (arenas and allocator are shared with gpt2_eval's)
+static void drop_batch_prebuilt(gpt2_model * m) {
+    if (m->bnext_plan) {
+        ggml_backend_synchronize(m->backend);
+        ggml_backend_graph_plan_free(m->backend, m->bnext_plan);
+        m->bnext_plan = nullptr;
+    }
+    m->bnext_gf = nullptr;
+    m->bnext_tokens = m->bnext_head = -1;
+}
+
+// host_io: the pinned staging block and the device input block, grown to hold n_tokens tokens and
+// positions and an n_ctx x n_tokens mask
+static bool batch_inputs_reserve(gpt2_model * m, int n_tokens) {
+    const size_t need = (size_t) 2 * n_tokens * 4 + (size_t) m->hp.n_ctx * n_tokens * 4;
+    if (!m->bin_dev || ggml_nbytes(m->bin_dev) < need) {
+        drop_batch_prebuilt(m);
+        ggml_backend_synchronize(m->backend);
+        if (m->buf_bin_host) ggml_backend_buffer_free(m->buf_bin_host);
+        if (m->buf_bin_dev) ggml_backend_buffer_free(m->buf_bin_dev);
+        if (m->ctx_bin) ggml_free(m->ctx_bin);
+        m->bin_host = m->bin_dev = nullptr;
+        m->buf_bin_host = m->buf_bin_dev = nullptr;
+        ggml_init_params ip = {ggml_tensor_overhead() * 2, nullptr, true};
+        m->ctx_bin = ggml_init(ip);
+        ggml_tensor * h = ggml_new_tensor_1d(m->ctx_bin, GGML_TYPE_F32, (int64_t) (need / 4));
+        ggml_tensor * d = ggml_new_tensor_1d(m->ctx_bin, GGML_TYPE_F32, (int64_t) (need / 4));
+        ggml_set_name(h, "in/batch_host");
+        ggml_set_name(d, "in/batch");
+        m->buf_bin_host = ggml_backend_buft_alloc_buffer(m->host_buft, ggml_backend_buft_get_alloc_size(m->host_buft, h));
+        m->buf_bin_dev = ggml_backend_alloc_buffer(m->backend, ggml_nbytes(d) + 256);
+        if (!m->buf_bin_host || !m->buf_bin_dev) return false;
+        ggml_tallocr ah = ggml_tallocr_new(m->buf_bin_host);
+        ggml_tallocr_alloc(&ah, h);
+        ggml_tallocr ad = ggml_tallocr_new(m->buf_bin_dev);
+        ggml_tallocr_alloc(&ad, d);
+        m->bin_host = h;
+        m->bin_dev = d;
+    }
+    if (m->batch_reserved < n_tokens) {
+        // the compute buffer sized for this batch at a full KV cache, once, while nothing runs: a
+        // graph allocated during the previous step's execution must never grow (reallocate) it
+        drop_batch_prebuilt(m);
+        ggml_backend_synchronize(m->backend);
+        ggml_cgraph * worst = build_graph_batched(*m, n_tokens, m->hp.n_ctx, m->hp.n_ctx - n_tokens, m->graph_slot ^ 1);
+        if (!ggml_gallocr_reserve(m->allocr, worst)) return false;
+        m->batch_reserved = n_tokens;
+    }
+    return true;
+}
+
 int gpt2_decode_batch(gpt2_model * m, int n_tokens, const int32_t * tokens, const int32_t * pos, const int32_t * seq_id,
                       float * logits, int all_logits) {
     if (n_tokens <= 0 || !tokens || !pos || !seq_id) {
@@ -707,17 +787,51 @@ int gpt2_decode_batch(gpt2_model * m, int n_tokens, const int32_t * tokens, cons
     }
     m->kv_n = m->kv_head + (uint32_t) n_tokens;
     const int n_kv = (int) m->kv_n;
-    m->graph_slot ^= 1;
-    ggml_cgraph * gf = build_graph_batched(*m, n_tokens, n_kv, (int) m->kv_head, m->graph_slot);
-    const int64_t t1 = now_us();
-    if (!ggml_gallocr_alloc_graph(m->allocr, gf)) {
-        fprintf(stderr, "gpt2_decode_batch: graph allocation failed\n");
-        return 1;
+    const size_t nv = (size_t) m->hp.n_vocab;
+    const size_t lg_off = all_logits ? 0 : sizeof(float) * nv * (n_tokens - 1), lg_size = sizeof(float) * nv * (all_logits ? n_tokens : 1);
+    // host_io (pinned staging): inputs in one async copy, the step launched as a plan prebuilt during
+    // the previous step, the logits staged behind it, the next step prebuilt while this one runs
+    const bool fast = m->host_io && m->backend->iface.graph_plan_create && lg_size <= ggml_nbytes(m->logits_host) &&
+                      batch_inputs_reserve(m, n_tokens);
+    ggml_cgraph * gf = nullptr;
+    ggml_backend_graph_plan_t plan = nullptr;
+    int64_t t1, t2;
+    if (fast && m->bnext_gf && m->bnext_tokens == n_tokens && m->bnext_head == (int) m->kv_head) {
+        gf = m->bnext_gf;
+        plan = m->bnext_plan;
+        m->bnext_plan = nullptr;
+        m->bnext_gf = nullptr;
+        m->graph_slot ^= 1;
+        m->batch_plans++;
+        t1 = t2 = now_us();
+    } else {
+        drop_batch_prebuilt(m);
+        m->graph_slot ^= 1;
+        gf = build_graph_batched(*m, n_tokens, n_kv, (int) m->kv_head, m->graph_slot);
+        t1 = now_us();
+        if (!ggml_gallocr_alloc_graph(m->allocr, gf)) {
+            fprintf(stderr, "gpt2_decode_batch: graph allocation failed\n");
+            return 1;
+        }
+        m->batch_direct++;
+        t2 = now_us();
     }
-    const int64_t t2 = now_us();
-    ggml_backend_tensor_set(ggml_graph_get_tensor(gf, "inp_tokens"), tokens, 0, (size_t) n_tokens * sizeof(int32_t));
-    ggml_backend_tensor_set(ggml_graph_get_tensor(gf, "position"), pos, 0, (size_t) n_tokens * sizeof(int32_t));
-    {
+    if (fast) {
+        // [tokens | pos | mask] into the pinned block, one async copy into the device block
+        char * hb = (char *) m->bin_host->data;
+        memcpy(hb, tokens, (size_t) n_tokens * 4);
+        memcpy(hb + (size_t) n_tokens * 4, pos, (size_t) n_tokens * 4);
+        float * mask = (float *) (hb + (size_t) 2 * n_tokens * 4);
+        for (int j = 0; j < n_tokens; j++) {
+            for (int i = 0; i < n_kv; i++) {
+                const auto & c = m->cells[i];
+                mask[(size_t) j * n_kv + i] = (!c.has(seq_id[j]) || c.pos > pos[j]) ? -INFINITY : 0.0f;
+            }
+        }
+        ggml_backend_tensor_set_async(m->backend, m->bin_dev, hb, 0, (size_t) 2 * n_tokens * 4 + (size_t) n_kv * n_tokens * 4);
+    } else {
+        ggml_backend_tensor_set(ggml_graph_get_tensor(gf, "inp_tokens"), tokens, 0, (size_t) n_tokens * sizeof(int32_t));
+        ggml_backend_tensor_set(ggml_graph_get_tensor(gf, "position"), pos, 0, (size_t) n_tokens * sizeof(int32_t));
         std::vector<float> mask((size_t) n_kv * n_tokens, 0.0f);
         for (int j = 0; j < n_tokens; j++) {
             for (int i = 0; i < n_kv; i++) {
@@ -728,24 +842,54 @@ int gpt2_decode_batch(gpt2_model * m, int n_tokens, const int32_t * tokens, cons
         ggml_backend_tensor_set(ggml_graph_get_tensor(gf, "KQ_mask"), mask.data(), 0, mask.size() * sizeof(float));
     }
     const int64_t t3 = now_us();
-    if (ggml_backend_graph_compute(m->backend, gf) != GGML_STATUS_SUCCESS) {
-        fprintf(stderr, "gpt2_decode_batch: graph compute failed\n");
-        return 1;
-    }
     ggml_tensor * out = ggml_graph_get_tensor(gf, "logits");
-    const size_t nv = (size_t) m->hp.n_vocab;
-    if (logits) {
-        if (all_logits) ggml_backend_tensor_get(out, logits, 0, sizeof(float) * nv * n_tokens);
-        else ggml_backend_tensor_get(out, logits, sizeof(float) * nv * (n_tokens - 1), sizeof(float) * nv);
-    }
     m->kv_head += (uint32_t) n_tokens;
     m->last_nodes = gf->n_nodes;
+    if (!fast) {
+        if (ggml_backend_graph_compute(m->backend, gf) != GGML_STATUS_SUCCESS) {
+            fprintf(stderr, "gpt2_decode_batch: graph compute failed\n");
+            return 1;
+        }
+        if (logits) {
+            if (all_logits) ggml_backend_tensor_get(out, logits, 0, sizeof(float) * nv * n_tokens);
+            else ggml_backend_tensor_get(out, logits, sizeof(float) * nv * (n_tokens - 1), sizeof(float) * nv);
+        }
+    } else {
+        const ggml_status st = plan ? ggml_backend_graph_plan_compute(m->backend, plan) : ggml_backend_graph_compute_async(m->backend, gf);
+        if (st != GGML_STATUS_SUCCESS) {
+            fprintf(stderr, "gpt2_decode_batch: graph compute failed\n");
+            if (plan) ggml_backend_graph_plan_free(m->backend, plan);
+            return 1;
+        }
+        ggml_backend_tensor_get_async(m->backend, out, m->logits_host->data, lg_off, lg_size);
+        // the next step of the same batch size (one token per sequence: main-batched.cpp's loop),
+        // built, allocated and captured while the device runs this one; its inputs are data
+        const int nh = (int) m->kv_head;
+        if (nh + n_tokens <= m->hp.n_ctx) {
+            ggml_cgraph * nx = build_graph_batched(*m, n_tokens, nh + n_tokens, nh, m->graph_slot ^ 1);
+            if (ggml_gallocr_alloc_graph(m->allocr, nx)) {
+                m->bnext_gf = nx;
+                m->bnext_tokens = n_tokens;
+                m->bnext_head = nh;
+                m->bnext_plan = ggml_backend_graph_plan_create(m->backend, nx);
+            }
+        }
+        ggml_backend_synchronize(m->backend);
+        if (plan) ggml_backend_graph_plan_free(m->backend, plan);  // its graph has run
+        if (logits) memcpy(logits, m->logits_host->data, lg_size);
+    }
     m->us_build = t1 - t0;
     m->us_alloc = t2 - t1;
     m->us_inputs = t3 - t2;
     m->us_compute = now_us() - t3;
     return 0;
 }
+
+void gpt2_batch_stats(const gpt2_model * m, int64_t * out2) {
+    out2[0] = m->batch_plans;
+    out2[1] = m->batch_direct;
+}
+
 size_t gpt2_model_size(const gpt2_model * m) { return m->weight_bytes; }
 size_t gpt2_compute_buffer_size(const gpt2_model * m) { return ggml_gallocr_get_buffer_size(m->allocr, 0); }
 
@@ -789,6 +933,7 @@ int gpt2_eval(gpt2_model * m, int n_past, const int32_t * tokens, int N, float *
         return 0;
     }
 #endif
+    drop_batch_prebuilt(m);
     const int64_t t0 = now_us();
     ggml_cgraph * gf;
     int64_t t1, t1b;

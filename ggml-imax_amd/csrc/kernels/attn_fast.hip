@@ -165,6 +165,7 @@ __global__ __launch_bounds__(512) void k_attn_proj(mi_attn_desc a, mi_attn_proj_
     extern __shared__ __attribute__((aligned(16))) float sm[];  // s[n_kv] | red[8][D + 8] | (16 B aligned) oh[D] f16
     __shared__ float shm[8];
     MI_STAMP(p.stamps, 0);
+    MI_STAMP_CLK(p.stamps, 6);
     const int rb = blockIdx.x, h = blockIdx.y;
     const int c = threadIdx.x % LPR;
     const int64_t row = (int64_t) rb * RPW + threadIdx.x / LPR;
@@ -190,6 +191,7 @@ __global__ __launch_bounds__(512) void k_attn_proj(mi_attn_desc a, mi_attn_proj_
     acc = group_sum<LPR>(acc);
     // head 0: (x + bias) + resid, the order of the unfused epilogue
     if (c == 0 && row < p.N) p.parts[(size_t) h * p.N + row] = h == 0 ? (acc + e_bias) + e_res : acc;
+    MI_STAMP_CLK(p.stamps, 5);
     MI_STAMP(p.stamps, 7);
 }
 

@@ -21,9 +21,19 @@
         if ((buf) && threadIdx.x == 0)                                                                                     \
             (buf)[((size_t) blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();        \
     } while (0)
+// the shader clock (s_memtime) at the same point: slot 6 at entry, 5 at exit give the clock the
+// workgroup ran at (delta memtime / delta realtime x 100 MHz)
+#define MI_STAMP_CLK(buf, slot)                                                                                            \
+    do {                                                                                                                   \
+        if ((buf) && threadIdx.x == 0)                                                                                     \
+            (buf)[((size_t) blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memtime();             \
+    } while (0)
 #else
 #define MI_STAMP(buf, slot) \
     do {                    \
+    } while (0)
+#define MI_STAMP_CLK(buf, slot) \
+    do {                        \
     } while (0)
 #endif
 

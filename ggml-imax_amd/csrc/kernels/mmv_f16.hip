@@ -163,6 +163,36 @@ struct ColStager {
     }
 };
 
+// Several f32 activation columns -> f16 LDS (each zero-padded to kp), rounds of JX float4 per thread
+// over the flattened [nc][K / 4] index space, every load of a round in flight together (a column
+// per round costs a dependent memory round trip per column)
+template <int JX>
+__device__ __forceinline__ void stage_cols(const mi_src_cols & x, int64_t c0, int nc, int64_t K, int64_t kp, uint16_t * xs) {
+    const int64_t k4 = K / 4, total = (int64_t) nc * k4;
+    for (int64_t base = 0; base < total; base += (int64_t) JX * blockDim.x) {
+        float4 v[JX];
+#pragma unroll
+        for (int j = 0; j < JX; j++) {
+            const int64_t i = base + (int64_t) j * blockDim.x + threadIdx.x;
+            const int64_t ic = i < total ? i : total - 1;  // branch-free loads (see norm_load)
+            const int64_t c = ic / k4, q = ic - c * k4;
+            v[j] = *(const float4 *) (x.base + (c0 + c) * x.nb1 + q * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < JX; j++) {
+            const int64_t i = base + (int64_t) j * blockDim.x + threadIdx.x;
+            if (i < total) {
+                const int64_t c = i / k4, q = i - c * k4;
+                *(uint2 *) (xs + c * kp + q * 4) = make_uint2(pack_h2(v[j].x, v[j].y), pack_h2(v[j].z, v[j].w));
+            }
+        }
+    }
+    for (int64_t i = threadIdx.x; i < (int64_t) nc * (kp - K); i += blockDim.x) {
+        const int64_t c = i / (kp - K);
+        xs[c * kp + K + (i - c * (kp - K))] = 0;
+    }
+}
+
 // One workgroup = RGS row groups of 4 weight rows (16 lanes per row) x KS waves per group
 // (runtime: KS = blockDim.x / 64 / RGS); a group's waves split the rows' 128-wide K steps: wave
 // s of the group takes steps s, s + KS, ... -- at most U of them in registers when ONE, else a
@@ -179,6 +209,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
                                                   int64_t kp, int rgs) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][kp] f16 (zero beyond K), then [waves][4][NC] f32
     MI_STAMP(e.stamps, 0);
+    MI_STAMP_CLK(e.stamps, 6);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x >> 6) / rgs;
     const int grp = wid / nw, wave = wid % nw;  // row group, K slice
     const int m = lane & (kLpr - 1), rg = lane >> 4;
@@ -232,10 +263,25 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
         if (priv) {
             norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xw, lane);
         } else {
+            // several columns per wave: the next column's x is requested before this one is
+            // normalized (g and b are the same for every column), so the columns' loads overlap
             const int nwt = blockDim.x >> 6;
             for (int c = wid; c < nc; c += nwt) {
-                if (c != wid) norm_load<JM, GB>((const float *) (x.base + (c0 + c) * x.nb1), K, lane, pro, pv, pg, pb);
+                const int cn = c + nwt < nc ? c + nwt : nc - 1;
+                float4 nv[JM > 0 ? JM : 1];
+                {
+                    const float * xc = (const float *) (x.base + (c0 + cn) * x.nb1);
+#pragma unroll
+                    for (int j = 0; j < JM; j++) {
+                        const int64_t k = (int64_t) j * 256 + lane * 4;
+                        const bool in = k < K;
+                        const float4 vv = *(const float4 *) (xc + (in ? k : K - 4));
+                        nv[j] = in ? vv : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
                 norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) c * kp, lane);
+#pragma unroll
+                for (int j = 0; j < JM; j++) pv[j] = nv[j];
             }
         }
     } else if (xh) {
@@ -244,10 +290,12 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
             uint4 * xd = (uint4 *) (xs + (size_t) c * kp);
             for (int64_t k = threadIdx.x; k < kp / 8; k += blockDim.x) xd[k] = k < k8 ? src[k] : make_uint4(0u, 0u, 0u, 0u);
         }
-    } else {
+    } else if (nc == 1) {
         st.store(xs, kp, 0);
         st.column((const float *) (x.base + c0 * x.nb1), K, kp, xs, (int64_t) JX * blockDim.x);
-        for (int c = 1; c < nc; c++) st.column((const float *) (x.base + (c0 + c) * x.nb1), K, kp, xs + (size_t) c * kp, 0);
+    } else {
+        (void) st;
+        stage_cols<JX>(x, c0, nc, K, kp, xs);
     }
     MI_STAMP(e.stamps, 1);  // activations staged (normalized) by wave 0
     if (!priv) mi_lds_barrier();
@@ -313,6 +361,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
                 *(float *) (e.copy[k].ptr + col * e.copy[k].col_stride + (row - e.copy[k].row0) * sizeof(float)) = v;
         }
     }
+    MI_STAMP_CLK(e.stamps, 5);
     MI_STAMP(e.stamps, 7);
 }
 
@@ -327,6 +376,7 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
                                                        mi_norm_prologue pro, int64_t kp) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [kp] f16
     MI_STAMP(e.stamps, 0);
+    MI_STAMP_CLK(e.stamps, 6);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int m = lane & (kLpr - 1), rg = lane >> 4;
     const int64_t ngroups = (N + 3) / 4, stride = (int64_t) gridDim.x * 4;
@@ -389,6 +439,7 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
         for (int u = 0; u < U; u++) cur[u] = nxt[u];
         eb = ebn;
     }
+    MI_STAMP_CLK(e.stamps, 5);
     MI_STAMP(e.stamps, 7);
 }
 
@@ -406,6 +457,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
     const int rw = blockDim.x >> 6;
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [rw][kp] f16 per wave, then [kp] f32 (the sum)
     MI_STAMP(e.stamps, 0);
+    MI_STAMP_CLK(e.stamps, 6);
     float * xf = (float *) (xs + (size_t) rw * kp);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int m = lane & (kLpr - 1), rg = lane >> 4;
@@ -494,6 +546,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
                 *(float *) (e.copy[k].ptr + (row - e.copy[k].row0) * sizeof(float)) = r;
         }
     }
+    MI_STAMP_CLK(e.stamps, 5);
     MI_STAMP(e.stamps, 7);
 }
 

@@ -85,6 +85,77 @@ __device__ __forceinline__ void quantize_slice(float4 v4, int lane, const lds_ac
     }
 }
 
+// Q8_K of one superblock held by a 16-lane row, 16 consecutive elements per lane (a wave quantizes
+// four superblocks at once): quantize_row_q8_K_reference (src/ggml-quants.c:3370-3407) as the
+// reference's gcc -mfma build rounds it -- the first element of largest |x| keeps its sign
+// (a row's max and min decide it; only when +a and -a both occur is the first index looked up),
+// iscale = -127/max, q = min(127, RNE(iscale x)) by the fma bit trick, d = 1/iscale, zero
+// superblocks d = 0. 16-lane DPP reductions (4 steps) instead of whole-wave ones with readlanes.
+// `live`: this row's superblock exists (every lane takes part in the reductions).
+__device__ __forceinline__ float mi_dppf_max16(float v) {
+    auto f = [](int x) { return __int_as_float(x); };
+    auto i = [](float x) { return __float_as_int(x); };
+    v = fmaxf(v, f(mi_dpp<MI_DPP_QP_1032>(0, i(v))));
+    v = fmaxf(v, f(mi_dpp<MI_DPP_QP_2301>(0, i(v))));
+    v = fmaxf(v, f(mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, i(v))));
+    v = fmaxf(v, f(mi_dpp<MI_DPP_ROW_MIRROR>(0, i(v))));
+    return v;
+}
+__device__ __forceinline__ uint32_t mi_dpp_umin16(uint32_t v) {
+    v = min(v, (uint32_t) mi_dpp<MI_DPP_QP_1032>(0, (int) v));
+    v = min(v, (uint32_t) mi_dpp<MI_DPP_QP_2301>(0, (int) v));
+    v = min(v, (uint32_t) mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, (int) v));
+    v = min(v, (uint32_t) mi_dpp<MI_DPP_ROW_MIRROR>(0, (int) v));
+    return v;
+}
+__device__ __forceinline__ void quantize_row16(const float4 (&v4)[4], int lane, const lds_act & a, int64_t K, int c, int sl, bool live) {
+    float x[16];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        x[4 * u] = v4[u].x; x[4 * u + 1] = v4[u].y; x[4 * u + 2] = v4[u].z; x[4 * u + 3] = v4[u].w;
+    }
+    float mx = x[0], mn = x[0];
+#pragma unroll
+    for (int i = 1; i < 16; i++) {
+        mx = fmaxf(mx, x[i]);
+        mn = fminf(mn, x[i]);
+    }
+    mx = mi_dppf_max16(mx);
+    mn = -mi_dppf_max16(-mn);
+    float vmax = mx >= -mn ? mx : mn;
+    const bool tie = mx == -mn && mx != 0.0f;
+    if (__any(tie)) {  // +a and -a both largest in some row: the first one (key = 2 index + sign) wins
+        uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+        for (int i = 15; i >= 0; i--)
+            if (fabsf(x[i]) == mx) key = (uint32_t) ((((lane & 15) * 16 + i) << 1) | (x[i] < 0.0f ? 1 : 0));
+        key = mi_dpp_umin16(key);
+        if (tie) vmax = (key & 1) ? mn : mx;
+    }
+    const float iscale = vmax != 0.0f ? -127.f / vmax : 0.0f;
+    uint32_t w[4];
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint32_t pk = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const float t = __builtin_fmaf(iscale, x[4 * j + e], 12582912.f);
+            int q = (__float_as_int(t) & 0x007fffff) - 0x00400000;
+            q = q < 127 ? q : 127;
+            pk |= ((uint32_t) (q & 0xFF)) << (8 * e);
+        }
+        w[j] = pk;
+        s = mi_dot4((int) pk, 0x01010101, s);
+    }
+    const int s32 = s + mi_dpp<MI_DPP_QP_1032>(0, s);  // lanes 2m, 2m + 1 of the row: elements 32 m ..
+    if (live) {
+        *(uint4 *) (a.qs + c * K + sl * 256 + (lane & 15) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+        if ((lane & 1) == 0) a.s32[c * (K / 32) + sl * 8 + ((lane & 15) >> 1)] = (int16_t) s32;
+        if ((lane & 15) == 0) a.d[c * (K / 256) + sl] = vmax != 0.0f ? 1.0f / iscale : 0.0f;
+    }
+}
+
 // ------------------------------------------------------------------ weight formats
 
 template <bool Q5>
@@ -506,15 +577,43 @@ __device__ void norm_prologue(const mi_mmv_group & g, const char * X, int ncols,
 // one output element, through the graph's epilogue: + bias[row], then + resid or GELU (the fp16
 // table lookup of ggml_vec_gelu_f32 with its +-10 clamps), then the K/V-cache row copies -- each
 // step rounded as its own node would round it
-template <bool X>
-__device__ __forceinline__ void store_out(const mi_mmv_group & g, float * dst, int c, int row, float v) {
+// The epilogue operands of a wave's first row, requested in the prologue (a load at store time adds
+// a dependent memory round trip at the end of the kernel -- at GPT-2's sizes one row per wave)
+template <int NC>
+struct epi_pre {
+    int row = -1;
+    float bias = 0.0f;
+    float res[NC];
+};
+template <int NC>
+__device__ __forceinline__ void epi_prefetch(const mi_mmv_group & g, int row, const char * any, epi_pre<NC> & p) {
+    const mi_mmv_group::epilogue & e = g.epi;
+    p.row = row;
+    // unconditional loads at valid addresses (an absent operand reads `any`; its value is unused)
+    p.bias = *(e.bias ? e.bias + row : (const float *) any);
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const int cc = c < g.ncols ? c : g.ncols - 1;
+        p.res[c] = *(const float *) (e.resid ? e.resid + cc * e.resid_nb1 + (size_t) row * sizeof(float) : any);
+    }
+}
+
+template <bool X, int NC = 1>
+__device__ __forceinline__ void store_out(const mi_mmv_group & g, float * dst, int c, int row, float v, const epi_pre<NC> * pre = nullptr) {
     if constexpr (!X) {
         *(float *) ((char *) dst + c * g.ycol + (size_t) row * sizeof(float)) = v;
         return;
     }
     const mi_mmv_group::epilogue & e = g.epi;
-    if (e.bias) v = v + e.bias[row];
-    if (e.resid) v = v + *(const float *) (e.resid + c * e.resid_nb1 + (size_t) row * sizeof(float));
+    const bool hit = pre && row == pre->row;
+    float pr = pre ? pre->res[0] : 0.0f;
+    if (pre) {
+#pragma unroll
+        for (int cc = 1; cc < NC; cc++)
+            if (c == cc) pr = pre->res[cc];
+    }
+    if (e.bias) v = v + (hit ? pre->bias : e.bias[row]);
+    if (e.resid) v = v + (hit ? pr : *(const float *) (e.resid + c * e.resid_nb1 + (size_t) row * sizeof(float)));
     else if (e.gelu_table) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
     *(float *) ((char *) dst + c * g.ycol + (size_t) row * sizeof(float)) = v;
 #pragma unroll
@@ -538,6 +637,7 @@ template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO, bool 
 __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     MI_STAMP(g.stamps, 0);
+    MI_STAMP_CLK(g.stamps, 6);
     constexpr int NB = PD + 1;  // ring slots
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -583,19 +683,33 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     const int nsl = (int) (K / 256);
     const int total = nsl * ncols;
     float4 xfirst[4];
+    // Q8_K (R16): a round of a wave = slices p0 .. p0 + 3, one per 16-lane row (lane: 16 consecutive
+    // elements, quantize_row16); Q8_0: slices p0, p0 + 4, p0 + 8, p0 + 12, four elements per lane
+    constexpr bool R16 = F::QKA == 256;
+    const int p_first = R16 ? 4 * wave : wave;
     auto load_round = [&](float4 (&v)[4], const char * Xs, size_t xcs, int p0) {
         // unconditional (clamped) loads: a predicated load makes hipcc wait vmcnt(0) per load
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int p = min(p0 + 4 * u, total - 1);
+        if constexpr (R16) {
+            const int p = min(p0 + (lane >> 4), total - 1);
             const int c = p / nsl, sl = p - c * nsl;
-            v[u] = *(const float4 *) (Xs + c * xcs + ((size_t) sl * 256 + lane * 4) * sizeof(float));
+            const float4 * src = (const float4 *) (Xs + c * xcs + ((size_t) sl * 256 + (lane & 15) * 16) * sizeof(float));
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = src[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = min(p0 + 4 * u, total - 1);
+                const int c = p / nsl, sl = p - c * nsl;
+                v[u] = *(const float4 *) (Xs + c * xcs + ((size_t) sl * 256 + lane * 4) * sizeof(float));
+            }
         }
     };
+    epi_pre<NC> epre;
     if constexpr (PRO) {
         if (g.pro.mode && wave == 0) norm_cols_load(g, X, 0, nc0);
+        epi_prefetch<NC>(g, row_begin + wave < Nr ? row_begin + wave : Nr - 1, X, epre);
     } else {
-        load_round(xfirst, X, g.xcol, wave);
+        load_round(xfirst, X, g.xcol, p_first);
     }
     if constexpr (XF && !PRO) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // 1) the first PD rows' weights in flight
@@ -611,25 +725,32 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     if (PRO && g.pro.mode) {
         float * xn = (float *) (lds + g.pro_off);
         if (wave == 0) norm_prologue(g, X, ncols, xn, nc0);
+        MI_STAMP(g.stamps, 2);  // (norm prologue: slot 2 = wave 0's norm done, instead of the barrier below)
         __syncthreads();
         Xq = (const char *) xn;
         xcolq = (size_t) K * sizeof(float);
     }
     {
-        for (int p0 = wave; p0 < total; p0 += 16) {
+        for (int p0 = p_first; p0 < total; p0 += 16) {
             float4 v[4];
-            if (!PRO && p0 == wave) {
+            if (!PRO && p0 == p_first) {
 #pragma unroll
                 for (int u = 0; u < 4; u++) v[u] = xfirst[u];
             } else {
                 load_round(v, Xq, xcolq, p0);
             }
+            if constexpr (R16) {
+                const int p = min(p0 + (lane >> 4), total - 1);
+                const int c = p / nsl, sl = p - c * nsl;
+                quantize_row16(v, lane, act, K, c, sl, p0 + (lane >> 4) < total);
+            } else {
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int p = p0 + 4 * u;
-                if (p < total) {
-                    const int c = p / nsl, sl = p - c * nsl;
-                    quantize_slice<F::QKA>(v[u], lane, act, K, c, sl);
+                for (int u = 0; u < 4; u++) {
+                    const int p = p0 + 4 * u;
+                    if (p < total) {
+                        const int c = p / nsl, sl = p - c * nsl;
+                        quantize_slice<F::QKA>(v[u], lane, act, K, c, sl);
+                    }
                 }
             }
         }
@@ -640,7 +761,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
         for (int u = 0; u < PD; u++) prefetch(ring[u], u < klast ? u : klast);
     }
     __syncthreads();
-    MI_STAMP(g.stamps, 2);  // every wave's
+    if (!(PRO && g.pro.mode)) MI_STAMP(g.stamps, 2);  // every wave's
 
     // 3) stream: ring slot u holds row k0+u; refill it with row k0+u+PD right before using it
     //    (the last row again past the end: an L2 hit)
@@ -686,7 +807,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                         }
                     }
                     const float v = F::finish(A, M);
-                    if (ll == 0 && cl < ncols) store_out<PRO>(g, dst, cl, row, v);
+                    if (ll == 0 && cl < ncols) store_out<PRO, NC>(g, dst, cl, row, v, &epre);
                     continue;
                 }
                 // whole rows in the scratch: R rows' lane sums are collected, then one chain pass
@@ -708,13 +829,15 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                 }
                 if (slot == R - 1 || k == nrows - 1) {  // wave-uniform
                     sync();
+                    if (k == nrows - 1) MI_STAMP(g.stamps, 3);  // (reference order) the last rows' lane sums in the scratch
                     const int r = lane / (8 * NC), cl = (lane >> 3) % NC, ll = lane & 7;
                     const bool mine = r <= slot && cl < ncols;
                     float A = 0.0f, M = 0.0f;
                     if (mine && !g.abl) F::chain(scr + (r * NC + cl) * cs, ll, nitems, S, A, M);
                     const float v = F::finish(A, M);
+                    if (k == nrows - 1) MI_STAMP(g.stamps, 4);  // (reference order) chains done
                     if (ll == 0 && mine) {
-                        store_out<PRO>(g, dst, cl, row_begin + 4 * (k - slot + r) + wave, v);
+                        store_out<PRO, NC>(g, dst, cl, row_begin + 4 * (k - slot + r) + wave, v, &epre);
                     }
                     sync();
                 }
@@ -741,11 +864,12 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 const float v = mi_wave_sum_u(acc[c]);
-                if (lane == 0 && c < ncols) store_out<PRO>(g, dst, c, row, v);
+                if (lane == 0 && c < ncols) store_out<PRO, NC>(g, dst, c, row, v, &epre);
             }
             if (k == 0) MI_STAMP(g.stamps, 3);  // first row reduced and stored
         }
     }
+    MI_STAMP_CLK(g.stamps, 5);
     MI_STAMP(g.stamps, 7);
 }
 

@@ -264,6 +264,7 @@ _SIGS = {
     "gpt2_decode_batch": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int], c_int),
     "gpt2_kv_cache_seq_cp": ([c_void_p, c_int32, c_int32, c_int32, c_int32], None),
     "gpt2_kv_cache_clear": ([c_void_p], None),
+    "gpt2_batch_stats": ([c_void_p, c_void_p], None),
 }
 
 BACKEND_EXPORTS = [k for k in _SIGS if k.startswith("ggml_backend_mi355x") or k == "ggml_backend_is_mi355x"]

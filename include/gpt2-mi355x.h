@@ -75,6 +75,9 @@ GGML_API int gpt2_decode_batch(struct gpt2_model * model, int n_tokens, const in
                                const int32_t * seq_id, float * logits, int all_logits);
 GGML_API void gpt2_kv_cache_seq_cp(struct gpt2_model * model, int32_t seq_src, int32_t seq_dst, int32_t p0, int32_t p1);
 GGML_API void gpt2_kv_cache_clear(struct gpt2_model * model);
+// batched steps launched as a graph plan prebuilt during the previous step ([0]) and built on the
+// spot ([1]); with a host buffer type (gpt2_model_load_ex) a step's inputs go in as one async copy
+GGML_API void gpt2_batch_stats(const struct gpt2_model * model, int64_t * out2);
 // the host staging of the logits (gpt2_model_load_ex with a host buffer type), or NULL
 GGML_API const float * gpt2_logits_host(const struct gpt2_model * model);
 

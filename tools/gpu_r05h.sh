@@ -1,0 +1,9 @@
+#!/bin/bash
+set -eo pipefail
+OUT=gpurun_out/${1:-r05h}
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpt2.py tests/test_mul_mat_gpu.py -k "batched or f16 or float" > "$OUT/pytest.txt" 2>&1
+tail -2 "$OUT/pytest.txt"
+timeout -k 10 300 python3 -u bench.py --no-cpu --no-sweep --steps 20 > "$OUT/bench.json" 2> "$OUT/bench.err"
+python3 -c "import json; d=json.load(open('$OUT/bench.json')); print(d['value'], d['roofline']['frac'], d['gpt2']['ms_per_decode_token'], d['gpt2_q4_k']['ms_per_decode_token']); print(json.dumps(d['gpt2_batched']))"

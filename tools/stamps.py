@@ -60,8 +60,11 @@ def report(launches, title):
         tot_span += span
         tot_gap += gap
         wg = (t7 - t0) * TICK_US
-        ph = " ".join(f"{a}->{b}:{phase(st, a, b):.2f}" for a, b in ((0, 1), (1, 2), (2, 3), (0, 3), (3, 7), (1, 4), (4, 7))
-                      if not np.isnan(phase(st, a, b)))
+        ph = " ".join(f"{a}->{b}:{phase(st, a, b):.2f}" for a, b in ((0, 1), (1, 2), (0, 2), (2, 1), (2, 3), (0, 3), (3, 7), (1, 4), (4, 7))
+                      if not np.isnan(phase(st, a, b)) and 0 <= phase(st, a, b) < 1e4)
+        m = (st[:, 5] > st[:, 6]) & (st[:, 7] > st[:, 0]) & (st[:, 6] > 0)
+        if m.any():  # shader clock: memtime ticks / realtime ticks x 100 MHz
+            ph += f" clk:{np.median((st[m, 5] - st[m, 6]) / (st[m, 7] - st[m, 0])) * 100:.0f}MHz"
         print(f"{name:18s} {nb:5d} {gap:6.2f} {span:6.2f} {(t0.max() - t0.min()) * TICK_US:6.2f} {np.median(wg):6.2f} {wg.max():6.2f}  {ph}")
     print(f"launches {len(launches)}: sum of spans {tot_span:.1f} us, sum of gaps {tot_gap:.1f} us, "
           f"first entry -> last exit {(launches[-1][2][:, 7].max() - launches[0][2][:, 0].min()) * TICK_US:.1f} us")
