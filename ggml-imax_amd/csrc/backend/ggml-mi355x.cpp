@@ -96,6 +96,7 @@ static bool buffer_is_mi355x(ggml_backend_buffer_t buffer) {
 static void mi_buffer_free(ggml_backend_buffer_t buffer) {
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     mi_device_guard g(ctx->device);
+    mi_planes_drop(ctx->dev_ptr, buffer->size);
     MI_CHECK(hipFree(ctx->dev_ptr));
     delete ctx;
 }
@@ -107,6 +108,7 @@ static void mi_buffer_set_tensor(ggml_backend_buffer_t buffer, ggml_tensor * ten
     mi_device_guard g(ctx->device);
     // null stream: ordered after any queued work on the (blocking) backend streams
     MI_CHECK(hipMemcpyAsync((char *) tensor->data + offset, data, size, hipMemcpyHostToDevice, nullptr));
+    mi_planes_refresh((char *) tensor->data + offset, size, nullptr);  // repacked planes over these bytes
     MI_CHECK(hipStreamSynchronize(nullptr));
 }
 
@@ -128,6 +130,7 @@ static bool mi_buffer_cpy_tensor(ggml_backend_buffer_t buffer, const ggml_tensor
     } else {
         MI_CHECK(hipMemcpyPeerAsync(dst->data, dctx->device, src->data, sctx->device, ggml_nbytes(src), nullptr));
     }
+    mi_planes_refresh(dst->data, ggml_nbytes(src), nullptr);
     MI_CHECK(hipStreamSynchronize(nullptr));
     return true;
 }
@@ -136,6 +139,8 @@ static void mi_buffer_clear(ggml_backend_buffer_t buffer, uint8_t value) {
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     mi_device_guard g(ctx->device);
     MI_CHECK(hipMemset(ctx->dev_ptr, value, buffer->size));
+    mi_planes_refresh(ctx->dev_ptr, buffer->size, nullptr);
+    MI_CHECK(hipStreamSynchronize(nullptr));
 }
 
 static const ggml_backend_buffer_i k_mi_buffer_i = {
@@ -699,6 +704,8 @@ static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, in
 static void invalidate_activations(mi_backend_ctx * ctx, const ggml_tensor * written) {
     const char * lo = (const char *) written->data;
     const char * hi = lo + ggml_nbytes(written);
+    // a node writing into weight memory (through a view) renews the repacked planes over it
+    if (written->view_src && mi_planes_count() > 0) mi_planes_refresh(lo, (size_t) (hi - lo), ctx->stream);
     auto & c = ctx->act_cache;
     c.erase(std::remove_if(c.begin(), c.end(), [&](const mi_act_cache_entry & e) {
                 const char * elo = (const char *) e.data;
@@ -731,6 +738,15 @@ static int mm_act_kind(const mi_mm_desc & m, const ggml_tensor * src1) {
     // timing; the low bits are mmq_exact.hip's own kernel variants)
     if (kind <= 1 && (g_mi_tuning.mmq_variant & (1 << 30)) == 0 && mi_mmqx_supported(m.type, m.K, m.nb1, ncols, m.nb01)) return kind == 1 ? 8 : 9;
     return (kind == 2 ? 2 : kind + 3) + (mi_mmq_wants_blocked() ? 3 : 0);
+}
+
+// the repacked MFMA planes of the long Q4_K / Q5_K prompts' weights (before any capture: creating
+// them allocates); only graph leaves (weights), never a tensor a node of the graph writes
+static const char * planes_of(mi_backend_ctx * ctx, const ggml_tensor * a, const ggml_tensor * b) {
+    if (!g_mi_tuning.planes || (a->type != GGML_TYPE_Q4_K && a->type != GGML_TYPE_Q5_K) || a->op != GGML_OP_NONE || a->ne[2] != 1 ||
+        a->ne[3] != 1 || b->ne[1] * b->ne[2] * b->ne[3] < kMiPlanesMinCols || is_split_tensor(a))
+        return nullptr;
+    return mi_planes_get(a->type, a->data, a->nb[1], a->ne[0], a->ne[1], ctx->stream);
 }
 
 // The mul_mat of (src0, src1) with src0's rows taken from (W, N) and the output written at out
@@ -781,7 +797,7 @@ static void mul_mat_run(mi_backend_ctx * ctx, const ggml_tensor * src0, const vo
         if (xkind == 8 || xkind == 9) {
             // Q4_K / Q5_K / Q4_0 / Q8_0: the exact-integer int8 MFMA GEMMs (mmq_exact.hip)
             const mi_act_mmx act = xkind == 8 ? mi_act_mmx_carve(xa, m.K, ncols) : mi_act_mmx0_carve(xa, m.K, ncols);
-            mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, act, m.dst, m.nb1, ctx->stream);
+            mi_mul_mat_mmqx(m.type, m.W, m.nb01, m.K, m.N, act, m.dst, m.nb1, ctx->stream, W == src0->data && N == src0->ne[1] ? planes_of(ctx, src0, src1) : nullptr);
         } else if (xkind == 5 && m.type == GGML_TYPE_F16 && mi_mmf16p_supported(m.K, m.N, m.nb01, ncols, m.nb1)) {
             // F16 weights, a short prompt: 32 x 32 tiles with the K split over each tile's 4 waves
             mi_mul_mat_f16p(m.W, m.nb01, m.K, m.N, (const uint16_t *) xa, ncols, m.dst, m.nb1, ctx->stream);
@@ -1125,6 +1141,7 @@ static void rope_tables_prepare(mi_backend_ctx * ctx, const ggml_cgraph * cgraph
     for (int i = 0; i < cgraph->n_nodes; i++) {
         const ggml_tensor * n = cgraph->nodes[i];
         if (n->op == GGML_OP_ROPE && n->src[0] && n->src[0]->type == GGML_TYPE_F32) rope_table_ensure(ctx, n);
+        if (n->op == GGML_OP_MUL_MAT) (void) planes_of(ctx, n->src[0], n->src[1]);
     }
 }
 
@@ -1695,8 +1712,13 @@ static void plan_attention(const ggml_cgraph * g, const mi_uses & u, std::vector
         const ggml_tensor * vsrc = vt->src[0];
         if (!vsrc || vsrc->type != GGML_TYPE_F32 || !ggml_are_same_shape(vsrc, vt)) MI_ATTN_SKIP("check 2")
         if (sm->op != GGML_OP_SOFT_MAX || sm->src[1] || op_param_f(sm, 1) != 0.0f || u.of(sm) != 1) MI_ATTN_SKIP("check 3")
+        // the causal mask: diag_mask_inf(scale(KQ)) (single-sequence graphs), or scale(KQ) + mask with an
+        // F32 [n_kv, N] mask tensor broadcast over heads (batched decode across sequences)
         const ggml_tensor * dm = sm->src[0];
-        if (dm->op != GGML_OP_DIAG_MASK_INF || u.of(dm) != 1) MI_ATTN_SKIP("check 4")
+        const ggml_tensor * mask = nullptr;
+        if (dm->op == GGML_OP_ADD && dm->type == GGML_TYPE_F32 && dm->src[1] && dm->src[1]->type == GGML_TYPE_F32) mask = dm->src[1];
+        else if (dm->op != GGML_OP_DIAG_MASK_INF) MI_ATTN_SKIP("check 4")
+        if (u.of(dm) != 1) MI_ATTN_SKIP("check 4")
         const ggml_tensor * sc = dm->src[0];
         if (sc->op != GGML_OP_SCALE || u.of(sc) != 1) MI_ATTN_SKIP("check 5")
         const ggml_tensor * kq = sc->src[0];
@@ -1746,7 +1768,15 @@ static void plan_attention(const ggml_cgraph * g, const mi_uses & u, std::vector
         }
         if (!ok) MI_ATTN_SKIP("check 14")
         d.out = (char *) M->data;
-        d.n_past = ((const int32_t *) dm->op_params)[0];
+        if (mask) {
+            if (mask->ne[0] != d.n_kv || mask->ne[1] != d.N || mask->ne[2] != 1 || mask->ne[3] != 1 ||
+                mask->nb[0] != sizeof(float) || !mask->data || mask == sc) MI_ATTN_SKIP("check 4m")
+            d.mask = (const char *) mask->data;
+            d.mask_nb1 = mask->nb[1];
+            d.n_past = INT32_MAX / 2;  // never: the mask carries the causal structure
+        } else {
+            d.n_past = ((const int32_t *) dm->op_params)[0];
+        }
         d.pre_scale = op_param_f(sc, 0);
         d.sm_scale = op_param_f(sm, 0);
         const int absorbed_ids[] = {node_index(g, vt, idx), node_index(g, qc, idx), node_index(g, kq, idx), node_index(g, sc, idx),
@@ -1801,6 +1831,11 @@ static void plan_attention(const ggml_cgraph * g, const mi_uses & u, std::vector
         if (pl.q_copy_at < 0) {
             strided_range(d.q, qne, d.q_nb, 3, &lo, &hi);
             if (clobbered(node_index(g, qc, idx), lo, hi)) MI_ATTN_SKIP("check 20")
+        }
+        if (mask) {  // read at KQV instead of at the ADD; also must not overlap the merged output
+            const char * mlo2 = (const char *) mask->data;
+            const char * mhi2 = mlo2 + ggml_nbytes(mask);
+            if (clobbered(node_index(g, dm, idx), mlo2, mhi2) || (mlo2 < mhi && mlo < mhi2)) MI_ATTN_SKIP("check 21")
         }
         for (int a : absorbed_ids) absorbed_nodes[a] = 1;
         plans.push_back(pl);
@@ -1974,7 +2009,7 @@ static int run_prefill_group(mi_backend_ctx * ctx, ggml_cgraph * g, int i) {
     for (size_t k = 0; k < members.size(); k++) {
         const ggml_tensor * n = members[k];
         const mi_act_mmx act = kind == 8 ? mi_act_mmx_carve(xa[k], K, ncols) : mi_act_mmx0_carve(xa[k], K, ncols);
-        gg.m[k] = mi_mmx_member{n->src[0]->data, n->src[0]->nb[1], n->src[0]->ne[1], act, (float *) n->data, n->nb[1], 0};
+        gg.m[k] = mi_mmx_member{n->src[0]->data, n->src[0]->nb[1], n->src[0]->ne[1], act, (float *) n->data, n->nb[1], 0, planes_of(ctx, n->src[0], n->src[1])};
     }
     mi_mul_mat_mmqx_group(gg, ctx->stream);
     ctx->last_launches++;
@@ -2049,7 +2084,9 @@ static bool graphs_enabled(const mi_backend_ctx * ctx) {
 
 // ---- per-node timer ----------------------------------------------------------------------------
 // A dispatch unit is one pass of mi_graph_launch_nodes' loop: a node, or a fused chain of nodes
-// run by one kernel. perf_mark records an event before each unit; perf_finish records the end,
+// run by one kernel. perf_mark records an event before each unit (after the store of partial sums
+// an earlier unit deferred, which stays in that unit's time; nodes absorbed into another node's
+// kernel get no mark); perf_finish records the end,
 // waits for the stream and adds each unit's device time to the perf fields of its last node (the
 // other nodes of a fused chain get a run with no time, as the reference's fused-away work would),
 // and the whole graph's to the cgraph's (ggml.c:19907-19922). ggml_graph_print shows them.
@@ -2079,12 +2116,16 @@ static void perf_finish(mi_backend_ctx * ctx, ggml_cgraph * g, int64_t t_host0) 
         float ms = 0.0f;
         MI_CHECK(hipEventElapsedTime(&ms, ctx->perf_ev[k], ctx->perf_ev[k + 1]));
         const int lo = ctx->perf_at[k], hi = ctx->perf_at[k + 1];
-        int last = -1;
+        // the time goes to the unit's last node that is not executed inside another node's kernel
+        // (absorbed nodes between two units ran in an earlier unit's kernel: a run, no time)
+        int last = -1, last_any = -1;
         for (int j = lo; j < hi; j++) {
             if (is_noop(g->nodes[j])) continue;
             g->nodes[j]->perf_runs++;
-            last = j;
+            last_any = j;
+            if (!absorbed(j)) last = j;
         }
+        if (last < 0) last = last_any;
         if (last >= 0) {
             const int64_t us = (int64_t) llround(ms * 1000.0);
             g->nodes[last]->perf_time_us += us;
@@ -2502,10 +2543,10 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
     ctx->perf_at.clear();
     for (int i = 0; i < cgraph->n_nodes; i++) {
         ggml_tensor * node = cgraph->nodes[i];
-        if (perf && !is_noop(node)) perf_mark(ctx, i);
         if (absorbed(i) && q_copy_bytes) {
             for (const auto & pl : attn) {
                 if (pl.q_copy_at != i) continue;
+                if (perf) perf_mark(ctx, i);  // the Q copy: a unit of its own
                 mi_tensor_desc dq = pl.q_src;
                 dq.data = (char *) pl.d.q;
                 for (int k = 0; k < 3; k++) dq.nb[k] = pl.d.q_nb[k];
@@ -2518,8 +2559,9 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
             // a value held as partial sums is stored before any node but its norm consumer runs
             const bool consumer = !no_node_fusion && (fuse_mask & 1) && (node->op == GGML_OP_NORM || node->op == GGML_OP_RMS_NORM) &&
                                   node->src[0] == ctx->pend.out;
-            if (!consumer) flush_pending(ctx);
+            if (!consumer) flush_pending(ctx);  // (still timed with the unit that deferred it)
         }
+        if (perf) perf_mark(ctx, i);
         if (next_attn < attn.size() && attn[next_attn].kqv == i) {
             const int lastp = (fuse_mask & 128) ? try_fuse_attn_proj(ctx, cgraph, i, attn[next_attn], uses) : -1;
             if (lastp < 0) {
@@ -2584,13 +2626,14 @@ static enum ggml_status mi_graph_launch_nodes(mi_backend_ctx * ctx, ggml_cgraph 
         invalidate_activations(ctx, node);
     }
     flush_pending(ctx);
-    tl_absorbed = nullptr;
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
+        tl_absorbed = nullptr;
         fprintf(stderr, "%s: kernel launch failed: %s\n", __func__, hipGetErrorString(err));
         return GGML_STATUS_FAILED;
     }
     if (perf) perf_finish(ctx, cgraph, perf_t0);
+    tl_absorbed = nullptr;
     return GGML_STATUS_SUCCESS;
 }
 
@@ -2884,11 +2927,15 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         return true;
     }
     if (strcmp(name, "mmq_variant") == 0) {
+        // the opt-in forms measured slower than the defaults (k_mmqp weight ring 4 2^19, k_mmqp
+        // 64-column tiles 2^26; the k_mmf16p f32 fold behind 2^17) are compiled into diagnostic builds only
+        if (!mi_diag_build() && (value & kMiMmqDiagBits)) return false;
         g_mi_tuning.mmq_variant = value;
         return true;
     }
-    if (strcmp(name, "mmq_long") == 0 && ((value >= 0 && value <= 2) || (mi_diag_build() && value >= 16 && value <= 23))) {
-        // 0 auto, 1 k_mmqw, 2 k_mmqt; 16-23 k_mmqt stamps / ablations (diagnostic builds only)
+    if (strcmp(name, "mmq_long") == 0 && (value == 0 || value == 2 || (mi_diag_build() && (value == 1 || (value >= 16 && value <= 24))))) {
+        // 0 auto, 2 k_mmqt; diagnostic builds: 1 k_mmqw for Q4_K, 16-23 k_mmqt stamps / ablations,
+        // 24 k_mmqr per-step stamps
         g_mi_tuning.mmq_long = value;
         return true;
     }
@@ -2902,6 +2949,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "xfirst") == 0 && value >= -1 && value <= 1) {
         g_mi_tuning.xfirst = value;
+        return true;
+    }
+    if (strcmp(name, "planes") == 0 && value >= 0 && value <= 1) {
+        g_mi_tuning.planes = value;
         return true;
     }
     if (strcmp(name, "f16_waves") == 0 && value >= 0) {
@@ -2927,6 +2978,11 @@ bool ggml_backend_mi355x_stamps_enable(size_t slots) { return mi_stamps_enable(s
 void ggml_backend_mi355x_stamps_reset(void) { mi_stamps_reset(); }
 size_t ggml_backend_mi355x_stamps_read(uint64_t * words, size_t n, char * log, size_t log_size) {
     return mi_stamps_read(words, n, log, log_size);
+}
+
+size_t ggml_backend_mi355x_planes_stats(size_t * bytes) {
+    if (bytes) *bytes = mi_planes_bytes();
+    return mi_planes_count();
 }
 
 bool ggml_backend_mi355x_quantize_activations(ggml_backend_t backend, int vec_dot_type, const float * x, int64_t K,

@@ -69,6 +69,7 @@ __device__ __forceinline__ float attn_head(const mi_attn_desc & a, int h, int t,
 
     // ---- pass 1: scores and their max
     const int lim = a.n_past + t;  // keys k > lim are masked (diag_mask_inf)
+    const float * mrow = a.mask ? (const float *) (a.mask + (size_t) t * a.mask_nb1) : nullptr;
     float mx = -INFINITY;
     for (int c0 = 0; c0 < n_kv; c0 += CH) {
         if (c0) load_rows(kb, a.k_nb[1], c0, kr);
@@ -79,6 +80,7 @@ __device__ __forceinline__ float attn_head(const mi_attn_desc & a, int h, int t,
             d = group_sum<LPK>(d);
             const int key = c0 + kk * G + grp;
             float w = d * a.pre_scale;
+            if (mrow) w = w + mrow[min(key, n_kv - 1)];
             if (key >= a.n_past && key > lim) w = -INFINITY;
             w = w * a.sm_scale;
             if (key < n_kv) {

@@ -135,6 +135,7 @@ struct mi_tuning {
     int f16_ps_waves; // k_gemv_f16_ps (GEMV over summed partials): waves per workgroup, 2 / 4 / 8 (0 = automatic)
     int mmq_long;     // Q4_K / Q5_K prefill past 128 columns: 0 = automatic (Q4_K k_mmqt, Q5_K k_mmqw), 1 = k_mmqw, 2 = k_mmqt; 16-23 k_mmqt stamps (diagnostic builds)
     int xfirst;       // lone decode GEMVs: activation loads issued and landed before the weight loads: 1 always, 0 never, -1 auto (quantized, K >= 2048)
+    int planes;       // long Q4_K prompts on repacked MFMA planes (mmq_planes.hip k_mmqr): 1 on, 0 off (default: slower than k_mmqt with HBM-streamed weights)
 };
 extern mi_tuning g_mi_tuning;
 // the order of the graph being launched when mmv_order is -1 (set by the backend per graph)
@@ -211,6 +212,7 @@ struct mi_mmx_member {
     float * dst;
     size_t ycol;
     int64_t tile_begin;  // set by the launcher
+    const char * planes;  // Q4_K / Q5_K: the weights' repacked MFMA planes (mi_planes_get) or null
 };
 struct mi_mmx_group {
     int type = 0;
@@ -221,7 +223,25 @@ struct mi_mmx_group {
 void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s);
 // one member
 void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N, const mi_act_mmx & act, float * dst,
-                     size_t ycol, hipStream_t s);
+                     size_t ycol, hipStream_t s, const char * planes = nullptr);
+// Repacked MFMA planes of Q4_K / Q5_K weights for long prompts (mmq_planes.hip): per 32-row tile
+// and superblock the int8 planes q * (sc_j bit field) in v_mfma_i32_32x32x32_i8 operand order, the
+// U operand [m_j, 64 m_j] and (d, dmin) -- a device-side copy kept next to the canonical blocks,
+// which stay untouched (get_tensor, views, GET_ROWS, cpy see the reference bytes). mi_planes_get
+// returns the planes of W (creating them with one repack launch on s when missing and s is not
+// capturing), or null (disabled: GGML_MI355X_PLANES=0, unsupported shape, capture). Any write to
+// weight memory must be followed by mi_planes_refresh over the written bytes (a repack launch on
+// s for every overlapping entry; capturable); freeing the memory by mi_planes_drop.
+// mmq_variant bits of opt-in kernel forms measured slower than the defaults: diagnostic builds only
+constexpr int kMiMmqDiagBits = (1 << 19) | (1 << 26);  // (bit 2^17 doubles as k_mmqx's full-width bit)
+constexpr int64_t kMiPlanesMinCols = 129;  // prompts of more columns take the planes kernel
+const char * mi_planes_get(int type, const void * W, size_t nb01, int64_t K, int64_t N, hipStream_t s);
+void mi_planes_refresh(const void * lo, size_t bytes, hipStream_t s);
+void mi_planes_drop(const void * lo, size_t bytes);
+size_t mi_planes_count();
+size_t mi_planes_bytes();
+// the planes kernel over a group whose members all carry planes (false: not applicable)
+bool mi_mul_mat_mmqr_group(mi_mmx_group & g, hipStream_t s);
 
 // ---- companion ops (ops.hip) ----
 // a tensor view as the element-wise kernels see it: f32 (type 0), f16 (1) or i32 (26) elements
@@ -313,6 +333,8 @@ struct mi_attn_desc {
     int n_past;             // diag_mask_inf n_past
     float pre_scale;        // ggml_scale factor
     float sm_scale;         // soft_max scale (op_params[0])
+    const char * mask = nullptr;  // ADD(scale(KQ), mask) form: F32 mask [n_kv, N] added after the
+    size_t mask_nb1 = 0;          // pre-scale (n_past then disables the causal mask)
 };
 bool mi_attn_supported(int D, int n_kv);
 // mmv_order 1 (or attn_variant 1): the reference's summation order, bit-identical; otherwise the

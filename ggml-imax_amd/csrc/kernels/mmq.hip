@@ -595,15 +595,20 @@ bool mi_mmf16p_f32_supported(int64_t K, int64_t N, size_t nb01, int64_t ncols, s
     // opt-in (variant bit 2^17): measured SLOWER than the separate conversion launch + k_mmf16p
     // (profiles/r04c_pf_f16.txt, 16 rotated weights: B=64 23.3 vs 17.3 us, B=32 22.9 vs 17.2 us) --
     // every row tile re-reads and re-converts its columns' f32 (twice the bytes of f16, 128 row tiles)
-    return mi_mmf16p_supported(K, N, nb01, ncols, ycol) && ((uintptr_t) x % 16) == 0 && xnb1 % 16 == 0 &&
+    // (diagnostic builds only)
+    return MI_DIAG && mi_mmf16p_supported(K, N, nb01, ncols, ycol) && ((uintptr_t) x % 16) == 0 && xnb1 % 16 == 0 &&
            (g_mi_tuning.mmq_variant & (1 << 17)) != 0;
 }
 
 void mi_mul_mat_f16p_f32(const void * W, size_t nb01, int64_t K, int64_t N, const float * x, size_t xnb1, int64_t ncols, float * dst,
                          size_t ycol, hipStream_t s) {
+#if MI_DIAG
     const int64_t tiles = ((N + 31) / 32) * ((ncols + 31) / 32);
     hipLaunchKernelGGL((k_mmf16p<2, 4, true>), dim3((unsigned) tiles), dim3(256), 0, s, (const uint8_t *) W, nb01, K, N, nullptr, ncols,
                        dst, ycol, x, (int64_t) (xnb1 / sizeof(float)));
+#else
+    (void) W; (void) nb01; (void) K; (void) N; (void) x; (void) xnb1; (void) ncols; (void) dst; (void) ycol; (void) s;
+#endif
 }
 
 bool mi_mmq_wants_blocked() { return (g_mi_tuning.mmq_variant & 1) == 0; }

@@ -365,16 +365,18 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
     MI_STAMP(e.stamps, 7);
 }
 
-// Tall matrices (lm_head, N = 50257): one column, rows in one register pass (K <= 128 U). A
-// fixed grid of 4-wave workgroups (~8 waves per CU) stages / normalizes the column once per
-// workgroup, then every wave walks its row groups (4 rows) grid-stride, the next group's weights
-// requested before the current group is reduced: the weight stream keeps two row groups per wave
-// in flight instead of paying one launch-wide latency round per row group.
-template <int EPI, int U, int JM>
+// Tall matrices (lm_head, N = 50257): 1..8 columns (NC, padded), rows in one register pass (K <= 128 U).
+// A fixed grid of 4-wave workgroups (~8 waves per CU) stages / normalizes the columns once per
+// workgroup (wave w the columns w, w + 4: the columns' norms run in parallel), then every wave walks
+// its row groups (4 rows) grid-stride, the next group's weights requested before the current group
+// is reduced: the weight stream keeps two row groups per wave in flight instead of paying one
+// launch-wide latency round per row group. (A per-row-group grid would stage the columns once per
+// 4 rows: 12565 workgroups each normalizing every column for lm_head -- 66 us at 8 columns.)
+template <int EPI, int U, int JM, int NC>
 __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
-                                                       mi_src_cols x, float * __restrict__ dst, mi_f16_epilogue e,
-                                                       mi_norm_prologue pro, int64_t kp) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [kp] f16
+                                                       mi_src_cols x, int ncols, float * __restrict__ dst, size_t ycol,
+                                                       mi_f16_epilogue e, mi_norm_prologue pro, int64_t kp) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [NC][kp] f16
     MI_STAMP(e.stamps, 0);
     MI_STAMP_CLK(e.stamps, 6);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -398,19 +400,39 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
     };
 
     constexpr bool GB = JM > 0 && JM <= 4;
+    const int nc = ncols < NC ? ncols : NC;
     float4 pv[JM > 0 ? JM : 1], pg[GB ? JM : 1], pb[GB ? JM : 1];
     ColStager<4> st;
-    if constexpr (JM > 0) norm_load<JM, GB>((const float *) x.base, K, lane, pro, pv, pg, pb);
-    else st.load((const float *) x.base, K, 0);
+    if constexpr (JM > 0) norm_load<JM, GB>((const float *) (x.base + (size_t) (wid < nc ? wid : 0) * x.nb1), K, lane, pro, pv, pg, pb);
+    else if (NC == 1) st.load((const float *) x.base, K, 0);
     if (e.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint4 cur[U];
     float eb = 0.0f;
     load_group(cur, eb, grp);
     if constexpr (JM > 0) {
-        if (wid == 0) norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs, lane);
-    } else {
+        // wave w normalizes columns w, w + 4 (the second one's x requested before the first's store)
+        if (wid < nc) {
+            if (NC > 4 && wid + 4 < nc) {
+                float4 nv[JM];
+                const float * xc2 = (const float *) (x.base + (size_t) (wid + 4) * x.nb1);
+#pragma unroll
+                for (int j = 0; j < JM; j++) {
+                    const int64_t k = (int64_t) j * 256 + lane * 4;
+                    const bool in = k < K;
+                    const float4 vv = *(const float4 *) (xc2 + (in ? k : K - 4));
+                    nv[j] = in ? vv : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) wid * kp, lane);
+                norm_store<JM, GB>(nv, pg, pb, K, kp, pro, xs + (size_t) (wid + 4) * kp, lane);
+            } else {
+                norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) wid * kp, lane);
+            }
+        }
+    } else if (NC == 1) {
         st.store(xs, kp, 0);
         st.column((const float *) x.base, K, kp, xs, (int64_t) 4 * blockDim.x);
+    } else {
+        stage_cols<4>(x, 0, nc, K, kp, xs);
     }
     mi_lds_barrier();
     MI_STAMP(e.stamps, 2);
@@ -419,21 +441,33 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
         uint4 nxt[U];
         float ebn = 0.0f;
         load_group(nxt, ebn, grp + stride);
-        float acc = 0.0f;
+        float acc[NC];
 #pragma unroll
-        for (int u = 0; u < U; u++)
-            if (u < nit) acc = dot8(cur[u], *(const uint4 *) (xs + ((int64_t) u * kLpr + m) * kChunk), acc);
-        acc = row16_sum(acc);
+        for (int c = 0; c < NC; c++) acc[c] = 0.0f;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (u < nit) {
+#pragma unroll
+                for (int c = 0; c < NC; c++)
+                    if (c < nc) acc[c] = dot8(cur[u], *(const uint4 *) (xs + (size_t) c * kp + ((int64_t) u * kLpr + m) * kChunk), acc[c]);
+            }
+        }
+        float mine = 0.0f;  // lane m of the row holds column m
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const float t = row16_sum(acc[c]);
+            if (m == c) mine = t;
+        }
         const int64_t row = grp * 4 + rg;
-        if (m == 0 && row < N) {
-            float v = acc;
+        if (m < nc && row < N) {
+            float v = mine;
             if (EPI >= 1) v = v + eb;
             if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
-            dst[row] = v;
+            *(float *) ((char *) dst + (size_t) m * ycol + row * sizeof(float)) = v;
             // a CPY of the output rows (e.g. the logits into the caller's pinned host buffer: the
             // stores go out over PCIe while the GEMV runs, instead of a copy queued behind it)
             if (e.copy[0].ptr && row >= e.copy[0].row0 && row < e.copy[0].row1)
-                *(float *) (e.copy[0].ptr + (row - e.copy[0].row0) * sizeof(float)) = v;
+                *(float *) (e.copy[0].ptr + (size_t) m * e.copy[0].col_stride + (row - e.copy[0].row0) * sizeof(float)) = v;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) cur[u] = nxt[u];
@@ -623,26 +657,34 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
     // very tall matrices (lm_head): row groups share one staging of the activations per workgroup
     ks = std::min(ks, nit);
     if (pro.mode) ks = std::max(ks, (nit + 7) / 8);  // the prologue path runs one register pass
+    // several columns with the norm prologue: one column per wave where K allows (a lone wave
+    // normalizes its columns one after the other, ~0.9 us each: 8 columns 8.2 us of prologue)
+    if (pro.mode && nc > 1) ks = std::max(ks, std::min(nc, nit));
     const int per = (nit + ks - 1) / ks;  // steps per wave
     ks = (nit + per - 1) / per;
     const bool one = per <= 8;
     const int rgs = g_mi_tuning.f16_rgs > 0 ? std::max(1, std::min(g_mi_tuning.f16_rgs, 8 / ks)) : 1;
-    if (ncols == 1 && groups >= 4096 && K <= 1024 && !xh && !e.resid && !e.copy[1].ptr && g_mi_tuning.f16_rgs == 0 && !pro.parts) {
-        // tall matrix: grid-stride row groups (k_gemv_f16_tall)
-        const dim3 grid((unsigned) std::min<int64_t>((groups + 3) / 4, 512));
-        const size_t lds = (size_t) kp * sizeof(uint16_t);
+    if (groups / ((ncols + nc - 1) / nc) >= 4096 && K <= 1024 && !xh && !e.resid && !e.copy[1].ptr && g_mi_tuning.f16_rgs == 0 &&
+        !pro.parts && (ncols == 1 || ncols == nc)) {
+        // tall matrix: grid-stride row groups (k_gemv_f16_tall), 1..8 columns in one launch
+        const int64_t rgroups = (N + 3) / 4;
+        const dim3 grid((unsigned) std::min<int64_t>((rgroups + 3) / 4, 512));
+        const size_t lds = (size_t) nc * kp * sizeof(uint16_t);
         const int epi = e.gelu_table ? 3 : (e.bias ? 1 : 0);
         const uint8_t * w = (const uint8_t *) W;
         mi_f16_epilogue es = e;
         es.stamps = mi_stamp_take("k_gemv_f16_tall", grid.x);
         es.xfirst = g_mi_tuning.xfirst == 1;  // (off by default: GPT-2 decode 304 -> 316 us per token with it)
-#define MI_GEMV_TALL(EP, JMV) hipLaunchKernelGGL((k_gemv_f16_tall<EP, 8, JMV>), grid, dim3(256), lds, s, w, nb01, K, N, x, dst, es, pro, kp)
+#define MI_GEMV_TALL_N(EP, JMV, NCV) hipLaunchKernelGGL((k_gemv_f16_tall<EP, 8, JMV, NCV>), grid, dim3(256), lds, s, w, nb01, K, N, x, (int) ncols, dst, ycol, es, pro, kp)
+#define MI_GEMV_TALL(EP, JMV) do { switch (nc) { case 1: MI_GEMV_TALL_N(EP, JMV, 1); break; case 2: MI_GEMV_TALL_N(EP, JMV, 2); break; \
+                                                  case 4: MI_GEMV_TALL_N(EP, JMV, 4); break; default: MI_GEMV_TALL_N(EP, JMV, 8); break; } } while (0)
         if (pro.mode) {
             if (epi == 0) MI_GEMV_TALL(0, 4); else if (epi == 1) MI_GEMV_TALL(1, 4); else MI_GEMV_TALL(3, 4);
         } else {
             if (epi == 0) MI_GEMV_TALL(0, 0); else if (epi == 1) MI_GEMV_TALL(1, 0); else MI_GEMV_TALL(3, 0);
         }
 #undef MI_GEMV_TALL
+#undef MI_GEMV_TALL_N
         return;
     }
     if (pro.parts) {  // supported(): one column, K <= 1024, <= 16 parts

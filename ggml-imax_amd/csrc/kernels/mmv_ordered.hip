@@ -596,6 +596,7 @@ __global__ __launch_bounds__(kAttnThreads) void k_attn_ordered(mi_attn_desc a, c
                                           [&](int64_t i) { return qv[i]; }, a.D, q);
         if (q == 0 && k < a.n_kv) {
             float w = mul_rn(v, a.pre_scale);
+            if (a.mask) w = add_rn(w, *(const float *) (a.mask + (size_t) t * a.mask_nb1 + (size_t) k * 4));
             if (k >= a.n_past && k > a.n_past + t) w = -INFINITY;
             p[k] = mul_rn(w, a.sm_scale);
         }
@@ -740,6 +741,7 @@ __global__ __launch_bounds__(512) void k_attn_fast(mi_attn_desc a, const uint16_
         const float v = quad_reduce_avx(acc);
         if (q == 0 && k < n_kv) {
             float w = mul_rn(v, a.pre_scale);
+            if (a.mask) w = add_rn(w, *(const float *) (a.mask + (size_t) t * a.mask_nb1 + (size_t) k * 4));
             if (k >= a.n_past && k > a.n_past + t) w = -INFINITY;
             p[k] = mul_rn(w, a.sm_scale);
         }

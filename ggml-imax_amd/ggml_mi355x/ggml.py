@@ -244,6 +244,7 @@ _SIGS = {
     "ggml_backend_mi355x_stamps_enable": ([c_size_t], c_bool),
     "ggml_backend_mi355x_stamps_reset": ([], None),
     "ggml_backend_mi355x_stamps_read": ([c_void_p, c_size_t, c_char_p, c_size_t], c_size_t),
+    "ggml_backend_mi355x_planes_stats": ([c_void_p], c_size_t),
     "ggml_backend_mi355x_quantize_activations": ([c_void_p, c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p], c_bool),
     # GPT-2 driver (include/gpt2-mi355x.h)
     "gpt2_model_load": ([c_char_p, c_void_p, c_int, c_int], c_void_p),

@@ -99,6 +99,9 @@ GGML_API bool ggml_backend_mi355x_quantize_activations(ggml_backend_t backend, i
 GGML_API bool ggml_backend_mi355x_stamps_enable(size_t slots);
 GGML_API void ggml_backend_mi355x_stamps_reset(void);
 GGML_API size_t ggml_backend_mi355x_stamps_read(uint64_t * words, size_t n, char * log, size_t log_size);
+// Repacked MFMA planes of Q4_K / Q5_K weights kept for long prompts (no reference counterpart: the
+// reference's CPU mul_mat dequantizes per call): how many weight tensors carry them, and their bytes
+GGML_API size_t ggml_backend_mi355x_planes_stats(size_t * bytes);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,7 @@ SHA-256 of the whole Y plus every step-th column. Three checks:
   * prompt sharding (configs[4] on 8 GPUs, 64 columns each): the column shards computed alone
     concatenate to the unsharded result bit for bit.
 """
+import ctypes
 import hashlib
 
 import numpy as np
@@ -154,9 +155,11 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
         variants = [0, 16, 128, 128 | 65536, 128 | (1 << 24), 128 | (1 << 25)]
     else:
         variants = [0, 2048, 1 << 27, 128 | 131072, 128 | 65536, 128 | 131072 | (1 << 28)] + ([1 << 21] if B <= 16 else [])
-    # long-prompt kernels forced onto these shapes (variant bits 128 | 131072, mmq_long): k_mmqw (1),
-    # k_mmqt (2, K split over wave pairs, Q4_K)
+    # long-prompt kernels forced onto these shapes (variant bits 128 | 131072, mmq_long): k_mmqw (1,
+    # diagnostic builds only for Q4_K), k_mmqt (2, K split over wave pairs, Q4_K)
     longs = [(128 | 131072, L) for L in (1, 2)] if tname in ("q4_K", "q5_K") else []
+    if longs and not rt.ggml_backend_mi355x_set_tuning(b"mmq_long", 1):
+        longs = longs[1:]
     outs = {}
     try:
         for v in variants + longs:
@@ -176,17 +179,16 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
 
 @pytest.mark.parametrize("K,N,B", [(256, 64, 130), (1280, 96, 257), (3072, 200, 200), (11008, 256, 136), (4096, 4096, 512)])
 def test_split_k_prefill_bit_equal(rt, backend, K, N, B):
-    """k_mmqt (mmq_long 2, the Q4_K default past 128 columns: the two K halves of the canonical
-    order on two waves, met in LDS) forced onto
+    """k_mmqt (mmq_long 2, the Q4_K kernel past 128 columns without repacked planes: the two K
+    halves of the canonical order on two waves, met in LDS) forced onto
     ragged shapes: one superblock (empty high half), S = 5 (a one-superblock high half), S = 12,
     S = 43 (a high half shorter than the low: idle steps), ragged rows and columns; bit-identical to
-    the default kernel and within the exact-path tolerance of the oracle."""
+    the default kernel (k_mmqr on the planes) and within the exact-path tolerance of the oracle."""
     t = orc.Q4_K
     w = synth.uniform(K + 3 * N, K * N)
     x = synth.uniform(K + 5 * B, K * B)
     wq = orc.quantize(t, w, K)
     try:
-        assert rt.ggml_backend_mi355x_set_tuning(b"mmq_long", 1)  # k_mmqw / k_mmqx / k_mmqp as the shape picks
         base = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
         assert rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", 128 | 131072)
         assert rt.ggml_backend_mi355x_set_tuning(b"mmq_long", 2)
@@ -275,3 +277,90 @@ def test_long_prefill_into_host_memory(rt, backend, tname):
         cd.free()
     assert np.array_equal(host_y.view(np.uint32), dev_y.view(np.uint32)), rel_err(host_y, dev_y)
     assert rel_err(dev_y, orc.mul_mat(t, wq, K, N, x, B)) <= EXACT_TOL
+
+
+def _planes_stats(rt):
+    b = ctypes.c_size_t(0)
+    n = rt.ggml_backend_mi355x_planes_stats(ctypes.byref(b))
+    return int(n), int(b.value)
+
+
+@pytest.mark.parametrize("tname,K,N,B", [("q4_K", 256, 64, 130), ("q4_K", 1280, 96, 257), ("q4_K", 3072, 200, 200),
+                                         ("q4_K", 11008, 256, 136), ("q4_K", 4096, 4096, 512), ("q5_K", 1280, 96, 257),
+                                         ("q5_K", 4096, 1024, 512), ("q5_K", 2816, 130, 129)])
+def test_planes_prefill_bit_equal_canonical(rt, backend, tname, K, N, B):
+    """Long prompts (> 128 columns) on the repacked MFMA planes (mmq_planes.hip k_mmqr; Q4_K -- Q5_K
+    keeps the canonical kernels, the case checks the switch) against the
+    canonical kernels on the raw blocks (planes off: k_mmqt / k_mmqw): the same exact integer sums
+    and the same cfold combine, so bit-identical -- ragged rows (N % 64, N % 32), ragged columns,
+    one superblock (empty high half), odd superblock counts; and within the exact-path tolerance
+    of the oracle."""
+    t = orc.TYPES_BY_NAME[tname]
+    w = synth.uniform(K + 11 * N, K * N)
+    x = synth.uniform(K + 13 * B, K * B)
+    wq = orc.quantize(t, w, K)
+    base = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)  # (planes are opt-in: off by default)
+    n0, _ = _planes_stats(rt)
+    try:
+        assert rt.ggml_backend_mi355x_set_tuning(b"planes", 1)
+        y = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
+    finally:
+        rt.ggml_backend_mi355x_set_tuning(b"planes", 0)
+    assert _planes_stats(rt)[0] == n0, "planes of a freed buffer must be dropped with it"
+    assert np.array_equal(y.view(np.uint32), base.view(np.uint32)), rel_err(y, base)
+    if K * N * B <= 4096 * 1024 * 64:
+        assert rel_err(y, orc.mul_mat(t, wq, K, N, x, B)) <= EXACT_TOL
+
+
+@pytest.mark.parametrize("tname", ["q4_K"])
+def test_planes_follow_weight_writes(rt, backend, tname):
+    """The planes are a device-side copy next to the canonical blocks: set_tensor -> get_tensor
+    round-trips the reference bytes exactly (also after partial-offset writes), and a partial
+    rewrite of some rows (offset into the tensor) renews the planes, so the next long prompt sees
+    the new weights (compared with the oracle and with the canonical kernels)."""
+    t = orc.TYPES_BY_NAME[tname]
+    K, N, B = 2048, 192, 160
+    rb = orc.row_size(t, K)
+    wq = orc.quantize(t, synth.uniform(81, K * N), K)
+    wq2 = orc.quantize(t, synth.uniform(82, K * N), K)
+    x = synth.uniform(83, K * B)
+    ovh = rt.ggml_tensor_overhead() * 8 + rt.ggml_graph_overhead()
+    with G.Context(rt, ovh, no_alloc=True) as c:
+        w = rt.ggml_new_tensor_2d(c.ctx, t, K, N)
+        xt = rt.ggml_new_tensor_2d(c.ctx, G.GGML_TYPE_F32, K, B)
+        y = rt.ggml_mul_mat(c.ctx, w, xt)
+        g = rt.ggml_new_graph(c.ctx)
+        rt.ggml_build_forward_expand(g, y)
+        buf = rt.ggml_backend_alloc_ctx_tensors(c.ctx, backend)
+        assert buf
+        assert rt.ggml_backend_mi355x_set_tuning(b"planes", 1)
+        try:
+            n0, _ = _planes_stats(rt)
+            G.tensor_set(rt, w, wq)
+            G.tensor_set(rt, xt, x)
+            assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
+            n1, nbytes = _planes_stats(rt)
+            assert n1 == n0 + 1 and nbytes > 0, "the long prompt did not create the weight's planes"
+            y1 = G.tensor_get(rt, y)
+            assert rel_err(y1, orc.mul_mat(t, wq, K, N, x, B)) <= EXACT_TOL
+            back = np.empty_like(wq)
+            rt.ggml_backend_tensor_get(w, back.ctypes.data, 0, back.nbytes)
+            assert np.array_equal(back, wq), "get_tensor must return the canonical bytes"
+            # rows 37 .. 120 replaced, at an offset into the tensor (not row-tile aligned)
+            mixed = wq.copy()
+            lo, hi = 37 * rb, 121 * rb
+            mixed[lo:hi] = wq2[lo:hi]
+            G.tensor_set(rt, w, wq2[lo:hi], offset=lo)
+            rt.ggml_backend_tensor_get(w, back.ctypes.data, 0, back.nbytes)
+            assert np.array_equal(back, mixed)
+            assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
+            y2 = G.tensor_get(rt, y)
+            assert rel_err(y2, orc.mul_mat(t, mixed, K, N, x, B)) <= EXACT_TOL
+            assert rt.ggml_backend_mi355x_set_tuning(b"planes", 0)
+            assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
+            y3 = G.tensor_get(rt, y)
+            assert np.array_equal(y2.view(np.uint32), y3.view(np.uint32)), rel_err(y2, y3)
+        finally:
+            rt.ggml_backend_mi355x_set_tuning(b"planes", 0)
+            rt.ggml_backend_buffer_free(buf)
+    assert _planes_stats(rt)[0] == n0

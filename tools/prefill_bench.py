@@ -20,9 +20,13 @@ VARS = [(v, l) for v in VARS for l in LONGS]
 # PF_MMV_BLOCKS: decode GEMV grid targets to compare (0 = automatic)
 BLOCKS = [int(v) for v in os.environ.get("PF_MMV_BLOCKS", "0").split(",")]
 VARS = [(v, l, b) for (v, l) in VARS for b in BLOCKS]
+# PF_PLANES: repacked-planes settings to compare (Q4_K / Q5_K past 128 columns: 1 k_mmqr, 0 the canonical kernels)
+PLANES = [int(v) for v in os.environ.get("PF_PLANES", "1").split(",")]
+VARS = [(v, l, b, p) for (v, l, b) in VARS for p in PLANES]
 for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
     for B in Bs:
-      for var, lng, blk in VARS:
+      for var, lng, blk, pl in VARS:
+        lib.ggml_backend_mi355x_set_tuning(b"planes", pl)
         lib.ggml_backend_mi355x_set_tuning(b"mmq_variant", var)
         lib.ggml_backend_mi355x_set_tuning(b"mmq_long", lng)
         lib.ggml_backend_mi355x_set_tuning(b"mmv_blocks", blk)
@@ -44,7 +48,7 @@ for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
         y = G.tensor_get(lib, wl.y[0])
         ref = refs.setdefault((tname, B), y)
         same = "bit-equal to the first variant" if np.array_equal(y.view(np.uint32), ref.view(np.uint32)) else "DIFFERS from the first variant"
-        print(f"{tname:5s} B={B:4d} var={var:5d} long={lng} blocks={blk} R={R}: {ms * 1e3 / R:8.2f} us/mul_mat in a graph of {R}  {2 * 4096 * 4096 * B * R / (ms / 1e3) / 1e12:7.1f} TFLOP/s  "
+        print(f"{tname:5s} B={B:4d} var={var:5d} long={lng} blocks={blk} planes={pl} R={R}: {ms * 1e3 / R:8.2f} us/mul_mat in a graph of {R}  {2 * 4096 * 4096 * B * R / (ms / 1e3) / 1e12:7.1f} TFLOP/s  "
               f"| one per graph {ms1 * 1e3:8.2f} us  {same}")
         wl.free()
 lib.ggml_backend_free(be)

@@ -125,7 +125,54 @@ def gpt2_run(kind, n_tok):
     lib.ggml_backend_free(be)
 
 
+def normgemv(E, N, B, reps=6):
+    """norm -> mul(g) -> add(b) -> F16 mul_mat [E, N] x B columns -> add(bias): the fused F16 GEMV with
+    its norm prologue (GPT-2's c_attn / c_fc shape), one graph per step over rotated weights"""
+    from ggml_mi355x import synth
+    lib = G.runtime()
+    assert lib.ggml_backend_mi355x_stamps_enable(SLOTS), "stamps need the diagnostic build"
+    be = G.mi355x_backend(lib)
+    R = 24
+    ctx = G.Context(lib, lib.ggml_tensor_overhead() * (8 * R + 8) + lib.ggml_graph_overhead_custom(16, False) * R, no_alloc=True)
+    c = ctx.ctx
+    x = lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F32, E, B)
+    g = lib.ggml_new_tensor_1d(c, G.GGML_TYPE_F32, E)
+    b = lib.ggml_new_tensor_1d(c, G.GGML_TYPE_F32, E)
+    graphs, ws = [], []
+    for r in range(R):
+        w = lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F16, E, N)
+        bias = lib.ggml_new_tensor_1d(c, G.GGML_TYPE_F32, N)
+        h = lib.ggml_add(c, lib.ggml_mul(c, lib.ggml_norm(c, x, 1e-5), g), b)
+        out = lib.ggml_add(c, lib.ggml_mul_mat(c, w, h), bias)
+        gr = lib.ggml_new_graph_custom(c, 16, False)
+        lib.ggml_build_forward_expand(gr, out)
+        graphs.append(gr)
+        ws.append((w, bias))
+    buf = lib.ggml_backend_alloc_ctx_tensors(c, be)
+    G.tensor_set(lib, x, synth.uniform(1, E * B))
+    G.tensor_set(lib, g, synth.uniform(2, E) + np.float32(1))
+    G.tensor_set(lib, b, synth.uniform(3, E))
+    wv = synth.uniform(4, E * N).astype(np.float16)
+    for w, bias in ws:
+        G.tensor_set(lib, w, wv)
+        G.tensor_set(lib, bias, synth.uniform(5, N))
+    for gr in graphs:
+        lib.ggml_backend_graph_compute(be, gr)
+    lib.ggml_backend_mi355x_stamps_reset()
+    for i in range(reps):
+        lib.ggml_backend_graph_compute_async(be, graphs[i % R])
+    lib.ggml_backend_synchronize(be)
+    _, L = read(lib)
+    report(L, f"== norm -> F16 GEMV {E}x{N}, {B} columns")
+    lib.ggml_backend_buffer_free(buf)
+    ctx.free()
+    lib.ggml_backend_free(be)
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "normgemv":
+        normgemv(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+        sys.exit(0)
     if sys.argv[1] == "lone":
         lone(sys.argv[2:] or ["q4_K:4096:4096:1"])
     else:
