@@ -2959,6 +2959,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.f16_waves = value;
         return true;
     }
+    if (strcmp(name, "f16_norm_waves") == 0 && value >= 0 && value <= 8) {
+        g_mi_tuning.f16_norm_waves = value;
+        return true;
+    }
     if (strcmp(name, "f16_ps_waves") == 0 && (value == 0 || value == 2 || value == 4 || value == 8)) {
         g_mi_tuning.f16_ps_waves = value;
         return true;

@@ -44,6 +44,13 @@ __device__ __forceinline__ float dot8(const uint4 & w, const uint4 & x, float ac
     return acc;
 }
 
+// zero a weight chunk past the row's end at its use, not at its load: a select right after the
+// load was compiled into a branch whose register writes wait for the load (vmcnt(0)), which
+// serialised the prologue's loads (k_gemv_f16_ps: one full memory round trip per chunk past nit)
+__device__ __forceinline__ uint4 keep_if(bool keep, const uint4 & v) {
+    return keep ? v : make_uint4(0u, 0u, 0u, 0u);
+}
+
 // sum over each aligned 16-lane row; every lane of the row gets it
 __device__ __forceinline__ float row16_sum(float v) {
     auto f = [](int x) { return __int_as_float(x); };
@@ -70,11 +77,8 @@ __device__ __forceinline__ void norm_load(const float * __restrict__ xc, int64_t
         // unconditional loads at clamped addresses + selects: a load under a lane branch makes
         // the compiler wait for it at the branch's join (vmcnt(0)), serialising every load
         const int64_t k = (int64_t) j * 256 + lane * 4;
-        const bool in = k < K;
-        const int64_t kc = in ? k : K - 4;
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 vv = *(const float4 *) (xc + kc);
-        v[j] = in ? vv : z;
+        const int64_t kc = k < K ? k : K - 4;
+        v[j] = *(const float4 *) (xc + kc);  // (zeroed past K in norm_store, at use)
         if constexpr (GB) {
             // absent g / b: the load reads x instead (valid address, no branch), the value is
             // not used (norm_store checks pro.g / pro.b)
@@ -88,6 +92,9 @@ template <int JM, bool GB>
 __device__ __forceinline__ void norm_store(float4 (&v)[JM], const float4 (&g)[GB ? JM : 1], const float4 (&bb)[GB ? JM : 1], int64_t K,
                                            int64_t kp, const mi_norm_prologue & pro, uint16_t * xs, int lane) {
     const float fk = (float) K;
+#pragma unroll
+    for (int j = 0; j < JM; j++)  // elements past K (clamped loads) are zero
+        if ((int64_t) j * 256 + lane * 4 >= K) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     float scale;
     if (pro.mode == 2) {
         float s2 = 0.0f;
@@ -139,20 +146,23 @@ __device__ __forceinline__ void norm_store(float4 (&v)[JM], const float4 (&g)[GB
 template <int JX>
 struct ColStager {
     float4 v[JX];
+    int64_t kk = 0;  // K of the last load
     __device__ __forceinline__ void load(const float * __restrict__ xc, int64_t K, int64_t base) {
 #pragma unroll
         for (int j = 0; j < JX; j++) {
             const int64_t i = base + (int64_t) j * blockDim.x + threadIdx.x;  // float4 index
-            const bool in = i * 4 < K;
-            const float4 vv = *(const float4 *) (xc + (in ? i * 4 : K - 4));  // branch-free (see norm_load)
-            v[j] = in ? vv : make_float4(0.f, 0.f, 0.f, 0.f);
+            // branch-free (see norm_load); past K zeroed at the store: a select right after the
+            // load became a branch that waited for it (vmcnt(0) per load)
+            v[j] = *(const float4 *) (xc + (i * 4 < K ? i * 4 : K - 4));
         }
+        kk = K;
     }
     __device__ __forceinline__ void store(uint16_t * xd, int64_t kp, int64_t base) {
 #pragma unroll
         for (int j = 0; j < JX; j++) {
             const int64_t i = base + (int64_t) j * blockDim.x + threadIdx.x;
-            if (i * 4 < kp) *(uint2 *) (xd + i * 4) = make_uint2(pack_h2(v[j].x, v[j].y), pack_h2(v[j].z, v[j].w));
+            const float4 w = i * 4 < kk ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i * 4 < kp) *(uint2 *) (xd + i * 4) = make_uint2(pack_h2(w.x, w.y), pack_h2(w.z, w.w));
         }
     }
     __device__ __forceinline__ void column(const float * __restrict__ xc, int64_t K, int64_t kp, uint16_t * xd, int64_t from) {
@@ -202,7 +212,7 @@ __device__ __forceinline__ void stage_cols(const mi_src_cols & x, int64_t c0, in
 // is how many rows' bytes are in flight at once; several row groups per workgroup only for very
 // tall matrices (lm_head), where the per-workgroup staging of the activations would otherwise
 // cost more L2 traffic than the weights.
-template <int NC, int EPI, int U, bool ONE, int JM>
+template <int NC, int EPI, int U, bool ONE, int JM, bool XH = false>
 __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                                   mi_src_cols x, const uint16_t * __restrict__ xh, int64_t ncols,
                                                   float * __restrict__ dst, size_t ycol, mi_f16_epilogue e, mi_norm_prologue pro,
@@ -226,8 +236,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
     auto ld = [&](int j) -> uint4 {
         const int it = wave + (j < nj ? j : nj - 1) * nw;
         const int64_t c = (int64_t) it * kLpr + m;
-        const uint4 v = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);
-        return c < k8 ? v : make_uint4(0u, 0u, 0u, 0u);
+        return *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);  // (zeroed past K at use: keep_if)
     };
 
     // Everything that does not depend on the weights is requested before them (vmcnt retires in
@@ -241,19 +250,25 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
     if constexpr (JM > 0) {
         norm_load<JM, GB>((const float *) (x.base + (c0 + (wid < nc ? wid : 0)) * x.nb1), K, lane, pro, pv, pg, pb);
     } else {
-        if (!xh) st.load((const float *) (x.base + c0 * x.nb1), K, 0);
-    }
-    float e_bias = 0.0f, e_res = 0.0f;
-    {
-        const int64_t rc = live ? row : 0, cc = c0 + (m < nc ? m : nc - 1);
-        if (EPI >= 1) e_bias = e.bias[rc];
-        if (EPI == 2) e_res = *(const float *) (e.resid + cc * e.resid_nb1 + rc * sizeof(float));
+        // (XH: f16 activations given; a template switch, not a runtime branch: a load under a
+        // branch is waited for at its join, before the weights below are even requested)
+        if constexpr (!XH) st.load((const float *) (x.base + c0 * x.nb1), K, 0);
     }
     // xfirst: the activation-side loads land before any weight load is queued behind them
     if (e.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint4 cur[U];
 #pragma unroll
     for (int u = 0; u < U; u++) cur[u] = ld(u);
+    // the epilogue's bias / residual right behind the weights (they land with them; requested
+    // before, the compiler paired a loaded register into a weight-address computation and made the
+    // weight requests wait for it)
+    asm volatile("" ::: "memory");
+    float e_bias = 0.0f, e_res = 0.0f;
+    {
+        const int64_t rc = live ? row : 0, cc = c0 + (m < nc ? m : nc - 1);
+        if (EPI >= 1) e_bias = e.bias[rc];
+        if (EPI == 2) e_res = *(const float *) (e.resid + cc * e.resid_nb1 + rc * sizeof(float));
+    }
 
     // stage the f16 activation columns (zero-padded to kp). One column with the norm prologue:
     // every wave normalizes it into its own LDS copy (PRIV), so no wave waits for another's.
@@ -274,9 +289,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
 #pragma unroll
                     for (int j = 0; j < JM; j++) {
                         const int64_t k = (int64_t) j * 256 + lane * 4;
-                        const bool in = k < K;
-                        const float4 vv = *(const float4 *) (xc + (in ? k : K - 4));
-                        nv[j] = in ? vv : make_float4(0.f, 0.f, 0.f, 0.f);
+                        nv[j] = *(const float4 *) (xc + (k < K ? k : K - 4));  // (zeroed in norm_store)
                     }
                 }
                 norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) c * kp, lane);
@@ -284,18 +297,20 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
                 for (int j = 0; j < JM; j++) pv[j] = nv[j];
             }
         }
-    } else if (xh) {
+    } else if constexpr (XH) {
         for (int c = 0; c < nc; c++) {
             const uint4 * src = (const uint4 *) (xh + (c0 + c) * K);
             uint4 * xd = (uint4 *) (xs + (size_t) c * kp);
             for (int64_t k = threadIdx.x; k < kp / 8; k += blockDim.x) xd[k] = k < k8 ? src[k] : make_uint4(0u, 0u, 0u, 0u);
         }
-    } else if (nc == 1) {
-        st.store(xs, kp, 0);
-        st.column((const float *) (x.base + c0 * x.nb1), K, kp, xs, (int64_t) JX * blockDim.x);
     } else {
-        (void) st;
-        stage_cols<JX>(x, c0, nc, K, kp, xs);
+        if (nc == 1) {
+            st.store(xs, kp, 0);
+            st.column((const float *) (x.base + c0 * x.nb1), K, kp, xs, (int64_t) JX * blockDim.x);
+        } else {
+            (void) st;
+            stage_cols<JX>(x, c0, nc, K, kp, xs);
+        }
     }
     MI_STAMP(e.stamps, 1);  // activations staged (normalized) by wave 0
     if (!priv) mi_lds_barrier();
@@ -303,8 +318,9 @@ __global__ __launch_bounds__(512) void k_gemv_f16(const uint8_t * __restrict__ W
     float acc[NC];
 #pragma unroll
     for (int c = 0; c < NC; c++) acc[c] = 0.0f;
-    auto step = [&](const uint4 & w, int j) {
+    auto step = [&](const uint4 & wl, int j) {
         const int64_t k = ((int64_t) (wave + j * nw) * kLpr + m) * kChunk;
+        const uint4 w = keep_if(k < K, wl);
 #pragma unroll
         for (int c = 0; c < NC; c++)
             if (c < nc) acc[c] = dot8(w, *(const uint4 *) (xw + (size_t) c * kp + k), acc[c]);
@@ -393,8 +409,7 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
         for (int u = 0; u < U; u++) {
             const int it = u < nit ? u : nit - 1;
             const int64_t c = (int64_t) it * kLpr + m;
-            const uint4 v = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);
-            w[u] = c < k8 ? v : make_uint4(0u, 0u, 0u, 0u);
+            w[u] = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);  // (zeroed past K at use)
         }
         if (EPI >= 1) eb = e.bias[r];
     };
@@ -418,9 +433,7 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
 #pragma unroll
                 for (int j = 0; j < JM; j++) {
                     const int64_t k = (int64_t) j * 256 + lane * 4;
-                    const bool in = k < K;
-                    const float4 vv = *(const float4 *) (xc2 + (in ? k : K - 4));
-                    nv[j] = in ? vv : make_float4(0.f, 0.f, 0.f, 0.f);
+                    nv[j] = *(const float4 *) (xc2 + (k < K ? k : K - 4));  // (zeroed in norm_store)
                 }
                 norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) wid * kp, lane);
                 norm_store<JM, GB>(nv, pg, pb, K, kp, pro, xs + (size_t) (wid + 4) * kp, lane);
@@ -447,9 +460,10 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (u < nit) {
+                const uint4 w = keep_if((int64_t) u * kLpr + m < k8, cur[u]);
 #pragma unroll
                 for (int c = 0; c < NC; c++)
-                    if (c < nc) acc[c] = dot8(cur[u], *(const uint4 *) (xs + (size_t) c * kp + ((int64_t) u * kLpr + m) * kChunk), acc[c]);
+                    if (c < nc) acc[c] = dot8(w, *(const uint4 *) (xs + (size_t) c * kp + ((int64_t) u * kLpr + m) * kChunk), acc[c]);
             }
         }
         float mine = 0.0f;  // lane m of the row holds column m
@@ -531,8 +545,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
     for (int u = 0; u < U; u++) {
         const int it = u < nit ? u : nit - 1;
         const int64_t c = (int64_t) it * kLpr + m;
-        const uint4 v = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);
-        cur[u] = c < k8 && u < nit ? v : make_uint4(0u, 0u, 0u, 0u);
+        cur[u] = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);  // (zeroed past K at use)
     }
 
 #pragma unroll
@@ -566,7 +579,7 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
     float acc = 0.0f;
 #pragma unroll
     for (int u = 0; u < U; u++)
-        if (u < nit) acc = dot8(cur[u], *(const uint4 *) (xw + ((int64_t) u * kLpr + m) * kChunk), acc);
+        if (u < nit) acc = dot8(keep_if((int64_t) u * kLpr + m < k8, cur[u]), *(const uint4 *) (xw + ((int64_t) u * kLpr + m) * kChunk), acc);
     acc = row16_sum(acc);
     if (live && m == 0) {
         float r = acc;
@@ -596,7 +609,8 @@ void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_c
     mi_f16_epilogue es = e;
     es.stamps = mi_stamp_take(JM ? "k_gemv_f16_norm" : "k_gemv_f16", grid.x * grid.y);
     es.xfirst = g_mi_tuning.xfirst == 1;  // (off by default: GPT-2 decode 304 -> 316 us per token with it)
-#define MI_GEMV_F16(EP) hipLaunchKernelGGL((k_gemv_f16<NC, EP, U, ONE, JM>), grid, dim3(64 * ks * rgs), lds, s, w, nb01, K, N, x, xh, ncols, dst, ycol, es, pro, kp, rgs)
+#define MI_GEMV_F16X(EP, XHV) hipLaunchKernelGGL((k_gemv_f16<NC, EP, U, ONE, JM, XHV>), grid, dim3(64 * ks * rgs), lds, s, w, nb01, K, N, x, xh, ncols, dst, ycol, es, pro, kp, rgs)
+#define MI_GEMV_F16(EP) do { if constexpr (JM == 0) { if (xh) MI_GEMV_F16X(EP, true); else MI_GEMV_F16X(EP, false); } else MI_GEMV_F16X(EP, false); } while (0)
     switch (epi) {
         case 0: MI_GEMV_F16(0); break;
         case 1: MI_GEMV_F16(1); break;
@@ -604,6 +618,7 @@ void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_c
         default: MI_GEMV_F16(3); break;
     }
 #undef MI_GEMV_F16
+#undef MI_GEMV_F16X
 }
 
 template <int U, bool ONE, int JM>
@@ -657,9 +672,12 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
     // very tall matrices (lm_head): row groups share one staging of the activations per workgroup
     ks = std::min(ks, nit);
     if (pro.mode) ks = std::max(ks, (nit + 7) / 8);  // the prologue path runs one register pass
-    // several columns with the norm prologue: one column per wave where K allows (a lone wave
-    // normalizes its columns one after the other, ~0.9 us each: 8 columns 8.2 us of prologue)
-    if (pro.mode && nc > 1) ks = std::max(ks, std::min(nc, nit));
+    // several columns with the norm prologue: the columns' norms spread over 3 waves (a lone wave
+    // normalizes its columns one after the other, ~0.9 us each: 8 columns 8.2 us of prologue; one
+    // column per wave makes 6-wave workgroups of which only two fit a CU at 106 VGPRs, so GPT-2's
+    // 768 c_fc workgroups ran in two rounds: batched decode 0.700 -> 0.672 ms/step with 3,
+    // profiles/r05r_batched_norm_waves.txt)
+    if (pro.mode && nc > 1) ks = std::max(ks, std::min(g_mi_tuning.f16_norm_waves > 0 ? g_mi_tuning.f16_norm_waves : 3, nit));
     const int per = (nit + ks - 1) / ks;  // steps per wave
     ks = (nit + per - 1) / per;
     const bool one = per <= 8;

@@ -553,14 +553,17 @@ __device__ void norm_prologue(const mi_mmv_group & g, const char * X, int ncols,
         float scale;
         if (g.pro.mode == 2) {
             const float mean = wave_mean_cpu_order<true, kJ>(r.v, K);
+            if (c == 0) MI_STAMP(g.stamps, 6);  // (diagnostic: first column's x landed, mean certified)
             scale = 1.0f / sqrtf(add_rn(mean, g.pro.eps));
         } else {
             const float mean = wave_mean_cpu_order<false, kJ>(r.v, K);
+            if (c == 0) MI_STAMP(g.stamps, 6);
 #pragma unroll
             for (int j = 0; j < kJ; j++) r.v[j] = sub_rn(r.v[j], mean);
             const float variance = wave_mean_cpu_order<true, kJ>(r.v, K);
             scale = 1.0f / sqrtf(add_rn(variance, g.pro.eps));
         }
+        if (c == 0) MI_STAMP(g.stamps, 5);  // (diagnostic: first column's scale)
 #pragma unroll
         for (int j = 0; j < kJ; j++) {
             const int64_t k = (int64_t) j * 64 + lane;
@@ -637,7 +640,7 @@ template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO, bool 
 __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     MI_STAMP(g.stamps, 0);
-    MI_STAMP_CLK(g.stamps, 6);
+    if (!(PRO && g.pro.mode)) MI_STAMP_CLK(g.stamps, 6);  // (norm prologue: slots 6, 5 time its phases)
     constexpr int NB = PD + 1;  // ring slots
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -706,6 +709,10 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     };
     epi_pre<NC> epre;
     if constexpr (PRO) {
+        // wave 0 alone requests the norm's column. (The load under this branch is waited for at
+        // its join, before wave 0 requests its weights; every wave loading the column instead --
+        // unconditional, ahead of the weights -- queued waves 1-3's weights behind it: Q4_K GPT-2
+        // decode 0.417 -> 0.443 ms/token, profiles/r05t_bench_quick.json)
         if (g.pro.mode && wave == 0) norm_cols_load(g, X, 0, nc0);
         epi_prefetch<NC>(g, row_begin + wave < Nr ? row_begin + wave : Nr - 1, X, epre);
     } else {
@@ -869,7 +876,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
             if (k == 0) MI_STAMP(g.stamps, 3);  // first row reduced and stored
         }
     }
-    MI_STAMP_CLK(g.stamps, 5);
+    if (!(PRO && g.pro.mode)) MI_STAMP_CLK(g.stamps, 5);
     MI_STAMP(g.stamps, 7);
 }
 

@@ -62,7 +62,13 @@ def report(launches, title):
         wg = (t7 - t0) * TICK_US
         ph = " ".join(f"{a}->{b}:{phase(st, a, b):.2f}" for a, b in ((0, 1), (1, 2), (0, 2), (2, 1), (2, 3), (0, 3), (3, 7), (1, 4), (4, 7))
                       if not np.isnan(phase(st, a, b)) and 0 <= phase(st, a, b) < 1e4)
-        m = (st[:, 5] > st[:, 6]) & (st[:, 7] > st[:, 0]) & (st[:, 6] > 0)
+        # norm prologue (k_mmv_stream PRO): realtime slots 6 (mean certified), 5 (scale) instead of the clock
+        rt = (st[:, 6] > st[:, 0]) & (st[:, 6] - st[:, 0] < 10**5) & (st[:, 5] >= st[:, 6]) & (st[:, 5] - st[:, 6] < 10**5)
+        if rt.sum() > len(st) // 2:
+            ph += " | norm: " + " ".join(f"{a}->{b}:{phase(st[rt], a, b):.2f}" for a, b in ((0, 6), (6, 5), (5, 2)))
+            m = np.zeros(len(st), bool)
+        else:
+            m = (st[:, 5] > st[:, 6]) & (st[:, 7] > st[:, 0]) & (st[:, 6] > 0)
         if m.any():  # shader clock: memtime ticks / realtime ticks x 100 MHz
             ph += f" clk:{np.median((st[m, 5] - st[m, 6]) / (st[m, 7] - st[m, 0])) * 100:.0f}MHz"
         print(f"{name:18s} {nb:5d} {gap:6.2f} {span:6.2f} {(t0.max() - t0.min()) * TICK_US:6.2f} {np.median(wg):6.2f} {wg.max():6.2f}  {ph}")
