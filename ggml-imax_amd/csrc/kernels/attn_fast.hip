@@ -64,15 +64,29 @@ __device__ __forceinline__ float attn_head(const mi_attn_desc & a, int h, int t,
             r[kk][1] = *(const float4 *) (p + 16);
         }
     };
+    // KQ mask row (batched decode): its values for a chunk's keys requested with the chunk's K
+    // rows, unconditionally from a valid address (K itself when there is no mask: n_kv floats of
+    // it are readable) -- a load under a branch, or one issued next to its use, is waited for at
+    // once; the values are used only with a mask
+    const bool use_mask = a.mask != nullptr;
+    const float * mrow = use_mask ? (const float *) (a.mask + (size_t) t * a.mask_nb1) : (const float *) a.k;
+    float mk[KPG];
+    auto load_mask = [&](int c0) {
+#pragma unroll
+        for (int kk = 0; kk < KPG; kk++) mk[kk] = mrow[min(c0 + kk * G + grp, n_kv - 1)];
+    };
     load_rows(kb, a.k_nb[1], 0, kr);
+    load_mask(0);
     load_rows(vb, a.v_nb[0], 0, vr);
 
     // ---- pass 1: scores and their max
     const int lim = a.n_past + t;  // keys k > lim are masked (diag_mask_inf)
-    const float * mrow = a.mask ? (const float *) (a.mask + (size_t) t * a.mask_nb1) : nullptr;
     float mx = -INFINITY;
     for (int c0 = 0; c0 < n_kv; c0 += CH) {
-        if (c0) load_rows(kb, a.k_nb[1], c0, kr);
+        if (c0) {
+            load_rows(kb, a.k_nb[1], c0, kr);
+            load_mask(c0);
+        }
 #pragma unroll
         for (int kk = 0; kk < KPG; kk++) {
             float d = kr[kk][0].x * q0.x + kr[kk][0].y * q0.y + kr[kk][0].z * q0.z + kr[kk][0].w * q0.w +
@@ -80,7 +94,7 @@ __device__ __forceinline__ float attn_head(const mi_attn_desc & a, int h, int t,
             d = group_sum<LPK>(d);
             const int key = c0 + kk * G + grp;
             float w = d * a.pre_scale;
-            if (mrow) w = w + mrow[min(key, n_kv - 1)];
+            if (use_mask) w = w + mk[kk];
             if (key >= a.n_past && key > lim) w = -INFINITY;
             w = w * a.sm_scale;
             if (key < n_kv) {

@@ -166,9 +166,21 @@ struct ColStager {
         }
     }
     __device__ __forceinline__ void column(const float * __restrict__ xc, int64_t K, int64_t kp, uint16_t * xd, int64_t from) {
-        for (int64_t base = from; base < kp / 4; base += (int64_t) JX * blockDim.x) {
-            load(xc, K, base);
-            store(xd, kp, base);
+        // rounds pipelined (as stage_cols): the next round requested before this one is stored
+        const int64_t step = (int64_t) JX * blockDim.x;
+        if (from >= kp / 4) return;
+        load(xc, K, from);
+        for (int64_t base = from; base < kp / 4; base += step) {
+            float4 cur[JX];
+#pragma unroll
+            for (int j = 0; j < JX; j++) cur[j] = v[j];
+            if (base + step < kp / 4) load(xc, K, base + step);
+#pragma unroll
+            for (int j = 0; j < JX; j++) {
+                const int64_t i = base + (int64_t) j * blockDim.x + threadIdx.x;
+                const float4 w = i * 4 < kk ? cur[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (i * 4 < kp) *(uint2 *) (xd + i * 4) = make_uint2(pack_h2(w.x, w.y), pack_h2(w.z, w.w));
+            }
         }
     }
 };
@@ -179,8 +191,8 @@ struct ColStager {
 template <int JX>
 __device__ __forceinline__ void stage_cols(const mi_src_cols & x, int64_t c0, int nc, int64_t K, int64_t kp, uint16_t * xs) {
     const int64_t k4 = K / 4, total = (int64_t) nc * k4;
-    for (int64_t base = 0; base < total; base += (int64_t) JX * blockDim.x) {
-        float4 v[JX];
+    const int64_t step = (int64_t) JX * blockDim.x;
+    auto load = [&](float4 (&v)[JX], int64_t base) {
 #pragma unroll
         for (int j = 0; j < JX; j++) {
             const int64_t i = base + (int64_t) j * blockDim.x + threadIdx.x;
@@ -188,6 +200,13 @@ __device__ __forceinline__ void stage_cols(const mi_src_cols & x, int64_t c0, in
             const int64_t c = ic / k4, q = ic - c * k4;
             v[j] = *(const float4 *) (x.base + (c0 + c) * x.nb1 + q * 16);
         }
+    };
+    // rounds pipelined: the next round's loads are requested before this round is converted and
+    // stored, so the rounds cost about one memory round trip instead of one each
+    float4 v[JX], nv[JX];
+    load(v, 0);
+    for (int64_t base = 0; base < total; base += step) {
+        if (base + step < total) load(nv, base + step);
 #pragma unroll
         for (int j = 0; j < JX; j++) {
             const int64_t i = base + (int64_t) j * blockDim.x + threadIdx.x;
@@ -196,6 +215,8 @@ __device__ __forceinline__ void stage_cols(const mi_src_cols & x, int64_t c0, in
                 *(uint2 *) (xs + c * kp + q * 4) = make_uint2(pack_h2(v[j].x, v[j].y), pack_h2(v[j].z, v[j].w));
             }
         }
+#pragma unroll
+        for (int j = 0; j < JX; j++) v[j] = nv[j];
     }
     for (int64_t i = threadIdx.x; i < (int64_t) nc * (kp - K); i += blockDim.x) {
         const int64_t c = i / (kp - K);

@@ -979,7 +979,10 @@ void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
     // at K = 4096, and its quantization) is the long pole -- lone Q4_K 4096^2 6.93 -> 6.11 us per
     // graph, 3072 x 768 4.96 -> 4.57 us; at GPT-2's K = 768 the weights' latency would be exposed
     // after the activations' (decode token 456 -> 475 us, profiles/r05c_xfirst_ab.txt)
-    const bool xf = g.n == 1 && (g_mi_tuning.xfirst == 1 || (g_mi_tuning.xfirst < 0 && g.K >= 2048));
+    // Tall lone members (lm_head, N = 50257: ~17 rows per wave) take the same instances for their
+    // prefetch depth: with one row in flight every row paid a memory round trip (Q4_K GPT-2 lm_head
+    // 22.8 us, profiles/r05o_gpt2_q4k_token_stamps.txt)
+    const bool xf = g.n == 1 && (g_mi_tuning.xfirst == 1 || (g_mi_tuning.xfirst < 0 && (g.K >= 2048 || g.N >= 16384)));
     if (g.pro.mode || e.bias || e.resid || e.gelu_table || e.copy[0].ptr || e.copy[1].ptr) {
         // the graph's norm prologue and/or epilogue: instances of their own (prefetch depth 1) so
         // that their registers and per-row branches do not weigh on the plain kernels

@@ -195,7 +195,9 @@ __global__ __launch_bounds__(256) void k_get_rows_q(mi_tensor_desc d, mi_tensor_
 // and the two f32 values are added once, as the ADD node does. 1-D index vectors, f32 dst rows.
 template <int T>  // 0: f32 / f16 (ld_f), else the quantized type
 __device__ __forceinline__ float emb_elem(const mi_tensor_desc & a, int32_t r, int64_t c) {
-    if constexpr (T == 0) return ld_f(a.data + c * a.nb[0] + (size_t) r * a.nb[1], a.type);
+    // (f32 / f16 resolved at compile time: a runtime type select put the loads under a branch)
+    if constexpr (T == 0) return *(const float *) (a.data + c * a.nb[0] + (size_t) r * a.nb[1]);
+    else if constexpr (T == 1) return mi_h2f(*(const uint16_t *) (a.data + c * a.nb[0] + (size_t) r * a.nb[1]));
     else return dequant_elem<T>((const uint8_t *) a.data + (size_t) r * a.nb[1], c);
 }
 
@@ -210,10 +212,23 @@ __global__ __launch_bounds__(256) void k_get_rows_add(mi_tensor_desc d, mi_tenso
     const int r = (int) blockIdx.y;
     const int32_t rb = *(const int32_t *) (ib.data + (size_t) r * ib.nb[0]);
     const int32_t ra = *(const int32_t *) (ia.data + (size_t) r * ia.nb[0]);
-    for (int c = (int) (blockIdx.x * blockDim.x + threadIdx.x); c < ne0; c += (int) (gridDim.x * blockDim.x)) {
-        const float vb = emb_elem<TB>(b, rb, c);
-        const float va = emb_elem<TA>(a, ra, c);
-        *(float *) (d.data + (size_t) c * d.nb[0] + (size_t) r * d.nb[1]) = va + vb;
+    // every element's loads before any store (the stores may alias the tables as far as the
+    // compiler knows, so a load-add-store loop paid one memory round trip per iteration); clamped
+    // unconditional loads
+    constexpr int V = 4;
+    const int stride = (int) (gridDim.x * blockDim.x);
+    for (int c0 = (int) (blockIdx.x * blockDim.x + threadIdx.x); c0 < ne0; c0 += V * stride) {
+        float v[V];
+#pragma unroll
+        for (int u = 0; u < V; u++) {
+            const int c = min(c0 + u * stride, ne0 - 1);
+            v[u] = emb_elem<TA>(a, ra, c) + emb_elem<TB>(b, rb, c);
+        }
+#pragma unroll
+        for (int u = 0; u < V; u++) {
+            const int c = c0 + u * stride;
+            if (c < ne0) *(float *) (d.data + (size_t) c * d.nb[0] + (size_t) r * d.nb[1]) = v[u];
+        }
     }
     MI_STAMP(st, 7);
 }
@@ -478,6 +493,7 @@ static void launch_get_rows_add(const mi_tensor_desc & d, const mi_tensor_desc &
             case 8: hipLaunchKernelGGL((k_get_rows_add<TA, 8>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
             case 12: hipLaunchKernelGGL((k_get_rows_add<TA, 12>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
             case 13: hipLaunchKernelGGL((k_get_rows_add<TA, 13>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
+            case 1: hipLaunchKernelGGL((k_get_rows_add<TA, 1>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
             default: hipLaunchKernelGGL((k_get_rows_add<TA, 0>), g, dim3(256), 0, s, dc, a, iac, b, ibc, ne0, st); break;
         }
     }
@@ -491,6 +507,7 @@ void mi_op_get_rows_add(const mi_tensor_desc & d, const mi_tensor_desc & a, cons
         case 8: launch_get_rows_add<8>(d, a, ia, b, ib, n, s); break;
         case 12: launch_get_rows_add<12>(d, a, ia, b, ib, n, s); break;
         case 13: launch_get_rows_add<13>(d, a, ia, b, ib, n, s); break;
+        case 1: launch_get_rows_add<1>(d, a, ia, b, ib, n, s); break;
         default: launch_get_rows_add<0>(d, a, ia, b, ib, n, s); break;
     }
 }

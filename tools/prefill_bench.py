@@ -21,7 +21,7 @@ VARS = [(v, l) for v in VARS for l in LONGS]
 BLOCKS = [int(v) for v in os.environ.get("PF_MMV_BLOCKS", "0").split(",")]
 VARS = [(v, l, b) for (v, l) in VARS for b in BLOCKS]
 # PF_PLANES: repacked-planes settings to compare (Q4_K / Q5_K past 128 columns: 1 k_mmqr, 0 the canonical kernels)
-PLANES = [int(v) for v in os.environ.get("PF_PLANES", "1").split(",")]
+PLANES = [int(v) for v in os.environ.get("PF_PLANES", "0").split(",")]
 VARS = [(v, l, b, p) for (v, l, b) in VARS for p in PLANES]
 for tname in os.environ.get("PF_TYPES", "q4_K,q5_K,q4_0,q8_0,f16").split(","):
     for B in Bs:
