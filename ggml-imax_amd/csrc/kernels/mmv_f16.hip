@@ -191,6 +191,34 @@ struct ColStager {
 template <int JX>
 __device__ __forceinline__ void stage_cols(const mi_src_cols & x, int64_t c0, int nc, int64_t K, int64_t kp, uint16_t * xs) {
     const int64_t k4 = K / 4, total = (int64_t) nc * k4;
+    if (nc <= 8 && k4 <= 2 * (int64_t) blockDim.x) {
+        // every (column, float4) of the thread requested at once -- up to 8 columns x 2 float4 --
+        // with no index division (the flattened form below divides a 64-bit index by K / 4 twice
+        // per element: GPT-2's 8-column MLP projection spent 4.2 us staging its 96 KB)
+        const int tid = (int) threadIdx.x, nt = (int) blockDim.x, k4i = (int) k4;
+        float4 v[8][2];
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int q = tid + j * nt;
+                const char * col = x.base + (c0 + (c < nc ? c : nc - 1)) * x.nb1;
+                v[c][j] = *(const float4 *) (col + (size_t) (q < k4i ? q : k4i - 1) * 16);
+            }
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int q = tid + j * nt;
+                if (c < nc && q < k4i)
+                    *(uint2 *) (xs + (size_t) c * kp + (size_t) q * 4) = make_uint2(pack_h2(v[c][j].x, v[c][j].y), pack_h2(v[c][j].z, v[c][j].w));
+            }
+        if (kp > K) {
+            const int pad = (int) (kp - K);
+            for (int i = tid; i < nc * pad; i += nt) xs[(size_t) (i / pad) * kp + K + (i % pad)] = 0;
+        }
+        return;
+    }
     const int64_t step = (int64_t) JX * blockDim.x;
     auto load = [&](float4 (&v)[JX], int64_t base) {
 #pragma unroll

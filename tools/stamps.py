@@ -175,7 +175,51 @@ def normgemv(E, N, B, reps=6):
     lib.ggml_backend_free(be)
 
 
+def f16gemv(K, N, B, reps=6):
+    """F16 mul_mat [K, N] x B columns -> add(bias) -> add(residual): GPT-2's MLP c_proj shape, no
+    prologue, one graph per step over rotated weights"""
+    from ggml_mi355x import synth
+    lib = G.runtime()
+    assert lib.ggml_backend_mi355x_stamps_enable(SLOTS), "stamps need the diagnostic build"
+    be = G.mi355x_backend(lib)
+    R = 24
+    ctx = G.Context(lib, lib.ggml_tensor_overhead() * (8 * R + 8) + lib.ggml_graph_overhead_custom(16, False) * R, no_alloc=True)
+    c = ctx.ctx
+    x = lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F32, K, B)
+    res = lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F32, N, B)
+    graphs, ws = [], []
+    for r in range(R):
+        w = lib.ggml_new_tensor_2d(c, G.GGML_TYPE_F16, K, N)
+        bias = lib.ggml_new_tensor_1d(c, G.GGML_TYPE_F32, N)
+        out = lib.ggml_add(c, lib.ggml_add(c, lib.ggml_mul_mat(c, w, x), bias), res)
+        gr = lib.ggml_new_graph_custom(c, 16, False)
+        lib.ggml_build_forward_expand(gr, out)
+        graphs.append(gr)
+        ws.append((w, bias))
+    buf = lib.ggml_backend_alloc_ctx_tensors(c, be)
+    G.tensor_set(lib, x, synth.uniform(1, K * B))
+    G.tensor_set(lib, res, synth.uniform(2, N * B))
+    wv = synth.uniform(4, K * N).astype(np.float16)
+    for w, bias in ws:
+        G.tensor_set(lib, w, wv)
+        G.tensor_set(lib, bias, synth.uniform(5, N))
+    for gr in graphs:
+        lib.ggml_backend_graph_compute(be, gr)
+    lib.ggml_backend_mi355x_stamps_reset()
+    for i in range(reps):
+        lib.ggml_backend_graph_compute_async(be, graphs[i % R])
+    lib.ggml_backend_synchronize(be)
+    _, L = read(lib)
+    report(L, f"== F16 GEMV {K}x{N} + bias + residual, {B} columns")
+    lib.ggml_backend_buffer_free(buf)
+    ctx.free()
+    lib.ggml_backend_free(be)
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "f16gemv":
+        f16gemv(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+        sys.exit(0)
     if sys.argv[1] == "normgemv":
         normgemv(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
         sys.exit(0)
