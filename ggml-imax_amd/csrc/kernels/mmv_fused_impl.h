@@ -636,7 +636,10 @@ __device__ __forceinline__ void store_out(const mi_mmv_group & g, float * dst, i
 // requested first, a lone Q4_K 4096^2 member's activations took 3.6 us to land and quantize,
 // profiles/r05b_lone_gemv_stamps.txt); the weights are then requested while the activations are
 // quantized (PRO: after the prologue's quantization)
-template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO, bool XF>
+// MR > 1 (one column, rows of at most 16 items: tall short-K matrices such as GPT-2's lm_head,
+// K = 768 = 12 Q4_K items): each wave step covers MR rows, 16 lanes per row (lane 16 r + i: item i
+// of the step's row r) instead of one row on 64 lanes of which K / ITEM do work
+template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO, bool XF, int MR = 1>
 __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     MI_STAMP(g.stamps, 0);
@@ -677,7 +680,14 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
             F::load(slot[i], wr, item < nitems ? item : nitems - 1);
         }
     };
-    const int klast = nrows > 0 ? nrows - 1 : 0;
+    // MR > 1: ring slot = one step of MR rows; lane 16 r + i loads item i of row MR k + r
+    auto prefetch_mr = [&](typename F::Regs (&slot)[IPL], int k) {
+        const uint8_t * wr = wrow_of(MR * k + (lane >> 4));
+        const int item = lane & 15;
+        F::load(slot[0], wr, item < nitems ? item : nitems - 1);
+    };
+    const int nsteps = MR > 1 ? (nrows + MR - 1) / MR : nrows;
+    const int klast = nsteps > 0 ? nsteps - 1 : 0;
 
     // 0) what the prologue reads first, requested before the weights (vmcnt retires in order: a
     //    use of it would otherwise wait for the weight loads too): the norm prologue's first
@@ -722,7 +732,10 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     // 1) the first PD rows' weights in flight
     if constexpr (!(XF && PRO)) {
 #pragma unroll
-        for (int u = 0; u < PD; u++) prefetch(ring[u], u < klast ? u : klast);
+        for (int u = 0; u < PD; u++) {
+            if constexpr (MR > 1) prefetch_mr(ring[u], u < klast ? u : klast);
+            else prefetch(ring[u], u < klast ? u : klast);
+        }
     }
 
     // 2) quantize the member's activation columns into LDS (wave w: 256-slices w, w+4, ...),
@@ -765,11 +778,64 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     MI_STAMP(g.stamps, 1);  // wave 0's activation slices loaded and quantized
     if constexpr (XF && PRO) {
 #pragma unroll
-        for (int u = 0; u < PD; u++) prefetch(ring[u], u < klast ? u : klast);
+        for (int u = 0; u < PD; u++) {
+            if constexpr (MR > 1) prefetch_mr(ring[u], u < klast ? u : klast);
+            else prefetch(ring[u], u < klast ? u : klast);
+        }
     }
     __syncthreads();
     if (!(PRO && g.pro.mode)) MI_STAMP(g.stamps, 2);  // every wave's
 
+    if constexpr (MR > 1) {
+        static_assert(NC == 1 && IPL == 1 && !TAIL, "multi-row steps: one column, one item per lane");
+        const int rr = lane >> 4, it = lane & 15;
+        auto sync = [] {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+        };
+        for (int k0 = 0; k0 < nsteps; k0 += NB) {
+#pragma unroll
+            for (int u = 0; u < NB; u++) {
+                const int k = k0 + u;
+                if (k >= nsteps) break;  // wave-uniform
+                prefetch_mr(ring[(u + PD) % NB], k + PD < klast ? k + PD : klast);
+                const int j = MR * k + rr;  // this lane's row of the wave
+                if constexpr (ORD) {
+                    // R = g.ord_rows rows (a multiple of MR) collect their lane sums, then one
+                    // chain pass: lane 8 r + l runs CPU lane l of row slot r (as the one-row form)
+                    const int RS = g.ord_rows / MR, cs = g.ord_cs, S = g.ord_s;
+                    const int slot = k % RS;
+                    if (it < nitems) F::template dot_ord<1>(ring[u][0], it, it, act, K, ncols, scr + (slot * MR + rr) * cs, cs, S);
+                    if (slot == RS - 1 || k == nsteps - 1) {  // wave-uniform
+                        sync();
+                        if (k == nsteps - 1) MI_STAMP(g.stamps, 3);
+                        const int r = lane >> 3, ll = lane & 7;
+                        const int jr = (k - slot) * MR + r;
+                        const bool mine = r < (slot + 1) * MR && jr < nrows;
+                        float A = 0.0f, M = 0.0f;
+                        if (mine && !g.abl) F::chain(scr + r * cs, ll, nitems, S, A, M);
+                        const float v = F::finish(A, M);
+                        if (k == nsteps - 1) MI_STAMP(g.stamps, 4);
+                        if (ll == 0 && mine) store_out<PRO, 1>(g, dst, 0, row_begin + 4 * jr + wave, v, &epre);
+                        sync();
+                    }
+                } else {
+                    float acc[1] = {0.0f};
+                    if (it < nitems) F::template dot<1>(ring[u][0], it, act, K, ncols, acc);
+                    // sum over the row's 16 lanes (DPP within a 16-lane row)
+                    auto f = [](int x) { return __int_as_float(x); };
+                    auto i = [](float x) { return __float_as_int(x); };
+                    float v = acc[0];
+                    v += f(mi_dpp<MI_DPP_QP_1032>(0, i(v)));
+                    v += f(mi_dpp<MI_DPP_QP_2301>(0, i(v)));
+                    v += f(mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, i(v)));
+                    v += f(mi_dpp<MI_DPP_ROW_MIRROR>(0, i(v)));
+                    if (it == 0 && j < nrows) store_out<PRO, 1>(g, dst, 0, row_begin + 4 * j + wave, v, &epre);
+                    if (k == 0) MI_STAMP(g.stamps, 3);
+                }
+            }
+        }
+    } else
     // 3) stream: ring slot u holds row k0+u; refill it with row k0+u+PD right before using it
     //    (the last row again past the end: an L2 hit)
     for (int k0 = 0; k0 < nrows; k0 += NB) {
@@ -909,7 +975,7 @@ static int mi_cu_count() {
     return n;
 }
 
-template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO = false, bool XF = false>
+template <class F, int NC, int PD, int IPL, bool TAIL, bool ORD, bool PRO = false, bool XF = false, int MR = 1>
 void launch_one(mi_mmv_group g, hipStream_t s) {
     const size_t act = lds_bytes<F::QKA>(NC, g.K);
     size_t lds = act;
@@ -921,6 +987,7 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
         const int cs = F::ord_words(nitems, S);
         int R = (int) ((36 * 1024) / ((size_t) 4 * NC * cs * 4));
         if (R > 8 / NC) R = 8 / NC;
+        if (MR > 1) R = R >= MR ? R / MR * MR : 0;  // whole multi-row steps per chain pass (0: refused below)
         if (R >= 1) {
             g.ord_rows = R;
             g.ord_cs = cs;
@@ -932,11 +999,17 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
         }
         lds = ord_offset(act) + (size_t) 4 * (g.ord_rows ? g.ord_rows : 1) * NC * g.ord_cs * 4;
     }
+    if constexpr (MR > 1 && ORD) {
+        if (g.ord_rows < MR) {  // a chain pass must hold whole multi-row steps: the one-row form
+            launch_one<F, NC, PD, IPL, TAIL, ORD, PRO, XF, 1>(g, s);
+            return;
+        }
+    }
     if (PRO && g.pro.mode) {
         g.pro_off = (int) ord_offset(lds);
         lds = (size_t) g.pro_off + (size_t) NC * g.K * sizeof(float);
     }
-    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL, TAIL, ORD, PRO, XF>;
+    const void * fn = (const void *) k_mmv_stream<F, NC, PD, IPL, TAIL, ORD, PRO, XF, MR>;
     if (lds > 64 * 1024) {
         static bool attr_set = false;  // per instance
         if (!attr_set) {
@@ -960,7 +1033,7 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
     g.rows_per_block = rows;
     g.blocks_per_member = (int) ((g.N + rows - 1) / rows);
     g.stamps = mi_stamp_take(ORD ? "k_mmv_stream_ord" : "k_mmv_stream", (unsigned) (g.blocks_per_member * g.n));
-    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL, TAIL, ORD, PRO, XF>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds,
+    hipLaunchKernelGGL((k_mmv_stream<F, NC, PD, IPL, TAIL, ORD, PRO, XF, MR>), dim3((unsigned) (g.blocks_per_member * g.n)), dim3(256), lds,
                        s, g);
 }
 
@@ -983,7 +1056,17 @@ void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
     // prefetch depth: with one row in flight every row paid a memory round trip (Q4_K GPT-2 lm_head
     // 22.8 us, profiles/r05o_gpt2_q4k_token_stamps.txt)
     const bool xf = g.n == 1 && (g_mi_tuning.xfirst == 1 || (g_mi_tuning.xfirst < 0 && (g.K >= 2048 || g.N >= 16384)));
-    if (g.pro.mode || e.bias || e.resid || e.gelu_table || e.copy[0].ptr || e.copy[1].ptr) {
+    const bool pro_epi = g.pro.mode || e.bias || e.resid || e.gelu_table || e.copy[0].ptr || e.copy[1].ptr;
+    if constexpr (NC == 1) {
+        // tall lone members with rows of <= 16 items (GPT-2 lm_head: 50257 x 768, 12 Q4_K items per
+        // row): four rows per wave step on 16 lanes each (MR = 4); variant 9x: the one-row form
+        if (g.n == 1 && g.N >= 16384 && items <= 16 && variant / 10 != 9) {
+            if (pro_epi) launch_one<F, 1, 4, 1, false, ORD, true, false, 4>(g, s);
+            else launch_one<F, 1, 4, 1, false, ORD, false, false, 4>(g, s);
+            return;
+        }
+    }
+    if (pro_epi) {
         // the graph's norm prologue and/or epilogue: instances of their own (prefetch depth 1) so
         // that their registers and per-row branches do not weigh on the plain kernels
         if (xf) {
