@@ -728,6 +728,11 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     } else {
         load_round(xfirst, X, g.xcol, p_first);
     }
+    // (keep these loads ahead of the weight prefetch: the scheduler hoisted the prefetch above
+    // them, and vmcnt retires in order -- the activations then waited for the weights)
+#ifndef MI_AB_NO_ACT_ORDER  // (A/B builds only)
+    asm volatile("" ::: "memory");
+#endif
     if constexpr (XF && !PRO) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // 1) the first PD rows' weights in flight
     if constexpr (!(XF && PRO)) {
