@@ -37,7 +37,9 @@ __device__ __forceinline__ float group_sum(float v) {  // sum over each aligned 
 // KPG: keys per lane group held in registers per pass. sm: LDS of n_kv + 8 (D + 8) floats.
 // Returns, in threads d < D, element d of the head's output (num / den); other threads return 0.
 template <int D, int KPG>
-__device__ __forceinline__ float attn_head(const mi_attn_desc & a, int h, int t, float * sm, float * shm) {
+// st (diagnostic builds): phase stamps of the calling workgroup -- slot 2 the first chunk scored
+// (q and the first K rows landed), 3 the max known (first barrier), 4 the p.v sums done
+__device__ __forceinline__ float attn_head(const mi_attn_desc & a, int h, int t, float * sm, float * shm, uint64_t * st = nullptr) {
     constexpr int LPK = D / 8;          // lanes per key
     constexpr int GPW = 64 / LPK;       // key groups per wave
     constexpr int G = 8 * GPW;          // key groups per workgroup
@@ -102,10 +104,12 @@ __device__ __forceinline__ float attn_head(const mi_attn_desc & a, int h, int t,
                 if (j == 0) s[key] = w;
             }
         }
+        if (c0 == 0) MI_STAMP(st, 2);
     }
     mx = mi_wave_max(mx);
     if (lane == 0) shm[wave] = mx;
     __syncthreads();  // s[] and shm[] complete
+    MI_STAMP(st, 3);
     mx = shm[0];
 #pragma unroll
     for (int w = 1; w < 8; w++) mx = fmaxf(mx, shm[w]);
@@ -133,6 +137,7 @@ __device__ __forceinline__ float attn_head(const mi_attn_desc & a, int h, int t,
 #pragma unroll
         for (int e = 0; e < 8; e++) o[e] += __shfl_xor(o[e], off, 64);
     }
+    MI_STAMP(st, 4);
     l = group_sum<LPK>(l);  // only lane j == 0 of each group accumulated l
     float * red = sm + n_kv;  // [8 waves][D + 8]: o slices, then l at [D]
     if (lane < LPK) {
@@ -192,7 +197,7 @@ __global__ __launch_bounds__(512) void k_attn_proj(mi_attn_desc a, mi_attn_proj_
     uint4 w = make_uint4(0u, 0u, 0u, 0u);
     if constexpr (!XF) w = *(const uint4 *) wp;
     const float e_bias = p.bias[rc], e_res = p.resid[rc];  // requested before the attention too
-    const float r = attn_head<D, KPG>(a, h, 0, sm, shm);
+    const float r = attn_head<D, KPG>(a, h, 0, sm, shm, p.stamps);
     if constexpr (XF) w = *(const uint4 *) wp;
     MI_STAMP(p.stamps, 1);  // the head's attention done
     uint16_t * oh = (uint16_t *) (sm + ((a.n_kv + 3) & ~3) + 8 * (D + 8));  // 16-byte aligned

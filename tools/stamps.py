@@ -60,7 +60,7 @@ def report(launches, title):
         tot_span += span
         tot_gap += gap
         wg = (t7 - t0) * TICK_US
-        ph = " ".join(f"{a}->{b}:{phase(st, a, b):.2f}" for a, b in ((0, 1), (1, 2), (0, 2), (2, 1), (2, 3), (0, 3), (3, 7), (1, 4), (4, 7))
+        ph = " ".join(f"{a}->{b}:{phase(st, a, b):.2f}" for a, b in ((0, 1), (1, 2), (0, 2), (2, 1), (2, 3), (0, 3), (3, 4), (3, 7), (1, 4), (4, 1), (4, 7))
                       if not np.isnan(phase(st, a, b)) and 0 <= phase(st, a, b) < 1e4)
         # norm prologue (k_mmv_stream PRO): realtime slots 6 (mean certified), 5 (scale) instead of the clock
         rt = (st[:, 6] > st[:, 0]) & (st[:, 6] - st[:, 0] < 10**5) & (st[:, 5] >= st[:, 6]) & (st[:, 5] - st[:, 6] < 10**5)
