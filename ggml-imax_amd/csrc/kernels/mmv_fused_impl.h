@@ -1030,7 +1030,10 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
     if (g_mi_tuning.mmv_blocks <= 0 && g.n == 1 && g.K >= 4096) target = std::min(target, mi_cu_count());
     // Q5_K grouped launches: twice the resident count (smaller workgroups, a later tail; 4096 x 11008
     // 5.56 -> 5.75 TB/s, r04r_gemv_sweep.txt)
-    else if (g_mi_tuning.mmv_blocks <= 0 && std::is_same<F, FmtKQ<true>>::value && !ORD && !PRO) target *= 2;
+    // Q4_K tall members (4096 x 11008): the same (5.47-5.49 -> 5.56-5.62 TB/s on one box,
+    // profiles/r05sw_gemv_blocks_sweep.txt; 4096^2 members unchanged within noise, left alone)
+    else if (g_mi_tuning.mmv_blocks <= 0 && !ORD && !PRO &&
+             (std::is_same<F, FmtKQ<true>>::value || (std::is_same<F, FmtKQ<false>>::value && g.N >= 8192))) target *= 2;
     int bpm = target / g.n;
     if (bpm < 1) bpm = 1;
     int64_t rows = (g.N + bpm - 1) / bpm;
