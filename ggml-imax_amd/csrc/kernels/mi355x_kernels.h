@@ -134,7 +134,7 @@ struct mi_tuning {
     int f16_rgs;      // fast F16 decode GEMV: row groups (4 rows) per workgroup (0 = automatic)
     int f16_ps_waves; // k_gemv_f16_ps (GEMV over summed partials): waves per workgroup, 2 / 4 / 8 (0 = automatic)
     int mmq_long;     // Q4_K / Q5_K prefill past 128 columns: 0 = automatic (Q4_K k_mmqt, Q5_K k_mmqw), 1 = k_mmqw, 2 = k_mmqt; 16-23 k_mmqt stamps (diagnostic builds)
-    int xfirst;       // lone decode GEMVs: activation loads issued and landed before the weight loads: 1 always, 0 never, -1 auto (quantized, K >= 2048)
+    int xfirst;       // lone decode GEMVs: activation loads issued and landed before the weight loads: 1 always, 0 / -1 never (-1: the default)
     int f16_norm_waves; // F16 GEMV, several columns with the norm prologue: waves per workgroup (0 = automatic)
     int planes;       // long Q4_K prompts on repacked MFMA planes (mmq_planes.hip k_mmqr): 1 on, 0 off (default: slower than k_mmqt with HBM-streamed weights)
 };

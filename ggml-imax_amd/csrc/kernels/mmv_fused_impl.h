@@ -1055,15 +1055,12 @@ template <class F, int NC, bool ORD>
 void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
     const int items = (int) (g.K / F::ITEM);
     const mi_mmv_group::epilogue & e = g.epi;
-    // lone members (a dependent layer's GEMV): activations first (XF), every row of a wave in flight.
-    // Automatic (xfirst -1): from K = 2048 on, where the activation side (16 KB of f32 per workgroup
-    // at K = 4096, and its quantization) is the long pole -- lone Q4_K 4096^2 6.93 -> 6.11 us per
-    // graph, 3072 x 768 4.96 -> 4.57 us; at GPT-2's K = 768 the weights' latency would be exposed
-    // after the activations' (decode token 456 -> 475 us, profiles/r05c_xfirst_ab.txt)
-    // Tall lone members (lm_head, N = 50257: ~17 rows per wave) take the same instances for their
-    // prefetch depth: with one row in flight every row paid a memory round trip (Q4_K GPT-2 lm_head
-    // 22.8 us, profiles/r05o_gpt2_q4k_token_stamps.txt)
-    const bool xf = g.n == 1 && (g_mi_tuning.xfirst == 1 || (g_mi_tuning.xfirst < 0 && (g.K >= 2048 || g.N >= 16384)));
+    // XF (activations landed before any weight request) is opt-in only (xfirst 1). It was the
+    // automatic choice for lone members at K >= 2048 while the scheduler hoisted the weight prefetch
+    // above the activation loads (lone Q4_K 4096^2 6.93 -> 6.11 us per graph then); with the
+    // activation loads pinned ahead of the prefetch, both stream together and XF only serializes
+    // them: 5.45 -> 4.95 us per graph without it (profiles/r05xf_xfirst_ab.txt)
+    const bool xf = g.n == 1 && g_mi_tuning.xfirst == 1;
     const bool pro_epi = g.pro.mode || e.bias || e.resid || e.gelu_table || e.copy[0].ptr || e.copy[1].ptr;
     if constexpr (NC == 1) {
         // tall lone members with rows of <= 16 items (GPT-2 lm_head: 50257 x 768, 12 Q4_K items per
