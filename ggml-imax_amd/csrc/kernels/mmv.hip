@@ -204,6 +204,66 @@ __global__ __launch_bounds__(256) void k_mmv_q0(const uint8_t * __restrict__ W, 
     mmv_store<NC>(g, dst, row, i11, i12, i13, acc, lane);
 }
 
+// Reference CPU order (mmv_order 1) for the Q4_0 / Q8_0 rows this generic path serves -- K % 256
+// != 0 (rows of any block count, so only 2-byte aligned) and 3-D weight batches, where the fused
+// reference-order kernel (mmv_fused_impl.h) does not apply. The reference's AVX2 dot
+// (ggml_vec_dot_q8_0_q8_0 src/ggml-quants.c:4819+, ggml_vec_dot_q4_0_q8_0 :3469+) keeps eight
+// float lanes: lane l gets the exact int32 sum of elements 4l..4l+3 of each block
+// (mul_sum_i8_pairs_float; Q4_0 after bytes_from_nibbles_32 - 8: low nibbles of bytes 4l.. for
+// l < 4, high nibbles of bytes 4(l-4).. for l >= 4) in acc[l] = fma(x.d * y.d, q, acc[l]) over the
+// blocks in order, then hsum_float_8. Here eight lanes are those eight CPU lanes of one row (8 rows
+// per wave): each runs its own chain, the hsum is three xor shuffles in the same pairing.
+template <int NC, bool Q8>
+__global__ __launch_bounds__(256) void k_mmv_q0_ord(const uint8_t * __restrict__ W, mi_act_q8 act, float * __restrict__ dst, mmv_geom g) {
+    const int l = threadIdx.x & 7;
+    const int64_t row = (int64_t) blockIdx.x * 32 + (threadIdx.x >> 3);
+    const bool live = row < g.N;
+    const int64_t rc = live ? row : g.N - 1;  // (dead groups run a valid row: no early exit before the shuffles)
+    int64_t i11, i12, i13, i02, i03;
+    mmv_coords(g, NC, i11, i12, i13, i02, i03);
+    constexpr int BS = Q8 ? 34 : 18;
+    const uint8_t * wrow = W + i02 * g.nb02 + i03 * g.nb03 + rc * g.nb01;
+    const int nb = (int) (g.K / 32);
+    const int64_t col0 = i11 + g.ne11 * (i12 + g.ne12 * i13);
+    // the lane's 4 quant bytes: block byte 2 + 4 l (Q4_0: 2 + 4 (l & 3), nibble half l >> 2)
+    const int qoff = 2 + 4 * (Q8 ? l : (l & 3));
+
+    float A[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) A[c] = 0.0f;
+
+#pragma unroll 4
+    for (int b = 0; b < nb; b++) {
+        const uintptr_t blk = (uintptr_t) (wrow + (size_t) b * BS);
+        // blocks are 2-byte aligned: d and the quants from the aligned dwords covering them
+        // (buffers carry 256 B of tail slack)
+        const uint32_t dw0 = *(const uint32_t *) (blk & ~(uintptr_t) 3);
+        const float dw = mi_h2f((uint16_t) ((blk & 2) ? dw0 >> 16 : dw0 & 0xFFFF));
+        const uintptr_t qa = blk + qoff;
+        const uint32_t * qp = (const uint32_t *) (qa & ~(uintptr_t) 3);
+        uint32_t q = __builtin_amdgcn_alignbyte(qp[1], qp[0], (uint32_t) (qa & 3));
+        if constexpr (!Q8) q = (l < 4 ? q : q >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && i11 + c >= g.ne11) break;
+            const int64_t col = col0 + c;
+            const int av = *(const int *) (act.qs + col * g.K + (int64_t) b * 32 + 4 * l);
+            // Q4_0: (q - 8) . y, exact (0xF8 = -8 per byte)
+            const int sumi = Q8 ? mi_dot4((int) q, av, 0) : mi_dot4((int) q, av, mi_dot4((int) 0xF8F8F8F8u, av, 0));
+            A[c] = fmaf(dw * act.d[col * nb + b], (float) sumi, A[c]);  // _mm256_fmadd_ps, exact int -> float
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        // hsum_float_8: ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7))
+        float z = A[c] + __shfl_xor(A[c], 4, 8);
+        z = z + __shfl_xor(z, 2, 8);
+        z = z + __shfl_xor(z, 1, 8);
+        if (l == 0 && live && i11 + c < g.ne11)
+            *(float *) ((char *) dst + (i11 + c) * g.nb1 + i12 * g.nb2 + i13 * g.nb3 + row * sizeof(float)) = z;
+    }
+}
+
 mmv_geom make_geom(const mi_mm_desc & m, int NC) {
     mmv_geom g;
     g.K = m.K;
@@ -246,6 +306,24 @@ mmv_geom make_geom(const mi_mm_desc & m, int NC) {
 void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s) {
     const int nc = m.ne11 >= 5 ? 8 : (int) m.ne11;
     const mi_act_q8 act_or_x = act;
+    if (mi_mmv_order() != 0 && (m.type == 2 || m.type == 8)) {  // reference CPU order: 8 rows per wave
+        const bool q8 = m.type == 8;
+#define MI_MMV_ORD_LAUNCH(NC)                                                                               \
+        do {                                                                                                 \
+            const mmv_geom g = make_geom(m, NC);                                                             \
+            const dim3 grid((unsigned) ((m.N + 31) / 32), (unsigned) (g.col_chunks * m.ne12 * m.ne13));     \
+            if (q8) hipLaunchKernelGGL((k_mmv_q0_ord<NC, true>), grid, dim3(256), 0, s, (const uint8_t *) m.W, act, m.dst, g); \
+            else hipLaunchKernelGGL((k_mmv_q0_ord<NC, false>), grid, dim3(256), 0, s, (const uint8_t *) m.W, act, m.dst, g); \
+        } while (0)
+        switch (nc) {
+            case 1: MI_MMV_ORD_LAUNCH(1); break;
+            case 2: MI_MMV_ORD_LAUNCH(2); break;
+            case 3: case 4: MI_MMV_ORD_LAUNCH(4); break;
+            default: MI_MMV_ORD_LAUNCH(8); break;
+        }
+#undef MI_MMV_ORD_LAUNCH
+        return;
+    }
     switch (m.type) {
         case 12: MI_MMV_SWITCH(k_mmv_kq, false); break;  // Q4_K
         case 13: MI_MMV_SWITCH(k_mmv_kq, true); break;   // Q5_K
