@@ -2951,6 +2951,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.xfirst = value;
         return true;
     }
+    if (strcmp(name, "f16_nc") == 0 && value >= 0 && value <= 88 && value % 10 <= 8) {
+        g_mi_tuning.f16_nc = value;
+        return true;
+    }
     if (strcmp(name, "planes") == 0 && value >= 0 && value <= 1) {
         g_mi_tuning.planes = value;
         return true;

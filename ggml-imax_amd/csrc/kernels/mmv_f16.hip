@@ -710,6 +710,14 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
     const int64_t kp = (K + kKStep - 1) / kKStep * kKStep;
     int nc = ncols >= 8 ? 8 : ncols >= 3 ? 4 : (int) ncols;
     while (nc > 1 && (int64_t) nc * kp * 2 > 60000) nc /= 2;
+    // columns per workgroup capped by the knob f16_nc (not for lm_head; ones digit: the plain GEMVs,
+    // tens digit: those with the norm prologue; 0 = up to 8). Default 10: the norm GEMVs stage one
+    // column per workgroup, so every wave normalizes its own copy with no barrier (batched decode,
+    // 8 columns: 0.666-0.669 -> 0.650-0.657 ms/step; 2 or 4 columns per workgroup are slower, and so
+    // is one column for the plain GEMVs: profiles/r05nc_batched_cols_per_wg.txt)
+    const int nc_cap = pro.mode ? g_mi_tuning.f16_nc / 10 : g_mi_tuning.f16_nc % 10;
+    if (nc_cap > 0 && (N + 3) / 4 < 4096)
+        while (nc > 1 && nc > nc_cap) nc /= 2;
     // waves per workgroup (K split): about kWaves waves on the chip (~8 per CU), at most 8 per
     // workgroup and no more than the row's K steps, then as few as give the same steps per wave
     const int nit = (int) (kp / kKStep);
