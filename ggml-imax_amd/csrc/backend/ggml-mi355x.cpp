@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -704,8 +705,9 @@ static void * get_activations(mi_backend_ctx * ctx, const ggml_tensor * src1, in
 static void invalidate_activations(mi_backend_ctx * ctx, const ggml_tensor * written) {
     const char * lo = (const char *) written->data;
     const char * hi = lo + ggml_nbytes(written);
-    // a node writing into weight memory (through a view) renews the repacked planes over it
-    if (written->view_src && mi_planes_count() > 0) mi_planes_refresh(lo, (size_t) (hi - lo), ctx->stream);
+    // a node writing into memory that repacked planes mirror (weights written through a view, or a
+    // reused compute-buffer region that once held a Q4_K leaf) renews the planes over it
+    if (mi_planes_count() > 0) mi_planes_refresh(lo, (size_t) (hi - lo), ctx->stream);
     auto & c = ctx->act_cache;
     c.erase(std::remove_if(c.begin(), c.end(), [&](const mi_act_cache_entry & e) {
                 const char * elo = (const char *) e.data;
@@ -746,6 +748,12 @@ static const char * planes_of(mi_backend_ctx * ctx, const ggml_tensor * a, const
     if (!g_mi_tuning.planes || (a->type != GGML_TYPE_Q4_K && a->type != GGML_TYPE_Q5_K) || a->op != GGML_OP_NONE || a->ne[2] != 1 ||
         a->ne[3] != 1 || b->ne[1] * b->ne[2] * b->ne[3] < kMiPlanesMinCols || is_split_tensor(a))
         return nullptr;
+    // only tensors of this backend's own device buffers: host and peer memory have write paths
+    // (host-buffer set/clear, peer copies) that do not renew the planes. Within a device buffer every
+    // write path renews them: set/get/cpy/clear (sync and async) and any graph node whose output
+    // overlaps an entry (invalidate_activations), so a compute buffer's reused memory is covered too
+    const ggml_backend_buffer_t buf = a->view_src ? a->view_src->buffer : a->buffer;
+    if (!buffer_is_mi355x(buf) || ((mi_buffer_ctx *) buf->context)->device != ctx->device) return nullptr;
     return mi_planes_get(a->type, a->data, a->nb[1], a->ne[0], a->ne[1], ctx->stream);
 }
 
@@ -1890,11 +1898,15 @@ static int try_fuse_attn_proj(mi_backend_ctx * ctx, ggml_cgraph * g, int i, cons
 // Quantized prompt mul_mats in a reference-order graph (mmv_order 1, or -1 resolved to 1: a quantized
 // model's graph): the int8-MFMA prefill GEMMs compute the reference's exact integer block sums but
 // fold them in their own canonical order, and since every layer re-quantizes its activations an ulp
-// there becomes a quant step (~1e-2 of max|logit|). Up to g_ord_prefill_cols columns such a mul_mat
-// runs instead as the reference-order decode GEMV (k_mmv_stream ORD: the CPU's vec_dot lane chains,
-// bit-identical) over chunks of 8 columns -- each chunk re-reads the weights, so longer prompts keep
-// the MFMA GEMM. GGML_MI355X_ORD_PREFILL_COLS / set_tuning("ord_prefill_cols", n); 0 turns it off.
-static int g_ord_prefill_cols = getenv("GGML_MI355X_ORD_PREFILL_COLS") ? atoi(getenv("GGML_MI355X_ORD_PREFILL_COLS")) : 64;
+// there becomes a quant step (~1e-2 of max|logit|). Such a mul_mat -- any column count since round 6
+// -- runs instead as the reference-order streaming GEMV (k_mmv_stream ORD: the CPU's vec_dot lane
+// chains, bit-identical; ggml.c:12056-12096 runs every column through the same vec_dot) over
+// 8-column chunks, up to kMiMaxMembers chunks per launch: each chunk is a member of one grouped
+// launch over the same weight rows, so a 512-column prompt is one launch whose chunks re-read the
+// weights from the caches rather than 64 dependent launches. GGML_MI355X_ORD_PREFILL_COLS /
+// set_tuning("ord_prefill_cols", n) caps the column count (longer prompts take the MFMA GEMMs);
+// 0 turns it off.
+static int g_ord_prefill_cols = getenv("GGML_MI355X_ORD_PREFILL_COLS") ? atoi(getenv("GGML_MI355X_ORD_PREFILL_COLS")) : INT_MAX;
 
 static bool ord_prefill_chunked(const ggml_tensor * n) {
     if (n->op != GGML_OP_MUL_MAT || mi_mmv_order() != 1 || is_split_tensor(n->src[0])) return false;
@@ -1912,22 +1924,34 @@ static bool ord_prefill_chunked(const ggml_tensor * n) {
 static void run_ord_prefill_chunks(mi_backend_ctx * ctx, ggml_tensor * n) {
     const ggml_tensor * a = n->src[0];
     const ggml_tensor * b = n->src[1];
-    for (int64_t c0 = 0; c0 < b->ne[1]; c0 += 8) {
+    const int64_t ncols = b->ne[1];
+    const int64_t full = ncols / 8;  // 8-column chunks; the ragged tail (< 8 columns) is one more launch
+    auto launch = [&](int64_t c_first, int64_t nchunks, int cols) {
         mi_mmv_group g;
         g.type = a->type;
-        g.n = 1;
-        g.ncols = (int) std::min<int64_t>(8, b->ne[1] - c0);
+        g.n = (int) nchunks;
+        g.ncols = cols;
         g.K = a->ne[0];
         g.N = a->ne[1];
         g.nb01 = a->nb[1];
         g.xcol = b->nb[1];
         g.ycol = n->nb[1];
-        g.m[0].W = a->data;
-        g.m[0].X = (const char *) b->data + c0 * b->nb[1];
-        g.m[0].dst = (float *) ((char *) n->data + c0 * n->nb[1]);
+        for (int64_t k = 0; k < nchunks; k++) {
+            const int64_t c0 = c_first + 8 * k;
+            g.m[k].W = a->data;
+            g.m[k].X = (const char *) b->data + c0 * b->nb[1];
+            g.m[k].dst = (float *) ((char *) n->data + c0 * n->nb[1]);
+        }
         mi_mul_mat_q_fused(g, ctx->stream);
         ctx->last_launches++;
+    };
+    if (full > 0) {
+        // split evenly over launches of at most kMiMaxMembers chunks (as run_fused_group)
+        const int64_t runs = (full + kMiMaxMembers - 1) / kMiMaxMembers;
+        const int64_t take = (full + runs - 1) / runs;
+        for (int64_t k0 = 0; k0 < full; k0 += take) launch(8 * k0, std::min<int64_t>(take, full - k0), 8);
     }
+    if (ncols % 8) launch(8 * full, 1, (int) (ncols % 8));
 }
 
 // the activation kind of a MUL_MAT node that runs on an exact int8 prefill GEMM (Q4_K / Q5_K: 8,
@@ -2192,6 +2216,10 @@ static void graph_key(const mi_backend_ctx * ctx, const ggml_cgraph * g, std::ve
     k.push_back((uint64_t) (g->size == 0 && g->visited_hash_table.size == 0));  // mi_uses::partial
     k.push_back((uint64_t) (uintptr_t) ctx->scratch);
     k.push_back(ctx->scratch_gen);
+    // captured long-prompt GEMMs bake in the repacked planes' addresses (mi_mmx_member::planes): a
+    // planes entry created or dropped since (a weight buffer freed and another allocated at the same
+    // address) must not replay a graph that reads freed planes
+    k.push_back(mi_planes_generation());
     {
         uint64_t tw[(sizeof(mi_tuning) + 7) / 8] = {};
         memcpy(tw, &g_mi_tuning, sizeof(mi_tuning));
@@ -2675,6 +2703,7 @@ static void mi_backend_set_tensor_async(ggml_backend_t backend, ggml_tensor * te
     MI_ASSERT(buffer_is_mi355x(buf) && "unsupported buffer type");
     mi_device_guard g(ctx->device);
     MI_CHECK(hipMemcpyAsync((char *) tensor->data + offset, data, size, hipMemcpyHostToDevice, ctx->stream));
+    mi_planes_refresh((char *) tensor->data + offset, size, ctx->stream);  // repacked planes over these bytes, after the copy
 }
 
 static void mi_backend_get_tensor_async(ggml_backend_t backend, const ggml_tensor * tensor, void * data, size_t offset, size_t size) {
@@ -2695,6 +2724,7 @@ static bool mi_backend_cpy_tensor_async(ggml_backend_t backend_src, ggml_backend
     if (cs->device == cd->device) {
         mi_device_guard g(cs->device);
         MI_CHECK(hipMemcpyAsync(dst->data, src->data, ggml_nbytes(dst), hipMemcpyDeviceToDevice, cd->stream));
+        mi_planes_refresh(dst->data, ggml_nbytes(dst), cd->stream);
         return true;
     }
     // cross-device: copy on the source stream after its producers, destination waits on an event
@@ -2706,6 +2736,7 @@ static bool mi_backend_cpy_tensor_async(ggml_backend_t backend_src, ggml_backend
     {
         mi_device_guard g2(cd->device);
         MI_CHECK(hipStreamWaitEvent(cd->stream, ev, 0));
+        mi_planes_refresh(dst->data, ggml_nbytes(dst), cd->stream);  // on the destination, behind the copy
     }
     MI_CHECK(hipEventDestroy(ev));
     return true;

@@ -241,6 +241,7 @@ const char * mi_planes_get(int type, const void * W, size_t nb01, int64_t K, int
 void mi_planes_refresh(const void * lo, size_t bytes, hipStream_t s);
 void mi_planes_drop(const void * lo, size_t bytes);
 size_t mi_planes_count();
+uint64_t mi_planes_generation();  // changes whenever a planes entry is created or dropped (graph keys)
 size_t mi_planes_bytes();
 // the planes kernel over a group whose members all carry planes (false: not applicable)
 bool mi_mul_mat_mmqr_group(mi_mmx_group & g, hipStream_t s);

@@ -2147,8 +2147,12 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     const bool direct = (var & 16) || (ncols <= 128 && !(var & 128)) || !dst_local;
     if (direct) {
         const int S = (int) (K / 256);
-        const int64_t lim16 = (var & (1 << 22)) ? 128 : 16;  // bit 2^22: 16 x 16 tiles up to 128 columns
-        if (S <= 16 && ncols <= lim16 && !(var & (2048 | 4096 | (1 << 21)))) {  // 16 x 16 tiles (bit 2^21: 32 x 32 tiles)
+        // 16 x 16 tiles (k_mmqd16) only when asked: variant bit 2^21 up to 16 columns, 2^22 up to 128.
+        // Round 6 (profiles/r06a_short_prefill.txt, Q4_K / Q5_K 4096^2, 8 rotated weights): k_mmqp's
+        // 32 x 32 tiles are faster at B = 9 and 16 both grouped (Q4_K 3.98 / 4.07 vs 5.56 / 5.63 us per
+        // mul_mat) and alone in a graph (11.5 / 11.4 vs 12.0 / 12.0 us)
+        const int64_t lim16 = (var & (1 << 22)) ? 128 : (var & (1 << 21)) ? 16 : 0;
+        if (S <= 16 && ncols <= lim16 && !(var & (2048 | 4096))) {
             const dim3 grid16((unsigned) mmx_deal(g, 16, 16));
             const size_t lds16 = (size_t) S * 64 * 4 * sizeof(float) + (size_t) S * 16 * sizeof(float);
             if (type == 12) hipLaunchKernelGGL((k_mmqd16<12>), grid16, dim3(64 * S), lds16, s, g);

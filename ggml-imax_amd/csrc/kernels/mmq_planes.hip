@@ -293,6 +293,7 @@ struct PlanesEntry {
 std::mutex g_planes_mu;
 std::map<uintptr_t, PlanesEntry> g_planes;  // keyed by W
 std::atomic<size_t> g_planes_n{0};           // g_planes.size(), readable without the lock
+std::atomic<uint64_t> g_planes_gen{0};       // bumped whenever an entry is created or dropped
 
 int planes_enabled() { return g_mi_tuning.planes; }
 
@@ -340,6 +341,7 @@ const char * mi_planes_get(int type, const void * W, size_t nb01, int64_t K, int
     launch_repack(e, W, s);
     g_planes[(uintptr_t) W] = e;
     g_planes_n = g_planes.size();
+    g_planes_gen++;
     return e.planes;
 }
 
@@ -364,6 +366,7 @@ void mi_planes_drop(const void * lo, size_t bytes) {
         if (it->first >= a && it->first < b) {
             (void) hipFree(it->second.planes);
             it = g_planes.erase(it);
+            g_planes_gen++;
         } else {
             ++it;
         }
@@ -372,6 +375,8 @@ void mi_planes_drop(const void * lo, size_t bytes) {
 }
 
 size_t mi_planes_count() { return g_planes_n.load(std::memory_order_relaxed); }
+
+uint64_t mi_planes_generation() { return g_planes_gen.load(std::memory_order_relaxed); }
 
 size_t mi_planes_bytes() {
     std::lock_guard<std::mutex> lk(g_planes_mu);

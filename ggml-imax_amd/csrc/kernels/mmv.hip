@@ -264,6 +264,99 @@ __global__ __launch_bounds__(256) void k_mmv_q0_ord(const uint8_t * __restrict__
     }
 }
 
+// Reference-order Q4_K / Q5_K mul_mat for the shapes the fused stream kernel does not take (3-D
+// weight batches broadcast over r2 / r3, strided src1): the reference's AVX2 vec_dot
+// (ggml-quants.c:7089-7152 Q4_K, :7920-8002 Q5_K) keeps eight int32 lanes `sumi` per superblock,
+// lane l = sum over the four 64-element chunks j of sc[2j] * (4 low-nibble products at 4l..4l+3) +
+// sc[2j+1] * (4 high-nibble products), then acc[l] = fma(d, (float) sumi[l], acc[l]) with
+// d = y.d * fp16(x.d); the mins go to four f32 lanes acc_m[k] = fma(dmin, (float) (m[2k] S[2k] +
+// m[2k+1] S[2k+1]), acc_m[k]) (Q4_K; dmin = -y.d * fp16(x.dmin)), or to one scalar the -mfma build
+// contracts, summs = fma(dmin, (float) sum_k prod[k], summs) (Q5_K). Result hsum_float_8(acc) +
+// ((acc_m0 + acc_m2) + (acc_m1 + acc_m3)), resp. + summs. Here eight lanes are the eight CPU lanes
+// of one row (8 rows per wave), lanes 0..3 also the four acc_m lanes.
+template <int NC, bool Q5>
+__global__ __launch_bounds__(256) void k_mmv_kq_ord(const uint8_t * __restrict__ W, mi_act_q8 act, float * __restrict__ dst, mmv_geom g) {
+    const int l = threadIdx.x & 7;
+    const int64_t row = (int64_t) blockIdx.x * 32 + (threadIdx.x >> 3);
+    const bool live = row < g.N;
+    const int64_t rc = live ? row : g.N - 1;  // (dead groups run a valid row: no early exit before the shuffles)
+    int64_t i11, i12, i13, i02, i03;
+    mmv_coords(g, NC, i11, i12, i13, i02, i03);
+    constexpr int BS = Q5 ? 176 : 144;
+    const uint8_t * wrow = W + i02 * g.nb02 + i03 * g.nb03 + rc * g.nb01;
+    const int nsb = (int) (g.K / 256);
+    const int64_t col0 = i11 + g.ne11 * (i12 + g.ne12 * i13);
+
+    float A[NC], M[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) A[c] = M[c] = 0.0f;
+
+    for (int s = 0; s < nsb; s++) {
+        const uint8_t * blk = wrow + (size_t) s * BS;
+        const uint4 hdr = *(const uint4 *) blk;
+        const float dw = mi_h2f((uint16_t) (hdr.x & 0xFFFF));
+        const float dmw = mi_h2f((uint16_t) (hdr.x >> 16));
+        uint32_t qlo[4], qhi[4];
+        int sc[8], mn[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) mi_scale_min_k4(j, hdr.y, hdr.z, hdr.w, sc[j], mn[j]);
+        const uint32_t hb = Q5 ? *(const uint32_t *) (blk + 16 + 4 * l) : 0u;  // qh bytes 4l..4l+3
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t q = *(const uint32_t *) (blk + (Q5 ? 48 : 16) + 32 * j + 4 * l);
+            qlo[j] = q & 0x0F0F0F0Fu;
+            qhi[j] = (q >> 4) & 0x0F0F0F0Fu;
+            if constexpr (Q5) {
+                qlo[j] |= ((hb >> (2 * j)) & 0x01010101u) << 4;
+                qhi[j] |= ((hb >> (2 * j + 1)) & 0x01010101u) << 4;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && i11 + c >= g.ne11) break;
+            const int64_t col = col0 + c;
+            const int8_t * aq = act.qs + col * g.K + (int64_t) s * 256 + 4 * l;
+            int sumi = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int lo = mi_dot4((int) qlo[j], *(const int *) (aq + 64 * j), 0);
+                const int hi = mi_dot4((int) qhi[j], *(const int *) (aq + 64 * j + 32), 0);
+                sumi += sc[2 * j] * lo + sc[2 * j + 1] * hi;  // madd(scale_l, p16l) + madd(scale_h, p16h)
+            }
+            const float ya = act.d[col * nsb + s];
+            A[c] = fmaf(ya * dw, (float) sumi, A[c]);  // _mm256_fmadd_ps(d, cvt(sumi), acc)
+            const float dmin = -ya * dmw;
+            const int16_t * S = act.s32 + col * (g.K / 32) + (int64_t) s * 8;
+            if constexpr (!Q5) {
+                if (l < 4) {
+                    const int prod = mn[2 * l] * (int) S[2 * l] + mn[2 * l + 1] * (int) S[2 * l + 1];
+                    M[c] = fmaf(dmin, (float) prod, M[c]);  // _mm_fmadd_ps(dmin, cvt(prod), acc_m)
+                }
+            } else {
+                int tot = 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) tot += mn[j] * (int) S[j];
+                M[c] = fmaf(dmin, (float) tot, M[c]);  // summs += dmin * hsum(prod), contracted
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        // hsum_float_8: ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7))
+        float z = A[c] + __shfl_xor(A[c], 4, 8);
+        z = z + __shfl_xor(z, 2, 8);
+        z = z + __shfl_xor(z, 1, 8);
+        float m = M[c];
+        if constexpr (!Q5) {
+            // acc_m + movehl(acc_m), then lane 0 + lane 1: (m0 + m2) + (m1 + m3)
+            m = m + __shfl_xor(m, 2, 8);
+            m = m + __shfl_xor(m, 1, 8);
+        }
+        if (l == 0 && live && i11 + c < g.ne11)
+            *(float *) ((char *) dst + (i11 + c) * g.nb1 + i12 * g.nb2 + i13 * g.nb3 + row * sizeof(float)) = z + m;
+    }
+}
+
 mmv_geom make_geom(const mi_mm_desc & m, int NC) {
     mmv_geom g;
     g.K = m.K;
@@ -306,7 +399,7 @@ mmv_geom make_geom(const mi_mm_desc & m, int NC) {
 void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s) {
     const int nc = m.ne11 >= 5 ? 8 : (int) m.ne11;
     const mi_act_q8 act_or_x = act;
-    if (mi_mmv_order() != 0 && (m.type == 2 || m.type == 8)) {  // reference CPU order: 8 rows per wave
+    if (mi_mmv_order() == 1 && (m.type == 2 || m.type == 8)) {  // reference CPU order: 8 rows per wave (mode 2 is a timing ablation of the fused kernel only)
         const bool q8 = m.type == 8;
 #define MI_MMV_ORD_LAUNCH(NC)                                                                               \
         do {                                                                                                 \
@@ -322,6 +415,24 @@ void mi_mul_mat_q(const mi_mm_desc & m, const mi_act_q8 & act, hipStream_t s) {
             default: MI_MMV_ORD_LAUNCH(8); break;
         }
 #undef MI_MMV_ORD_LAUNCH
+        return;
+    }
+    if (mi_mmv_order() == 1 && (m.type == 12 || m.type == 13)) {  // reference CPU order, K-quants: 8 rows per wave
+        const bool q5 = m.type == 13;
+#define MI_MMV_KORD_LAUNCH(NC)                                                                               \
+        do {                                                                                                  \
+            const mmv_geom g = make_geom(m, NC);                                                              \
+            const dim3 grid((unsigned) ((m.N + 31) / 32), (unsigned) (g.col_chunks * m.ne12 * m.ne13));      \
+            if (q5) hipLaunchKernelGGL((k_mmv_kq_ord<NC, true>), grid, dim3(256), 0, s, (const uint8_t *) m.W, act, m.dst, g); \
+            else hipLaunchKernelGGL((k_mmv_kq_ord<NC, false>), grid, dim3(256), 0, s, (const uint8_t *) m.W, act, m.dst, g); \
+        } while (0)
+        switch (nc) {
+            case 1: MI_MMV_KORD_LAUNCH(1); break;
+            case 2: MI_MMV_KORD_LAUNCH(2); break;
+            case 3: case 4: MI_MMV_KORD_LAUNCH(4); break;
+            default: MI_MMV_KORD_LAUNCH(8); break;
+        }
+#undef MI_MMV_KORD_LAUNCH
         return;
     }
     switch (m.type) {

@@ -203,6 +203,7 @@ _SIGS = {
     "ggml_backend_buft_supports_backend": ([c_void_p, c_void_p], c_bool),
     "ggml_backend_tensor_set": ([T, c_void_p, c_size_t, c_size_t], None),
     "ggml_backend_tensor_get": ([T, c_void_p, c_size_t, c_size_t], None),
+    "ggml_backend_tensor_set_async": ([c_void_p, T, c_void_p, c_size_t, c_size_t], None),
     "ggml_backend_graph_compute": ([c_void_p, POINTER(ggml_cgraph)], c_int),
     "ggml_backend_graph_compute_async": ([c_void_p, POINTER(ggml_cgraph)], c_int),
     "ggml_backend_synchronize": ([c_void_p], None),

@@ -250,9 +250,14 @@ def test_quantized_gpt2_logits_bit_identical_to_reference_cpu(quantized_paths, q
 
 
 def _teacher_forced_prompt(ours, rm, n_batch, n_decode=4):
-    """A 3x PROMPT (> 64 tokens) in chunks of n_batch (so prompt mul_mats have up to n_batch columns),
-    then a few decode steps; returns per-step max rel error and bit-identical fraction."""
-    toks = ours.tokenize(" ".join([PROMPT] * 3))
+    """A repeated PROMPT (> 64 tokens, and longer than one n_batch chunk) in chunks of n_batch (so
+    prompt mul_mats have up to n_batch columns), then a few decode steps; returns per-step max rel
+    error and bit-identical fraction."""
+    reps = 3
+    toks = ours.tokenize(" ".join([PROMPT] * reps))
+    while len(toks) <= n_batch + 16:
+        reps += 3
+        toks = ours.tokenize(" ".join([PROMPT] * reps))
     assert len(toks) > 64
     n_past, errs, same = 0, [], []
     for i in range(0, len(toks), n_batch):
@@ -278,13 +283,14 @@ def _teacher_forced_prompt(ours, rm, n_batch, n_decode=4):
 @pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
 @pytest.mark.parametrize("qtype", ["q4_k", "q4_0"])
-@pytest.mark.parametrize("n_batch", [32, 64])
+@pytest.mark.parametrize("n_batch", [32, 64, 128, 512])
 def test_quantized_gpt2_prompt_path_bit_identical_to_reference_cpu(quantized_paths, qtype, n_batch):
-    """The quantized model's PROMPT path: prompts evaluated in chunks of 32 / 64 tokens (both sides
-    the same batching), so every projection is a mul_mat of up to 64 columns. With the default
+    """The quantized model's PROMPT path: prompts evaluated in chunks of 32 .. 512 tokens (both sides
+    the same batching), so every projection is a mul_mat of up to n_batch columns. With the default
     settings such a graph runs in the reference order (mmv_order -1 -> 1), and its quantized prompt
-    mul_mats of <= 64 columns take the reference-order GEMV in 8-column chunks instead of the MFMA
-    GEMM (ord_prefill_cols): every prompt and decode step's logits are the reference CPU's bits."""
+    mul_mats -- of any column count since round 6 -- take the reference-order streaming GEMV, 8
+    columns per grouped member, instead of the MFMA GEMM (ord_prefill_cols): every prompt and decode
+    step's logits are the reference CPU's bits."""
     lib = G.runtime()
     be = G.mi355x_backend(lib)
     ours = gpt2.Model(lib, quantized_paths[qtype], be, n_ctx=1024, n_batch=n_batch)
@@ -303,8 +309,8 @@ def test_quantized_gpt2_prompt_path_bit_identical_to_reference_cpu(quantized_pat
 @pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
 @pytest.mark.parametrize("qtype", ["q4_k", "q4_0"])
 def test_quantized_gpt2_mfma_prompt_path_deviation(quantized_paths, qtype):
-    """The same prompt through the exact int8-MFMA prefill GEMMs (ord_prefill_cols 0: the path
-    prompts longer than 64 columns take): exact integer block sums, own f32 fold order; the logits
+    """The same prompt through the exact int8-MFMA prefill GEMMs (ord_prefill_cols 0: the opt-out
+    from the reference-order prompt path): exact integer block sums, own f32 fold order; the logits
     then differ from the reference CPU's by the model's re-quantization sensitivity -- recorded
     here beside the reference's own 1-ulp sensitivity (1.7e-2 of max|logit|,
     test_reference_quantized_gpt2_is_ulp_sensitive) and bounded by the same 3e-2 as the tree-order
@@ -319,7 +325,7 @@ def test_quantized_gpt2_mfma_prompt_path_deviation(quantized_paths, qtype):
         print(f"{qtype}: MFMA prompt path max rel logit error {max(errs):.3e}")
         assert max(errs) <= 3e-2, errs
     finally:
-        lib.ggml_backend_mi355x_set_tuning(b"ord_prefill_cols", 64)
+        lib.ggml_backend_mi355x_set_tuning(b"ord_prefill_cols", 2 ** 31 - 1)
         ours.free()
         rm.free()
         lib.ggml_backend_free(be)

@@ -10,10 +10,11 @@ byte-identical to the reference's).
 
 * T = 5 tokens (the decode path, B <= 8): the backend's default settings run a graph whose quantized
   mul_mats consume computed values in the reference CPU's order, so the block is bit-identical.
-* T = 16 tokens (the prompt path: the Q/K/V and gate/up mul_mats go to the exact int8-MFMA GEMM as
-  grouped launches): every mul_mat is within 1e-5 of the reference, but each Q4_K mul_mat
-  re-quantizes its input (Q8_K), which turns an ulp into a quant step; the bar is the reference
-  harness's NMSE 5e-4 (test-backend-ops) on the block output.
+* T = 16, 96, 200 tokens (the prompt path): under the default settings the quantized prompt
+  mul_mats run the reference-order GEMV too, so the block is bit-identical at any length. The
+  opt-out (ord_prefill_cols 0) sends them to the exact int8-MFMA GEMM: every mul_mat within 1e-5 of
+  the reference, but each Q4_K mul_mat re-quantizes its input (Q8_K), which turns an ulp into a
+  quant step; that path is held to the reference harness's NMSE 5e-4 (test-backend-ops).
 """
 import os
 
@@ -120,17 +121,27 @@ def test_llama_block_prompt_path_bit_identical(libs):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+@pytest.mark.parametrize("T", [96, 200])
+def test_llama_block_long_prompt_bit_identical(libs, T):
+    """Prompts past 64 tokens under the default settings (round 6: the reference-order prompt path
+    has no column limit): the Q/K/V and gate/up Q4_K mul_mats of 96 / 200 columns run the
+    reference-order streaming GEMV, 8 columns per grouped member, so the whole block -- attention
+    over T keys included -- is the reference CPU's bits."""
+    a, b, _, _ = _run(libs, T)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 def test_llama_block_prompt_path_mfma_within_tolerance(libs):
-    """T = 16 through the exact int8-MFMA GEMMs (ord_prefill_cols 0, the path of prompts longer
-    than 64 columns): the reference harness's NMSE 5e-4 on the block output and a max-rel bound. Each
-    Q4_K mul_mat is within 1e-5 of the reference, but its input is re-quantized (Q8_K), which turns an
-    f32 fold-order ulp into a quant step."""
+    """The opt-out (ord_prefill_cols 0): T = 16 through the exact int8-MFMA GEMMs -- the reference
+    harness's NMSE 5e-4 on the block output and a max-rel bound. Each Q4_K mul_mat is within 1e-5 of
+    the reference, but its input is re-quantized (Q8_K), which turns an f32 fold-order ulp into a
+    quant step."""
     rt = libs[0]
     assert rt.ggml_backend_mi355x_set_tuning(b"ord_prefill_cols", 0)
     try:
         a, b, nmse, rel = _run(libs, 16)
     finally:
-        rt.ggml_backend_mi355x_set_tuning(b"ord_prefill_cols", 64)
+        rt.ggml_backend_mi355x_set_tuning(b"ord_prefill_cols", 2 ** 31 - 1)
     assert np.all(np.isfinite(a))
     assert nmse <= 5e-4
     assert rel <= 3e-2, rel

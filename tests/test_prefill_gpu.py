@@ -144,7 +144,7 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
     combined in the cfold order: 8 contiguous superblock groups, each left-folded; groups 0-3 and
     4-7 left-folded separately, then added), so any kernel choice gives the same bits: k_mmqp (the default for <= 128
     columns), k_mmqd1 (variant bit 2048), k_mmqx (full- and half-width workgroups) and, for <= 16
-    columns, k_mmqd16 (the default there; 16 x 16 tiles on the 16x16x64 MFMA). Q4_0 / Q8_0:
+    columns, k_mmqd16 (variant bit 2^21; 16 x 16 tiles on the 16x16x64 MFMA). Q4_0 / Q8_0:
     k_mmq0p (32 x 32 tiles, <= 64 columns) and k_mmq0x (weights staged per 64 x 128 workgroup)."""
     t = orc.TYPES_BY_NAME[tname]
     K, N = 4096, 320
@@ -356,6 +356,18 @@ def test_planes_follow_weight_writes(rt, backend, tname):
             assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
             y2 = G.tensor_get(rt, y)
             assert rel_err(y2, orc.mul_mat(t, mixed, K, N, x, B)) <= EXACT_TOL
+            # an ASYNC write on the backend's stream (ggml_backend_tensor_set_async) renews them too
+            mixed_a = mixed.copy()
+            lo2, hi2 = 150 * rb, 170 * rb
+            chunk = np.ascontiguousarray(wq[lo2:hi2])
+            mixed_a[lo2:hi2] = chunk
+            rt.ggml_backend_tensor_set_async(backend, w, chunk.ctypes.data, lo2, chunk.nbytes)
+            assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
+            rt.ggml_backend_synchronize(backend)
+            y2a = G.tensor_get(rt, y)
+            assert rel_err(y2a, orc.mul_mat(t, mixed_a, K, N, x, B)) <= EXACT_TOL
+            mixed = mixed_a
+            y2 = y2a
             assert rt.ggml_backend_mi355x_set_tuning(b"planes", 0)
             assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
             y3 = G.tensor_get(rt, y)
@@ -363,4 +375,65 @@ def test_planes_follow_weight_writes(rt, backend, tname):
         finally:
             rt.ggml_backend_mi355x_set_tuning(b"planes", 0)
             rt.ggml_backend_buffer_free(buf)
+    assert _planes_stats(rt)[0] == n0
+
+
+def _graph_stats(rt, be):
+    arr = (ctypes.c_int64 * 6)()
+    assert rt.ggml_backend_mi355x_graph_stats_ex(be, arr, 6) == 6
+    return list(arr)
+
+
+def test_planes_captured_graph_after_weight_realloc(rt, backend):
+    """Captured graphs bake in the repacked planes' address (mi_mmx_member::planes): a weight buffer
+    freed and a new one allocated -- usually at the same address, same shapes, so every tensor
+    address of the graph key repeats -- must not replay a capture that reads the freed planes
+    (the planes generation is part of the graph key). Two long-prompt mul_mats in a chain (4
+    launches: captured on the second compute, replayed on the third), each round with new weights,
+    bit-identical to the canonical kernels (planes off) on the same inputs."""
+    t = orc.Q4_K
+    K = N = 1024
+    B = 160
+    x = synth.uniform(91, K * B)
+
+    def run(wq, planes, reps):
+        ovh = rt.ggml_tensor_overhead() * 8 + rt.ggml_graph_overhead()
+        with G.Context(rt, ovh, no_alloc=True) as cw, G.Context(rt, ovh, no_alloc=True) as cc:
+            w = rt.ggml_new_tensor_2d(cw.ctx, t, K, N)
+            bw = rt.ggml_backend_alloc_ctx_tensors(cw.ctx, backend)
+            xt = rt.ggml_new_tensor_2d(cc.ctx, G.GGML_TYPE_F32, K, B)
+            y2 = rt.ggml_mul_mat(cc.ctx, w, rt.ggml_mul_mat(cc.ctx, w, xt))
+            g = rt.ggml_new_graph(cc.ctx)
+            rt.ggml_build_forward_expand(g, y2)
+            bc = rt.ggml_backend_alloc_ctx_tensors(cc.ctx, backend)
+            assert bw and bc
+            addr = rt.ggml_backend_buffer_get_base(bw)
+            try:
+                assert rt.ggml_backend_mi355x_set_tuning(b"planes", planes)
+                # (the chain's second mul_mat consumes a computed value: the per-graph order would pick
+                # the reference-order prompt path; the tree order keeps the MFMA GEMMs on the planes)
+                assert rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
+                G.tensor_set(rt, w, wq)
+                G.tensor_set(rt, xt, x)
+                outs = []
+                for _ in range(reps):
+                    assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
+                    outs.append(G.tensor_get(rt, y2))
+            finally:
+                rt.ggml_backend_mi355x_set_tuning(b"planes", 0)
+                rt.ggml_backend_mi355x_set_tuning(b"mmv_order", -1)
+                rt.ggml_backend_buffer_free(bc)
+                rt.ggml_backend_buffer_free(bw)
+            return outs, addr
+
+    n0, _ = _planes_stats(rt)
+    for seed in (92, 93):
+        wq = orc.quantize(t, synth.uniform(seed, K * N), K)
+        base, _ = run(wq, 0, 1)
+        s0 = _graph_stats(rt, backend)
+        outs, _ = run(wq, 1, 3)
+        s1 = _graph_stats(rt, backend)
+        assert s1[4] > s0[4], "the chain was never replayed from a capture: the case tests nothing"
+        for y in outs:
+            assert np.array_equal(y.view(np.uint32), base[0].view(np.uint32)), rel_err(y, base[0])
     assert _planes_stats(rt)[0] == n0
