@@ -1093,7 +1093,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
 // and 97 into dst as uint64 [2][2][80] (0 start, 1 after the prologue, 2 + 4 u + {0 step start, 1
 // after the MFMA steps, 2 after the combine, 3 after the DMA wait}); 1 no weight DMAs after the
 // prologue, 2 no combine, 4 no DMAs at all after the prologue (profiles/r04l_mmqt_stamps.txt).
-template <int TYPE, int ABL = 0>
+// HS (round 6): the two K halves synchronize separately. Each half's 36 pieces are issued by its own
+// four waves (9 each, as before) and the stage barrier is a per-half LDS counter (arrive after the
+// wave's DMAs and LDS reads have completed, spin until the half's four waves have arrived) instead of
+// the workgroup's s_barrier, so waves w and w + 4 -- the two waves of one SIMD, one of each half --
+// are no longer held in lock step: one half's combine (VALU) can run under the other half's MFMAs.
+// The halves have equal stage counts and meet at a full barrier before the final lo + hi.
+template <int TYPE, int ABL = 0, bool HS = false>
 __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -1111,6 +1117,7 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     constexpr int NI = 2 * NPIECE / 8;        // pieces per wave and stage (9)
     constexpr int SINK = 2 * SB;              // d_a DMAs of waves 2-7 land here
     __shared__ __attribute__((aligned(16))) char lds[SINK + DB];
+    __shared__ uint32_t hbar[2];              // HS: per-half arrival counters
 
     const int tid = (int) threadIdx.x;
     const int lane = tid & 63;
@@ -1132,7 +1139,8 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     uint32_t pstride[NI], poff[NI], pdst[NI];
 #pragma unroll
     for (int i = 0; i < NI; i++) {
-        const int q = w + 8 * i, hf = q / NPIECE, t = q % NPIECE;
+        const int q = w + 8 * i;
+        const int hf = HS ? kh : q / NPIECE, t = HS ? (w & 3) + 4 * i : q % NPIECE;
         pdst[i] = (uint32_t) (hf * HB + 1024 * t);
         if (t < 16) {  // activation quants: step kk, 32-column group cg
             const int kk = t >> 1, cg = t & 1, col = 32 * cg + (lane >> 1);
@@ -1161,10 +1169,15 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         if constexpr ((ABL & 1) != 0) if (u > 0 && i < NI && (w + 8 * i) % NPIECE >= 18) return;
         char * sbuf = lds + (u & 1) * SB;
         if (i < NI) {
-            const int hf = (w + 8 * i) / NPIECE;
+            const int hf = HS ? kh : (w + 8 * i) / NPIECE;
             const int sb = std::min(hf ? SK + u : u, S - 1);
             const char * src = pbase[i] + (size_t) sb * pstride[i] + poff[i];
             mi_glds16(src, mi_lds_addr(sbuf + pdst[i]));
+        } else if constexpr (HS) {  // wave 0 of each half its d_a, the others into the sink
+            const int sb = std::min(kh ? SK + u : u, S - 1);
+            const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
+            char * dd = (w & 3) ? lds + SINK : sbuf + kh * HB + XB + UB + WB;
+            mi_glds4(src, mi_lds_addr(dd));
         } else {
             const int sb = std::min(w == 1 ? SK + u : u, S - 1);
             const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
@@ -1189,6 +1202,21 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         stamp(stamp_slot);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
+    // HS: the half's barrier for the stage-u wait (u >= 1: the 4 u-th arrival of the half's waves)
+    auto half_wait = [&](int u) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        stamp(stamp_slot);
+        if (lane == 0) __hip_atomic_fetch_add(&hbar[kh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t target = 4u * (uint32_t) u;
+        // (bounded: every wave arrives once per stage, so the bound is never reached; it only keeps
+        // a fault from hanging the device)
+        for (int spin = 0; spin < (1 << 24) && __hip_atomic_load(&hbar[kh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target; spin++)
+            __builtin_amdgcn_s_sleep(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    if constexpr (HS) {
+        if (tid < 2) hbar[tid] = 0;  // (ordered before any arrival by the prologue's full barrier)
+    }
 
     // ---- compute: rows n0 + 32 rw + r of half kh; tiles ct = columns 32 ct ..
     const uint32_t xoff0 = (uint32_t) (r * 32 + 16 * (h ^ ((r >> 4) & 1)));  // tile 0; tile 1 at + 1024
@@ -1317,7 +1345,8 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
         stamp(3 + 4 * u);
         combine_stage(u & 1, sb0 + u);
         stamp(4 + 4 * u);
-        stage_wait();
+        if constexpr (HS) half_wait(u + 1);
+        else stage_wait();
     }
     if constexpr ((ABL & 8) != 0) {  // dst holds the stamps; keep the results alive
         float t = 0.0f;
@@ -1330,6 +1359,7 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     // the halves meet: waves 4-7 leave their sums in LDS (the stage buffers are idle: every DMA
     // has landed and every wave has passed the last barrier), waves 0-3 add and store
     f32x16 * ex = (f32x16 *) lds;
+    if constexpr (HS) mi_lds_barrier();  // the halves drift: both done with the stage buffers
     if (kh) {
         ex[(rw * 2 + 0) * 64 + lane] = y[0];
         ex[(rw * 2 + 1) * 64 + lane] = y[1];
@@ -1341,6 +1371,253 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
 #pragma unroll
     for (int ct = 0; ct < 2; ct++) {
         const f32x16 yv = y[ct] + ex[(rw * 2 + ct) * 64 + lane];  // cfold_end: lo + hi
+        // element el: prompt column c0 + 32 ct + (el & 3) + 8 (el >> 2) + 4 h
+#pragma unroll
+        for (int el = 0; el < 16; el++) {
+            const int64_t c = c0 + 32 * ct + (el & 3) + 8 * (el >> 2) + 4 * h;
+            if (c < ncols) *(float *) ((char *) dst + c * ycol + n * sizeof(float)) = yv[el];
+        }
+    }
+}
+
+// ---- long prompts, one wave per SIMD, software-pipelined: k_mmqv (round 6) --------------------------
+// k_mmqt's phases run in lock step per stage: every wave issues its MFMAs, then its combine (VALU),
+// and the two waves of a SIMD do so together (stamps: MFMA steps ~2500-3200 cycles, combine ~1800,
+// barrier ~1200 per stage, profiles/r04l_mmqt_stamps.txt; synchronizing the halves separately did not
+// separate them, profiles/r06d_mmqt_stamps.txt). Here one wave per SIMD (4 waves, 128 rows x 64
+// columns, each wave 32 rows x 64 columns over the WHOLE K) overlaps the two inside itself: the
+// combine of superblock s - 1 (T = (P1 << 3) + P0, t = fma(-dmin_w, U, d_w T): 4 VALU per element, no
+// branches) is issued between the MFMAs of superblock s, so the MFMA pipe hides the VALU latency
+// chains; only the group fold (cfold_vec: g = fma(d_a, t, g), group ends) runs on its own. Stage =
+// one superblock: activation quants [8][64][32] (swizzled halves), U halves, the 128 rows' raw
+// blocks, d_a (k_mmqt's half-stage image, 36.4 KB) by LDS-DMA, 4 buffers, issued two stages ahead (9
+// one-KB pieces + one d_a DMA per wave and stage: s_waitcnt vmcnt(10) leaves the next stage in
+// flight). Same operands, same canonical combine: bit-identical to every kernel of the family.
+template <int TYPE>
+__global__ __launch_bounds__(256, 1) void k_mmqv(mi_mmx_group grp) {
+    MI_MMX_MEMBER(grp);
+    using F = XFmt<TYPE>;
+    static_assert(!F::Q5, "Q4_K only");
+    constexpr int NP = F::NP;
+    constexpr int BM = 128, BN = 64;
+    constexpr int XB = 8 * BN * 32;           // activation quants of one superblock
+    constexpr int UB = BN * 32;               // U halves
+    constexpr int WB = BM * F::BS;            // raw weight blocks
+    constexpr int DB = BN * 4;                // d_a
+    constexpr int HB = XB + UB + WB + DB;     // a stage: [X | U | W | d_a]
+    constexpr int NBUF = 4;
+    constexpr int NPIECE = (XB + UB + WB) / 1024;  // 36
+    constexpr int NI = NPIECE / 4;            // 9 per wave
+    static_assert(NPIECE % 4 == 0, "pieces evenly dealt");
+    constexpr int SINK = NBUF * HB;
+    __shared__ __attribute__((aligned(16))) char lds[SINK + DB];
+
+    const int tid = (int) threadIdx.x;
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t ncols = act.ncols;
+    const int S = (int) (K / 256);
+    const int gs = cfold_gs(S);
+    const int64_t nrt = (N + BM - 1) / BM;
+    const int64_t n0 = (mmx_tile % nrt) * BM, c0 = (mmx_tile / nrt) * BN;
+    const int nrows = (int) std::min<int64_t>(BM, N - n0);
+    auto col_of = [&](int c) { return (uint32_t) std::min<int64_t>(c0 + c, ncols - 1); };
+
+    const char * pbase[NI];
+    uint32_t pstride[NI], poff[NI], pdst[NI];
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        const int t = w + 4 * i;
+        pdst[i] = (uint32_t) (1024 * t);
+        if (t < 16) {  // activation quants: step kk, 32-column group cg
+            const int kk = t >> 1, cg = t & 1, col = 32 * cg + (lane >> 1);
+            pbase[i] = (const char *) act.xq + (size_t) kk * ncols * 32;
+            pstride[i] = 8 * (uint32_t) ncols * 32;
+            poff[i] = col_of(col) * 32 + 16 * ((lane & 1) ^ ((lane >> 5) & 1));
+        } else if (t < 18) {  // U halves
+            const int col = 32 * (t - 16) + (lane >> 1);
+            pbase[i] = (const char *) act.xu;
+            pstride[i] = (uint32_t) ncols * 32;
+            poff[i] = col_of(col) * 32 + 16 * ((lane & 1) ^ ((lane >> 5) & 1));
+        } else {  // raw weight blocks: 1 KB of the [128 rows][BS] image
+            const int o = 1024 * (t - 18) + 16 * lane, row = o / F::BS;
+            pbase[i] = (const char *) W + (size_t) n0 * nb01;
+            pstride[i] = F::BS;
+            poff[i] = (uint32_t) (std::min(row, nrows - 1) * nb01 + o % F::BS);
+        }
+    }
+    const uint32_t doff = col_of(lane) * 4;
+    // stage u (clamped: past the end re-reads the last superblock into an idle buffer) into buffer u % 4
+    auto stage_piece = [&](int u, int i) {
+        char * sbuf = lds + (u % NBUF) * HB;
+        const int sb = std::min(u, S - 1);
+        if (i < NI) {
+            mi_glds16(pbase[i] + (size_t) sb * pstride[i] + poff[i], mi_lds_addr(sbuf + pdst[i]));
+        } else {
+            const char * src = (const char *) act.xd + (size_t) sb * ncols * 4 + doff;
+            mi_glds4(src, mi_lds_addr(w ? lds + SINK : sbuf + XB + UB + WB));
+        }
+    };
+
+    const uint32_t xoff0 = (uint32_t) (r * 32 + 16 * (h ^ ((r >> 4) & 1)));  // tile 0; tile 1 at + 1024
+    const uint32_t woff = (uint32_t) (XB + UB + (32 * w + r) * F::BS);
+    f32x16 g[2] = {}, y[2] = {f32x16(-0.0f), f32x16(-0.0f)}, lo[2] = {f32x16(-0.0f), f32x16(-0.0f)};
+    i32x16 accA[2][NP], accB[2][NP];
+
+    // U of superblock sb (its stage buffer) on the f16 MFMA (A = [S & 63, S >> 6] of the lane's
+    // column, B = [m, 64 m] of its row); returns d_w, dmin_w of the row
+    auto u_of = [&](int sb, f32x16 (&Uo)[2]) {
+        const char * base = lds + (sb % NBUF) * HB;
+        const uint4 hdr = *(const uint4 *) (base + woff);
+        const uint32_t ma = hdr.z & 0x3F3F3F3Fu;
+        const uint32_t mb = ((hdr.w >> 4) & 0x0F0F0F0Fu) | ((hdr.z >> 2) & 0x30303030u);
+        const uint32_t mw = h ? mb : ma;
+        half8 mu;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t m = (mw >> (8 * q)) & 0xFF;
+            mu[2 * q] = (_Float16) (float) m;
+            mu[2 * q + 1] = (_Float16) (float) (64 * m);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            const half8 xu = *(const half8 *) (base + XB + xoff0 + 1024 * ct);
+            Uo[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xu, mu, f32x16{}, 0, 0, 0);
+        }
+        return std::make_pair(mi_h2f((uint16_t) (hdr.x & 0xFFFF)), mi_h2f((uint16_t) (hdr.x >> 16)));
+    };
+
+    // superblock u: its MFMAs into acc; the previous superblock's t values (accp; when `pre`)
+    // computed between the MFMA steps into tv; the stage two ahead's DMAs behind the steps
+    auto body = [&](auto pre_c, int u, i32x16 (&acc)[2][NP], const i32x16 (&accp)[2][NP], f32x16 (&tv)[2]) {
+        constexpr bool pre = decltype(pre_c)::value;
+        const char * base = lds + (u % NBUF) * HB;
+        const char * wr = base + woff;
+        f32x16 Up[2];
+        float dwp = 0.0f, dmp = 0.0f;
+        if constexpr (pre) {
+            const auto dd = u_of(u - 1, Up);
+            dwp = dd.first;
+            dmp = dd.second;
+        }
+        const uint4 hdr = *(const uint4 *) wr;
+        uint4 q4[4];
+#pragma unroll
+        for (int p = 0; p < 4; p++) q4[p] = *(const uint4 *) (wr + 16 + 32 * p + 16 * h);
+        const uint32_t w0 = hdr.y, w2 = hdr.w;
+        const uint32_t sca = w0 & 0x3F3F3F3Fu;
+        const uint32_t scb = (w2 & 0x0F0F0F0Fu) | ((w0 >> 2) & 0x30303030u);
+        uint32_t lq[4], hq[4];
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const i32x4 xa0 = *(const i32x4 *) (base + kk * (BN * 32) + xoff0);
+            const i32x4 xa1 = *(const i32x4 *) (base + kk * (BN * 32) + 1024 + xoff0);
+            if ((kk & 1) == 0) {
+                const uint4 q = q4[kk >> 1];
+                const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    lq[e] = qv[e] & 0x0F0F0F0Fu;
+                    hq[e] = (qv[e] >> 4) & 0x0F0F0F0Fu;
+                }
+            }
+            const uint32_t scw = kk < 4 ? sca : scb;
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                const uint32_t f = __builtin_amdgcn_ubfe(scw, 8 * (kk & 3) + 3 * p, 3);
+                const uint32_t * v = (kk & 1) ? hq : lq;
+                const i32x4 b = {(int) mulb(v[0], f), (int) mulb(v[1], f), (int) mulb(v[2], f), (int) mulb(v[3], f)};
+                acc[0][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa0, b, kk == 0 ? i32x16{} : acc[0][p], 0, 0, 0);
+                acc[1][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa1, b, kk == 0 ? i32x16{} : acc[1][p], 0, 0, 0);
+            }
+            // the previous superblock's values of elements 2 kk, 2 kk + 1 (both tiles)
+            if constexpr (pre) {
+#pragma unroll
+                for (int ct = 0; ct < 2; ct++) {
+#pragma unroll
+                    for (int e = 0; e < 2; e++) {
+                        const int el = 2 * kk + e;
+                        const int T = (accp[ct][1][el] << F::SHIFT) + accp[ct][0][el];
+                        tv[ct][el] = mmqx_pre(T, Up[ct][el], dwp, dmp);
+                    }
+                }
+            }
+            // the stage two ahead: one piece behind each step (steps 0..NI-1), the d_a DMA after the last
+            if (kk < NI) stage_piece(u + 2, kk);
+        }
+#pragma unroll
+        for (int i = 8; i <= NI; i++) stage_piece(u + 2, i);
+    };
+    // the last superblock's values (after its MFMAs, no next superblock to hide them under)
+    auto last_pre = [&](int sb, const i32x16 (&accp)[2][NP], f32x16 (&tv)[2]) {
+        f32x16 Up[2];
+        const auto dd = u_of(sb, Up);
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+            for (int el = 0; el < 16; el++) {
+                const int T = (accp[ct][1][el] << F::SHIFT) + accp[ct][0][el];
+                tv[ct][el] = mmqx_pre(T, Up[ct][el], dd.first, dd.second);
+            }
+    };
+    // the fold of superblock sb's values tv (d_a from its stage buffer)
+    auto fold = [&](int sb, const f32x16 (&tv)[2]) {
+        const float * dal = (const float *) (lds + (sb % NBUF) * HB + XB + UB + WB);
+#pragma unroll
+        for (int ct = 0; ct < 2; ct++) {
+            f32x16 dv;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const float2 d2 = *(const float2 *) &dal[32 * ct + 8 * (j >> 1) + 4 * h + 2 * (j & 1)];
+                dv[2 * j] = d2.x;
+                dv[2 * j + 1] = d2.y;
+            }
+            cfold_vec(g[ct], y[ct], lo[ct], tv[ct], dv, sb, gs, S);
+        }
+    };
+    auto stage_wait = [&] {
+        asm volatile("s_waitcnt vmcnt(10)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+
+    // prologue: stages 0 and 1 in flight
+#pragma unroll
+    for (int i = 0; i <= NI; i++) stage_piece(0, i);
+#pragma unroll
+    for (int i = 0; i <= NI; i++) stage_piece(1, i);
+    f32x16 tv[2];
+    using no_pre = std::integral_constant<bool, false>;
+    using with_pre = std::integral_constant<bool, true>;
+    stage_wait();
+    body(no_pre{}, 0, accA, accB, tv);
+    if (S == 1) {
+        last_pre(0, accA, tv);
+        fold(0, tv);
+    }
+    for (int u = 1; u < S; u += 2) {
+        stage_wait();
+        body(with_pre{}, u, accB, accA, tv);
+        fold(u - 1, tv);
+        if (u + 1 >= S) {  // the last superblock from accB
+            last_pre(u, accB, tv);
+            fold(u, tv);
+            break;
+        }
+        stage_wait();
+        body(with_pre{}, u + 1, accA, accB, tv);
+        fold(u, tv);
+        if (u + 2 >= S) {  // the last superblock from accA
+            last_pre(u + 1, accA, tv);
+            fold(u + 1, tv);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the clamped DMAs past the end have landed)
+
+    const int64_t n = n0 + 32 * w + r;
+    if (n >= N) return;
+#pragma unroll
+    for (int ct = 0; ct < 2; ct++) {
+        const f32x16 yv = cfold_end_vec(lo[ct], y[ct]);
         // element el: prompt column c0 + 32 ct + (el & 3) + 8 (el >> 2) + 4 h
 #pragma unroll
         for (int el = 0; el < 16; el++) {
@@ -2235,8 +2512,13 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     // combine deferred into the next step too: 36.9 vs 35.4 us, r04t_mmqt_split2_ab.txt -- all
     // removed)
     const int lng = g_mi_tuning.mmq_long;
-    if ((!MI_DIAG || lng == 0 || lng == 2) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
+    if ((!MI_DIAG || lng == 0 || lng == 2 || lng == 3 || lng == 4) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
+#if MI_DIAG  // measured slower (round 6, profiles/r06e_mmqv_prefill.txt): diagnostic builds only
+        if (lng == 3) hipLaunchKernelGGL((k_mmqt<12, 0, true>), gridt, dim3(512), 0, s, g);  // per-half stage sync
+        else if (lng == 4) hipLaunchKernelGGL((k_mmqv<12>), gridt, dim3(256), 0, s, g);  // one wave per SIMD, pipelined
+        else
+#endif
         hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
         return;
     }
@@ -2248,6 +2530,7 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
             case 2: hipLaunchKernelGGL((k_mmqt<12, 10>), gridt, dim3(512), 0, s, g); break;
             case 4: hipLaunchKernelGGL((k_mmqt<12, 12>), gridt, dim3(512), 0, s, g); break;
             case 6: hipLaunchKernelGGL((k_mmqt<12, 14>), gridt, dim3(512), 0, s, g); break;
+            case 7: hipLaunchKernelGGL((k_mmqt<12, 8, true>), gridt, dim3(512), 0, s, g); break;  // per-half sync, stamps
             default: hipLaunchKernelGGL((k_mmqt<12, 8>), gridt, dim3(512), 0, s, g); break;
         }
         return;

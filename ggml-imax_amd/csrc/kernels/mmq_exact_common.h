@@ -74,6 +74,7 @@ __device__ __forceinline__ void cfold(float & g, float & y, float & lo, float t,
     }
 }
 __device__ __forceinline__ float cfold_end(float lo, float y) { return lo + y; }
+__device__ __forceinline__ f32x16 cfold_end_vec(const f32x16 & lo, const f32x16 & y) { return lo + y; }
 // the same for a whole accumulator (sb wave-uniform) without per-element selects; the resets are
 // uniform branches kept as branches (the empty asm stops their if-conversion into 16 v_cndmask
 // per superblock)

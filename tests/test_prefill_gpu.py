@@ -177,10 +177,13 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
         assert np.array_equal(outs[v].view(np.uint32), outs[0].view(np.uint32)), (v, rel_err(outs[v], outs[0]))
 
 
+@pytest.mark.parametrize("lng", [2, 3, 4])
 @pytest.mark.parametrize("K,N,B", [(256, 64, 130), (1280, 96, 257), (3072, 200, 200), (11008, 256, 136), (4096, 4096, 512)])
-def test_split_k_prefill_bit_equal(rt, backend, K, N, B):
+def test_split_k_prefill_bit_equal(rt, backend, K, N, B, lng):
     """k_mmqt (mmq_long 2, the Q4_K kernel past 128 columns without repacked planes: the two K
-    halves of the canonical order on two waves, met in LDS) forced onto
+    halves of the canonical order on two waves, met in LDS; diagnostic builds also mmq_long 3, the
+    same with each half's stages synchronized on its own, and 4, k_mmqv: one wave per SIMD over the
+    whole K with the combine software-pipelined under the next superblock's MFMAs) forced onto
     ragged shapes: one superblock (empty high half), S = 5 (a one-superblock high half), S = 12,
     S = 43 (a high half shorter than the low: idle steps), ragged rows and columns; bit-identical to
     the default kernel (k_mmqr on the planes) and within the exact-path tolerance of the oracle."""
@@ -191,7 +194,8 @@ def test_split_k_prefill_bit_equal(rt, backend, K, N, B):
     try:
         base = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
         assert rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", 128 | 131072)
-        assert rt.ggml_backend_mi355x_set_tuning(b"mmq_long", 2)
+        if not rt.ggml_backend_mi355x_set_tuning(b"mmq_long", lng):
+            pytest.skip("mmq_long %d: diagnostic builds only (measured slower)" % lng)
         y = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
     finally:
         rt.ggml_backend_mi355x_set_tuning(b"mmq_variant", 0)

@@ -2,7 +2,8 @@
 diaglib`, GGML_MI355X_BACKEND_LIB=ggml-imax_amd/lib/diag/libggml_mi355x.so; results invalid).
 Q4_K 4096 x 4096 x B (default 512): per K step of waves 0 (low half) and 4 (high half) of workgroups
 0 and 97: cycles of the MFMA steps (with the next stage's DMAs behind them), the combine, the wait
-for the DMAs, and the barrier. argv[2]: ablation bits (1 no weight DMAs, 2 no combine, 4 no DMAs)."""
+for the DMAs, and the barrier. argv[2]: ablation bits (1 no weight DMAs, 2 no combine, 4 no DMAs;
+7: the per-half synchronized form, mmq_long 3, without ablations)."""
 import os, sys
 import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
