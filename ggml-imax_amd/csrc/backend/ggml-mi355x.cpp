@@ -2945,6 +2945,11 @@ int ggml_backend_mi355x_graph_stats_ex(ggml_backend_t backend, int64_t * stats, 
 }
 
 bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
+    if (strcmp(name, "mmv_dma") == 0 && (value == 0 || (mi_diag_build() && ((value >= 1 && value <= 3) || (value >= 11 && value <= 13))))) {
+        // (diagnostic builds only: measured slower than k_mmv_stream, profiles/r06h_gemv_lds_dma_ab.txt)
+        g_mi_tuning.mmv_dma = value;
+        return true;
+    }
     if (strcmp(name, "mmv_blocks") == 0 && value >= 0) {
         g_mi_tuning.mmv_blocks = value;
         return true;

@@ -184,6 +184,19 @@ struct FmtKQ {
     template <int NC>
     __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
         const int s = item >> 2, j = item & 3;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) s * 256 + 64 * j);
+            const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            const int alo[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const int ahi[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            const int ss = *(const int *) (a.s32 + c * (K / 32) + s * 8 + 2 * j);
+            acc[c] = item_dot(r, j, alo, ahi, ss, a.d[c * (K / 256) + s], acc[c]);
+        }
+    }
+    // one item (superblock s, 64-group j) of one column, the column's quants / 32-sums / scale given
+    __device__ static __forceinline__ float item_dot(const Regs & r, int j, const int (&alo)[8], const int (&ahi)[8], int ss, float ad, float acc) {
         const uint32_t q[8] = {r.qa.x, r.qa.y, r.qa.z, r.qa.w, r.qb.x, r.qb.y, r.qb.z, r.qb.w};
         uint32_t qlo[8], qhi[8];
         if constexpr (Q5) {
@@ -218,27 +231,19 @@ struct FmtKQ {
             m0 = (int) (((x2 >> 4) & 0xF) | (((x1 >> 6) & 3) << 4));
             m1 = (int) (((x2 >> 12) & 0xF) | (((x1 >> 14) & 3) << 4));
         }
+        int lo = 0, hi = 0;
 #pragma unroll
-        for (int c = 0; c < NC; c++) {
-            if (NC > 1 && c >= ncols) break;
-            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) s * 256 + 64 * j);
-            const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-            const int alo[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            const int ahi[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-            int lo = 0, hi = 0;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                lo = mi_dot4((int) qlo[i], alo[i], lo);
-                hi = mi_dot4((int) qhi[i], ahi[i], hi);
-            }
-            const int ss = *(const int *) (a.s32 + c * (K / 32) + s * 8 + 2 * j);
-            // sc*lo + sc*hi and m*bsum + m*bsum in f32 are exact (|.| < 2^24: 63*32*31*127 and
-            // 63*32*128 per term), i.e. (float) of the reference's int32 sums, without the
-            // quarter-rate 32-bit integer multiplies
-            const float sumi = fmaf((float) sc1, (float) hi, (float) sc0 * (float) lo);
-            const float summ = fmaf((float) m1, (float) (ss >> 16), (float) m0 * (float) (int) (int16_t) (ss & 0xFFFF));
-            acc[c] += a.d[c * (K / 256) + s] * (dw * sumi - dmw * summ);
+        for (int i = 0; i < 8; i++) {
+            lo = mi_dot4((int) qlo[i], alo[i], lo);
+            hi = mi_dot4((int) qhi[i], ahi[i], hi);
         }
+        // sc*lo + sc*hi and m*bsum + m*bsum in f32 are exact (|.| < 2^24: 63*32*31*127 and
+        // 63*32*128 per term), i.e. (float) of the reference's int32 sums, without the
+        // quarter-rate 32-bit integer multiplies
+        const float sumi = fmaf((float) sc1, (float) hi, (float) sc0 * (float) lo);
+        const float summ = fmaf((float) m1, (float) (ss >> 16), (float) m0 * (float) (int) (int16_t) (ss & 0xFFFF));
+        // explicit fmas (the file contracts freely): the same bits in every kernel that inlines this
+        return fmaf(ad, fmaf(-dmw, summ, dw * sumi), acc);
     }
 
     // CPU order (see ord_* below): per item (superblock s, 64-group j) the reference's eight int32
@@ -951,6 +956,157 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     MI_STAMP(g.stamps, 7);
 }
 
+// ------------------------------------------------------------------ LDS-DMA weight stream (round 6)
+#if MI_DIAG
+// k_mmv_dma: the tree-order Q4_K GEMV of one column with the weights moved by LDS-DMA. Measured
+// (profiles/r06h_gemv_lds_dma_ab.txt, headline workload): 5.6-6.0 TB/s against k_mmv_stream's
+// 6.2-6.3 on the same box (nt 3-7 % faster than the default policy); diagnostic builds only.
+// Design:
+// (global_load_lds_dwordx4, 1 KB per wave-instruction, every weight byte fetched exactly once --
+// k_mmv_stream's lanes load each 16-byte superblock header four times) into wave-private rings,
+// optionally with the nontemporal policy (NT; the guide's nt-weights row: LDS-DMA streams reach
+// 6.5-6.8 TB/s chip-wide nt, 6.4 default, MI355X_MICROARCH.md "ldsdma-fill"). Wave w of a workgroup
+// owns a contiguous run of rows, i.e. a contiguous byte stream (rows of 144 K / 256 bytes, packed);
+// a ring slot is a group of 4 rows = 9 x 1 KB pieces for K = 4096 (GR = 4 rows x BS x K / 256 / 1024
+// pieces; K = 4096 only, as the waits' immediates assume), G slots, G - 1 groups in flight. The dot products read the
+// slot with ds_read_b128 and use FmtKQ's arithmetic (the same per-item sums and wave reduction as
+// k_mmv_stream: the same bits); the 4 rows' results leave as one 16-byte store by lane 0. The DMAs
+// are inline asm outside the compiler's vmcnt bookkeeping: per group a wave issues exactly GR DMAs
+// and one store, so "group g landed" is s_waitcnt vmcnt((G - 1) (GR + 1)).
+__device__ __forceinline__ uint32_t mi_lds_addr_u8(const uint8_t * p) {  // LDS byte address, wave-uniform
+    return (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (uintptr_t) p);
+}
+__device__ __forceinline__ void mi_glds16_nt(const void * gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds));
+}
+__device__ __forceinline__ void mi_glds16_dflt(const void * gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds));
+}
+template <int G> struct dma_wait;
+template <> struct dma_wait<2> { __device__ static void run() { asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); } };
+template <> struct dma_wait<3> { __device__ static void run() { asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); } };
+template <> struct dma_wait<4> { __device__ static void run() { asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); } };
+
+constexpr int kDmaRowsPerGroup = 4;
+
+template <int NW, int G, bool NT>
+__global__ __launch_bounds__(64 * NW) void k_mmv_dma(mi_mmv_group g) {
+    using F = FmtKQ<false>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int64_t K = 4096;
+    constexpr int nsl = K / 256;
+    constexpr int RB = nsl * F::BS;                   // row bytes (rows packed: nb01 == RB)
+    constexpr int GB = kDmaRowsPerGroup * RB;         // group bytes
+    constexpr int GR = GB / 1024;                     // DMA pieces per group
+    static_assert(GB % 1024 == 0 && GR == 9, "dma_wait assumes 9 pieces + 1 store per group");
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int member = blockIdx.x / g.blocks_per_member;
+    const int rb = blockIdx.x - member * g.blocks_per_member;
+    const uint8_t * W = (const uint8_t *) g.m[member].W;
+    const char * X = g.m[member].X;
+    float * dst = g.m[member].dst;
+    const lds_act act = lds_carve<256>(lds, 1, K);
+    uint8_t * ring = lds + ord_offset(lds_bytes<256>(1, K)) + (size_t) wave * G * GB;
+
+    // rows of this workgroup, then of this wave (contiguous, whole groups except the member's last)
+    const int Nr = (int) g.N;
+    const int row_begin = rb * (int) g.rows_per_block;
+    const int row_end = min(row_begin + (int) g.rows_per_block, Nr);
+    const int rpw = (int) g.rows_per_block / NW;  // a multiple of kDmaRowsPerGroup (launcher)
+    const int r0 = min(row_begin + wave * rpw, row_end), r1 = min(r0 + rpw, row_end);
+    const int ngroups = (r1 - r0 + kDmaRowsPerGroup - 1) / kDmaRowsPerGroup;
+    const uint8_t * wbase = W + (size_t) r0 * RB;
+    const uint8_t * wlast = W + (size_t) Nr * RB - 16;  // (clamp: pieces past the member's end re-read its last bytes)
+    auto issue = [&](int grp) {
+        const int gc = grp < ngroups ? grp : (ngroups > 0 ? ngroups - 1 : 0);  // (past the end: the last group again)
+        const uint8_t * src = wbase + (size_t) gc * GB + 16 * lane;
+        const uint32_t dsts = mi_lds_addr_u8(ring + (grp % G) * GB);
+#pragma unroll
+        for (int p = 0; p < GR; p++) {
+            const uint8_t * a = src + 1024 * p;
+            a = a < wlast ? a : wlast;
+            if constexpr (NT) mi_glds16_nt(a, dsts + 1024 * p);
+            else mi_glds16_dflt(a, dsts + 1024 * p);
+        }
+    };
+
+    // activations: the column's slices quantized into LDS by every wave (as k_mmv_stream), requested
+    // before the first groups' DMAs
+    auto load_round = [&](float4 (&v)[4], int p0) {
+        const int p = min(p0 + (lane >> 4), nsl - 1);
+        const float4 * src = (const float4 *) (X + ((size_t) p * 256 + (lane & 15) * 16) * sizeof(float));
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = src[u];
+    };
+    float4 xfirst[4];
+    load_round(xfirst, 4 * wave);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the compiler does not count the DMAs below)
+    for (int grp = 0; grp < G - 1; grp++) issue(grp);
+    for (int p0 = 4 * wave; p0 < nsl; p0 += 4 * NW) {
+        float4 v[4];
+        if (p0 == 4 * wave) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = xfirst[u];
+        } else {
+            load_round(v, p0);
+        }
+        const int p = min(p0 + (lane >> 4), nsl - 1);
+        quantize_row16(v, lane, act, K, 0, p, p0 + (lane >> 4) < nsl);
+    }
+    __syncthreads();
+    // this lane's item (superblock s, 64-group j) is the same in every row: its activation operands
+    // stay in registers
+    const int s = lane >> 2, j = lane & 3;
+    int alo[8], ahi[8];
+    {
+        const int4 * p = (const int4 *) (act.qs + (int64_t) s * 256 + 64 * j);
+        const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+        const int l8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const int h8[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            alo[i] = l8[i];
+            ahi[i] = h8[i];
+        }
+    }
+    const int ss = *(const int *) (act.s32 + s * 8 + 2 * j);
+    const float ad = act.d[s];
+    const uint32_t ioff = (uint32_t) (s * F::BS);
+
+    // stream: group grp in slot grp % G; its refill (group grp + G - 1) issued first
+    for (int grp = 0; grp < ngroups; grp++) {
+        issue(grp + G - 1);
+        dma_wait<G>::run();
+        const uint8_t * slot = ring + (grp % G) * GB + ioff;
+        typename F::Regs rg[kDmaRowsPerGroup];
+#pragma unroll
+        for (int r = 0; r < kDmaRowsPerGroup; r++) {
+            rg[r].hdr = *(const uint4 *) (slot + r * RB);
+            rg[r].qa = *(const uint4 *) (slot + r * RB + 16 + 32 * j);
+            rg[r].qb = *(const uint4 *) (slot + r * RB + 32 + 32 * j);
+        }
+        float res[kDmaRowsPerGroup];
+#pragma unroll
+        for (int r = 0; r < kDmaRowsPerGroup; r++) res[r] = mi_wave_sum_u(F::item_dot(rg[r], j, alo, ahi, ss, ad, 0.0f));
+        const int row = r0 + kDmaRowsPerGroup * grp;
+        if (lane == 0) {
+            if (row + kDmaRowsPerGroup <= r1) {
+                *(float4 *) (dst + row) = make_float4(res[0], res[1], res[2], res[3]);
+            } else {
+                for (int r = 0; r < kDmaRowsPerGroup; r++)
+                    if (row + r < r1) dst[row + r] = res[r];
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the re-read DMAs past the end have landed)
+}
+#endif  // MI_DIAG
+
 // Workgroups that fit on the chip at once for this kernel instance (all of them are launched
 // in one wave, so no workgroup waits for another to retire). Speed only: nothing relies on
 // co-residency. Cached per kernel.
@@ -1045,6 +1201,42 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
                        s, g);
 }
 
+#if MI_DIAG
+// k_mmv_dma for a group (tree order, one column, packed Q4_K rows, K = 4096); false: not taken.
+// mmv_dma: 1 = 4 waves x 3 slots, 2 = 8 waves x 2 slots, 3 = 4 waves x 4 slots (+10: default load
+// policy instead of nontemporal); one workgroup per CU
+bool launch_dma(mi_mmv_group g, hipStream_t s) {
+    const int v = g_mi_tuning.mmv_dma;
+    const int64_t RB = g.K / 256 * 144;
+    if (g.K != 4096 || (int64_t) g.nb01 != RB || g.N >= (1 << 30)) return false;  // (9 pieces per group: the waits' immediates)
+    for (int i = 0; i < g.n; i++)
+        if (((uintptr_t) g.m[i].dst | (uintptr_t) g.m[i].W) % 16 != 0) return false;
+    const int shape = v % 10;
+    const bool nt = v < 10;
+    const int NW = shape == 2 ? 8 : 4, G = shape == 2 ? 2 : shape == 3 ? 4 : 3;
+    const size_t lds = ord_offset(lds_bytes<256>(1, g.K)) + (size_t) NW * G * 4 * RB;
+    if (lds > 160 * 1024) return false;
+    const int target = mi_cu_count();
+    int bpm = target / g.n;
+    if (bpm < 1) bpm = 1;
+    int64_t rows = (g.N + bpm - 1) / bpm;
+    const int64_t unit = (int64_t) NW * kDmaRowsPerGroup;
+    rows = (rows + unit - 1) / unit * unit;
+    g.rows_per_block = rows;
+    g.blocks_per_member = (int) ((g.N + rows - 1) / rows);
+    const void * fn;
+#define MI_DMA_K(NW_, G_, NT_) (const void *) k_mmv_dma<NW_, G_, NT_>
+    if (NW == 8) fn = nt ? MI_DMA_K(8, 2, true) : MI_DMA_K(8, 2, false);
+    else if (G == 4) fn = nt ? MI_DMA_K(4, 4, true) : MI_DMA_K(4, 4, false);
+    else fn = nt ? MI_DMA_K(4, 3, true) : MI_DMA_K(4, 3, false);
+#undef MI_DMA_K
+    (void) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    const dim3 grid((unsigned) (g.blocks_per_member * g.n)), block((unsigned) (64 * NW));
+    void * args[] = {&g};
+    return hipLaunchKernel(fn, grid, block, args, lds, s) == hipSuccess;
+}
+#endif  // MI_DIAG
+
 template <class F, int NC, int PD, int IPL, bool ORD, bool XF = false>
 void launch_tail(const mi_mmv_group & g, hipStream_t s) {
     if (g.K / F::ITEM > 64 * IPL) launch_one<F, NC, PD, IPL, true, ORD, false, XF>(g, s);
@@ -1062,6 +1254,11 @@ void launch_stream(const mi_mmv_group & g, int variant, hipStream_t s) {
     // them: 5.45 -> 4.95 us per graph without it (profiles/r05xf_xfirst_ab.txt)
     const bool xf = g.n == 1 && g_mi_tuning.xfirst == 1;
     const bool pro_epi = g.pro.mode || e.bias || e.resid || e.gelu_table || e.copy[0].ptr || e.copy[1].ptr;
+#if MI_DIAG  // measured slower (profiles/r06h_gemv_lds_dma_ab.txt): diagnostic builds only
+    if constexpr (NC == 1 && !ORD && std::is_same<F, FmtKQ<false>>::value) {
+        if (!pro_epi && g_mi_tuning.mmv_dma > 0 && launch_dma(g, s)) return;
+    }
+#endif
     if constexpr (NC == 1) {
         // tall lone members with rows of <= 16 items (GPT-2 lm_head: 50257 x 768, 12 Q4_K items per
         // row): four rows per wave step on 16 lanes each (MR = 4); variant 9x: the one-row form
