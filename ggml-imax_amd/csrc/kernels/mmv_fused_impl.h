@@ -195,6 +195,30 @@ struct FmtKQ {
             acc[c] = item_dot(r, j, alo, ahi, ss, a.d[c * (K / 256) + s], acc[c]);
         }
     }
+    // one column's operands of an item, held in registers across rows (the item of a lane is the
+    // same in every row)
+    struct Act {
+        int alo[8], ahi[8];
+        int ss;
+        float ad;
+    };
+    __device__ static __forceinline__ void act_load(Act & v, int item, const lds_act & a, int64_t K) {
+        const int s = item >> 2, j = item & 3;
+        const int4 * p = (const int4 *) (a.qs + (int64_t) s * 256 + 64 * j);
+        const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+        const int l8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const int h8[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            v.alo[i] = l8[i];
+            v.ahi[i] = h8[i];
+        }
+        v.ss = *(const int *) (a.s32 + s * 8 + 2 * j);
+        v.ad = a.d[s];
+    }
+    __device__ static __forceinline__ float dot_act(const Regs & r, int item, const Act & v, float acc) {
+        return item_dot(r, item & 3, v.alo, v.ahi, v.ss, v.ad, acc);
+    }
     // one item (superblock s, 64-group j) of one column, the column's quants / 32-sums / scale given
     __device__ static __forceinline__ float item_dot(const Regs & r, int j, const int (&alo)[8], const int (&ahi)[8], int ss, float ad, float acc) {
         const uint32_t q[8] = {r.qa.x, r.qa.y, r.qa.z, r.qa.w, r.qb.x, r.qb.y, r.qb.z, r.qb.w};
@@ -387,20 +411,44 @@ struct FmtQ0 {
             const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 32);
             const int4 a0 = p[0], a1 = p[1];
             const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            int sumi = 0;
-            if constexpr (Q8) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) sumi = mi_dot4((int) t[i], av[i], sumi);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    sumi = mi_dot4((int) (t[i] & 0x0F0F0F0Fu), av[i], sumi);
-                    sumi = mi_dot4((int) ((t[i] >> 4) & 0x0F0F0F0Fu), av[i + 4], sumi);
-                }
-                sumi -= 8 * (int) a.s32[c * (K / 32) + item];  // (q - 8) * y
-            }
-            acc[c] += (float) sumi * (dw * a.d[c * (K / 32) + item]);
+            acc[c] = block_dot(t, dw, av, Q8 ? 0 : (int) a.s32[c * (K / 32) + item], a.d[c * (K / 32) + item], acc[c]);
         }
+    }
+    __device__ static __forceinline__ float block_dot(const uint32_t (&t)[NQ], float dw, const int (&av)[8], int s32, float da, float acc) {
+        int sumi = 0;
+        if constexpr (Q8) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) sumi = mi_dot4((int) t[i], av[i], sumi);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                sumi = mi_dot4((int) (t[i] & 0x0F0F0F0Fu), av[i], sumi);
+                sumi = mi_dot4((int) ((t[i] >> 4) & 0x0F0F0F0Fu), av[i + 4], sumi);
+            }
+            sumi -= 8 * s32;  // (q - 8) * y
+        }
+        return fmaf((float) sumi, dw * da, acc);
+    }
+    struct Act {
+        int av[8];
+        int s32;
+        float da;
+    };
+    __device__ static __forceinline__ void act_load(Act & v, int item, const lds_act & a, int64_t K) {
+        const int4 * p = (const int4 *) (a.qs + (int64_t) item * 32);
+        const int4 a0 = p[0], a1 = p[1];
+        const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int i = 0; i < 8; i++) v.av[i] = av[i];
+        v.s32 = Q8 ? 0 : (int) a.s32[item];
+        v.da = a.d[item];
+    }
+    __device__ static __forceinline__ float dot_act(const Regs & r, int, const Act & v, float acc) {
+        uint32_t t[NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; i++) t[i] = r.off ? r.w[i + 1] : __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], 2);
+        const uint32_t dbits = (r.off ? r.w[0] >> 16 : r.w[0]) & 0xFFFF;
+        return block_dot(t, mi_h2f((uint16_t) dbits), v.av, v.s32, v.da, acc);
     }
 
     // CPU order: the reference's eight int32 lanes l of mul_sum_i8_pairs_float -- elements 4l..4l+3
@@ -496,21 +544,49 @@ struct FmtQ0Pair {
             const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
             const int av0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
             const int av1[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-            int s0 = 0, s1 = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                s0 = mi_dot4((int) (t0[i] & 0x0F0F0F0Fu), av0[i], s0);
-                s0 = mi_dot4((int) ((t0[i] >> 4) & 0x0F0F0F0Fu), av0[i + 4], s0);
-                s1 = mi_dot4((int) (r.w[i + 5] & 0x0F0F0F0Fu), av1[i], s1);
-                s1 = mi_dot4((int) ((r.w[i + 5] >> 4) & 0x0F0F0F0Fu), av1[i + 4], s1);
-            }
             const uint32_t ss = *(const uint32_t *) (a.s32 + c * (K / 32) + 2 * item);  // both blocks' sums
-            s0 -= 8 * (int) (int16_t) (ss & 0xFFFF);
-            s1 -= 8 * (int) (int16_t) (ss >> 16);
             const float2 da = *(const float2 *) (a.d + c * (K / 32) + 2 * item);
-            acc[c] += (float) s0 * (dw0 * da.x);
-            acc[c] += (float) s1 * (dw1 * da.y);
+            acc[c] = pair_dot(r, t0, dw0, dw1, av0, av1, ss, da, acc[c]);
         }
+    }
+    __device__ static __forceinline__ float pair_dot(const Regs & r, const uint32_t (&t0)[4], float dw0, float dw1, const int (&av0)[8],
+                                                     const int (&av1)[8], uint32_t ss, float2 da, float acc) {
+        int s0 = 0, s1 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            s0 = mi_dot4((int) (t0[i] & 0x0F0F0F0Fu), av0[i], s0);
+            s0 = mi_dot4((int) ((t0[i] >> 4) & 0x0F0F0F0Fu), av0[i + 4], s0);
+            s1 = mi_dot4((int) (r.w[i + 5] & 0x0F0F0F0Fu), av1[i], s1);
+            s1 = mi_dot4((int) ((r.w[i + 5] >> 4) & 0x0F0F0F0Fu), av1[i + 4], s1);
+        }
+        s0 -= 8 * (int) (int16_t) (ss & 0xFFFF);
+        s1 -= 8 * (int) (int16_t) (ss >> 16);
+        acc = fmaf((float) s0, dw0 * da.x, acc);
+        return fmaf((float) s1, dw1 * da.y, acc);
+    }
+    struct Act {
+        int av0[8], av1[8];
+        uint32_t ss;
+        float2 da;
+    };
+    __device__ static __forceinline__ void act_load(Act & v, int item, const lds_act & a, int64_t K) {
+        const int4 * p = (const int4 *) (a.qs + (int64_t) item * 64);
+        const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+        const int av0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const int av1[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            v.av0[i] = av0[i];
+            v.av1[i] = av1[i];
+        }
+        v.ss = *(const uint32_t *) (a.s32 + 2 * item);
+        v.da = *(const float2 *) (a.d + 2 * item);
+    }
+    __device__ static __forceinline__ float dot_act(const Regs & r, int, const Act & v, float acc) {
+        uint32_t t0[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) t0[i] = __builtin_amdgcn_alignbyte(r.w[i + 1], r.w[i], 2);
+        return pair_dot(r, t0, mi_h2f((uint16_t) (r.w[0] & 0xFFFF)), mi_h2f((uint16_t) (r.w[4] >> 16)), v.av0, v.av1, v.ss, v.da, acc);
     }
 };
 
@@ -845,7 +921,18 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                 }
             }
         }
-    } else
+    } else {
+    // (one column, tree order: the lane's items are the same in every row, so their activation
+    // operands are read from LDS once, here, instead of per row)
+    constexpr bool AREG = NC == 1 && !ORD && !TAIL;
+    typename F::Act areg[AREG ? IPL : 1];
+    if constexpr (AREG) {
+#pragma unroll
+        for (int i = 0; i < IPL; i++) {
+            const int item = lane + 64 * i;
+            F::act_load(areg[i], item < nitems ? item : nitems - 1, act, K);
+        }
+    }
     // 3) stream: ring slot u holds row k0+u; refill it with row k0+u+PD right before using it
     //    (the last row again past the end: an L2 hit)
     for (int k0 = 0; k0 < nrows; k0 += NB) {
@@ -932,7 +1019,11 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
 #pragma unroll
             for (int i = 0; i < IPL; i++) {
                 const int item = lane + 64 * i;
-                if (item < nitems) F::template dot<NC>(ring[u][i], item, act, K, ncols, acc);
+                if constexpr (AREG) {
+                    if (item < nitems) acc[0] = F::dot_act(ring[u][i], item, areg[i], acc[0]);
+                } else {
+                    if (item < nitems) F::template dot<NC>(ring[u][i], item, act, K, ncols, acc);
+                }
             }
             if constexpr (TAIL) {
                 // items beyond the ring's IPL per lane, loaded in-line (long rows only: a loop
@@ -951,6 +1042,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
             }
             if (k == 0) MI_STAMP(g.stamps, 3);  // first row reduced and stored
         }
+    }
     }
     if (!(PRO && g.pro.mode)) MI_STAMP_CLK(g.stamps, 5);
     MI_STAMP(g.stamps, 7);
