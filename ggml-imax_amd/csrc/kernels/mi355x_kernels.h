@@ -139,6 +139,7 @@ struct mi_tuning {
     int planes;       // long Q4_K prompts on repacked MFMA planes (mmq_planes.hip k_mmqr): 1 on, 0 off (default: slower than k_mmqt with HBM-streamed weights)
     int f16_nc;       // F16 decode GEMVs: columns per workgroup at most (ones digit: plain, tens: norm prologue; 0: up to 8)
     int mmv_dma;      // grouped tree-order Q4_K GEMVs on the LDS-DMA weight stream (k_mmv_dma): 0 off, 1-3 shapes, +10 default load policy
+    int f16_bn;       // F16 decode GEMVs, 2..8 columns with the norm prologue (K <= 1024) on k_gemv_f16_bn: 0 off, 1-5 shapes (default 5), +10 one column too
 };
 extern mi_tuning g_mi_tuning;
 // the order of the graph being launched when mmv_order is -1 (set by the backend per graph)

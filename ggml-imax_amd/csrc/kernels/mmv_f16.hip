@@ -646,6 +646,114 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
     MI_STAMP(e.stamps, 7);
 }
 
+// Several columns (2..8) with the norm prologue (round 6; batched decode's c_attn / c_fc, K <= 1024):
+// one workgroup of NW waves normalizes every column ONCE -- wave w the columns w, w + NW, ..., all of
+// a wave's columns requested together with g and b (shared by the columns) -- into f16 LDS, and its
+// waves then stream 4 rows each over the whole K with every row's chunks requested at kernel entry
+// (before the norm), reading the columns back as 16-byte broadcast reads. The one-column-per-
+// workgroup form (f16_nc 10, the default before) normalized each column in N / 4 workgroups and
+// re-read every weight row once per column; staging all columns in the row-group kernel serialized
+// the norms (k_gemv_f16 with 8 columns, ~0.9 us per column). Same per-element arithmetic (norm_store,
+// dot8, row16_sum): tree order, within the F16 tolerance of the reference.
+// KS > 1: the KS waves of a 4-row group split the row's chunks (wave part p takes chunks i = p mod KS)
+// and their partial sums meet in LDS, added in part order.
+template <int EPI, int JM, int NW, int KS = 1>
+__global__ __launch_bounds__(64 * NW) void k_gemv_f16_bn(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                        mi_src_cols x, int64_t ncols, float * __restrict__ dst, size_t ycol,
+                                                        mi_f16_epilogue e, mi_norm_prologue pro, int64_t kp) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [8][kp] f16, then [NW][4][8] f32 partials
+    constexpr int CPW = (8 + NW - 1) / NW;  // columns per wave
+    constexpr int NCH = JM * 256 / (kLpr * kChunk) / KS;  // 16-byte chunks per lane and row (K <= 256 JM)
+    MI_STAMP(e.stamps, 0);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int m = lane & (kLpr - 1), rg = lane >> 4;
+    const int grp = wid / KS, part = wid % KS;
+    const int64_t row = ((int64_t) blockIdx.x * (NW / KS) + grp) * 4 + rg;
+    const bool live = row < N;
+    const int nc = (int) std::min<int64_t>(8, ncols);
+    const int64_t k8 = K / kChunk;
+
+    // the wave's columns, g and b first (vmcnt retires in order), then the rows' weight chunks
+    float4 pv[CPW][JM], pg[JM], pb[JM];
+#pragma unroll
+    for (int j = 0; j < CPW; j++) {
+        const int c = wid + NW * j;
+        const float * xc = (const float *) (x.base + (c < nc ? c : nc - 1) * x.nb1);
+        if (j == 0) {
+            norm_load<JM, true>(xc, K, lane, pro, pv[0], pg, pb);
+        } else {
+            float4 dg[1], db[1];
+            norm_load<JM, false>(xc, K, lane, pro, pv[j], dg, db);
+        }
+    }
+    asm volatile("" ::: "memory");
+    const uint8_t * wrow = W + (live ? row : 0) * nb01;
+    uint4 cur[NCH];
+#pragma unroll
+    for (int i = 0; i < NCH; i++) {
+        const int64_t c = (int64_t) (i * KS + part) * kLpr + m;
+        cur[i] = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);  // (zeroed past K at use)
+    }
+    asm volatile("" ::: "memory");
+    float e_bias = 0.0f, e_res = 0.0f;
+    {
+        const int64_t rc = live ? row : 0, cc = m < nc ? m : nc - 1;
+        if (EPI >= 1) e_bias = e.bias[rc];
+        if (EPI == 2) e_res = *(const float *) (e.resid + cc * e.resid_nb1 + rc * sizeof(float));
+    }
+#pragma unroll
+    for (int j = 0; j < CPW; j++) {
+        const int c = wid + NW * j;
+        if (c < nc) norm_store<JM, true>(pv[j], pg, pb, K, kp, pro, xs + (size_t) c * kp, lane);
+    }
+    MI_STAMP(e.stamps, 1);
+    mi_lds_barrier();
+
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) acc[c] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NCH; i++) {
+        const int64_t k = ((int64_t) (i * KS + part) * kLpr + m) * kChunk;
+        const uint4 w = keep_if(k < K, cur[i]);
+        if (k < kp) {
+#pragma unroll
+            for (int c = 0; c < 8; c++)
+                if (c < nc) acc[c] = dot8(w, *(const uint4 *) (xs + (size_t) c * kp + k), acc[c]);
+        }
+    }
+    MI_STAMP(e.stamps, 3);
+    float mine = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        const float t = row16_sum(acc[c]);
+        if (m == c) mine = t;
+    }
+    if constexpr (KS > 1) {
+        float * red = (float *) (xs + (size_t) 8 * kp);
+        if (m < 8) red[(wid * 4 + rg) * 8 + m] = mine;
+        mi_lds_barrier();
+        if (part != 0) return;
+        if (m < 8) {
+            for (int p = 1; p < KS; p++) mine += red[((wid + p) * 4 + rg) * 8 + m];
+        }
+    }
+    if (live && m < nc) {
+        const int64_t col = m;
+        float v = mine;
+        if (EPI >= 1) v = v + e_bias;
+        if (EPI == 2) v = v + e_res;
+        if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
+        *(float *) ((char *) dst + col * ycol + row * sizeof(float)) = v;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (e.copy[k].ptr && row >= e.copy[k].row0 && row < e.copy[k].row1)
+                *(float *) (e.copy[k].ptr + col * e.copy[k].col_stride + (row - e.copy[k].row0) * sizeof(float)) = v;
+        }
+    }
+    MI_STAMP(e.stamps, 7);
+}
+
 template <int NC, int U, bool ONE, int JM>
 void launch_nc(const void * W, size_t nb01, int64_t K, int64_t N, const mi_src_cols & x, const uint16_t * xh, int64_t ncols, float * dst,
                size_t ycol, const mi_f16_epilogue & e, const mi_norm_prologue & pro, hipStream_t s, int ks, int rgs) {
@@ -790,6 +898,25 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         }
 #undef MI_GEMV_PS_E
 #undef MI_GEMV_PS
+    } else if (pro.mode && (ncols > 1 || g_mi_tuning.f16_bn >= 10) && K <= 1024 && g_mi_tuning.f16_bn > 0) {
+        // several columns with the norm prologue: normalized once per workgroup (k_gemv_f16_bn)
+        // f16_bn: 1 = 4 waves, 2 = 8 waves, 3 = 8 waves with K split over wave pairs, 4 = 8 waves K split
+        // over 4, 5 = 16 waves K split over 4
+        const int bn = g_mi_tuning.f16_bn % 10;  // (+10: one column too)
+        const int NWv = bn == 5 ? 16 : bn >= 2 ? 8 : 4, KSv = bn == 3 ? 2 : bn >= 4 ? 4 : 1;
+        const dim3 grid((unsigned) ((N + 4 * (NWv / KSv) - 1) / (4 * (NWv / KSv))));
+        const size_t lds = (size_t) 8 * kp * sizeof(uint16_t) + (size_t) NWv * 4 * 8 * sizeof(float);
+        const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
+        const uint8_t * w = (const uint8_t *) W;
+        mi_f16_epilogue es = e;
+        es.stamps = mi_stamp_take("k_gemv_f16_bn", grid.x);
+#define MI_GEMV_BN(EP, NWV, KSV) hipLaunchKernelGGL((k_gemv_f16_bn<EP, 4, NWV, KSV>), grid, dim3(64 * NWV), lds, s, w, nb01, K, N, x, ncols, dst, ycol, es, pro, kp)
+#define MI_GEMV_BN_E(NWV, KSV) switch (epi) { case 0: MI_GEMV_BN(0, NWV, KSV); break; case 1: MI_GEMV_BN(1, NWV, KSV); break; \
+                                                  case 2: MI_GEMV_BN(2, NWV, KSV); break; default: MI_GEMV_BN(3, NWV, KSV); break; }
+        if (bn == 5) { MI_GEMV_BN_E(16, 4) } else if (bn == 4) { MI_GEMV_BN_E(8, 4) } else if (KSv == 2) { MI_GEMV_BN_E(8, 2) }
+        else if (NWv == 8) { MI_GEMV_BN_E(8, 1) } else { MI_GEMV_BN_E(4, 1) }
+#undef MI_GEMV_BN_E
+#undef MI_GEMV_BN
     } else if (pro.mode) {  // supported() guarantees one pass (K <= 3072)
         if (K <= 1024) launch_one<4>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
         else launch_one<12>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);

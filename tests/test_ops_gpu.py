@@ -469,3 +469,44 @@ def test_per_node_timer_fills_perf_fields(capfd):
     finally:
         lib.ggml_backend_mi355x_set_perf(be, False)
         lib.ggml_backend_free(be)
+
+
+@pytest.mark.parametrize("bn", [0, 1, 3, 5])
+@pytest.mark.parametrize("K,N,ncols,epi", [(768, 2304, 8, "bias"), (768, 3072, 5, "gelu"), (512, 200, 2, "none"), (1024, 96, 3, "bias")])
+def test_norm_prologue_gemv_columns(libs, bn, K, N, ncols, epi):
+    """norm -> mul(g) -> add(b) -> F16 mul_mat (+ bias, + GELU) of 2..8 columns, the batched-decode
+    shape of GPT-2's c_attn / c_fc (main-batched.cpp): in tree order one launch whose prologue
+    normalizes the columns (f16_bn 1-5: k_gemv_f16_bn, every column normalized once per workgroup,
+    4 / 8 / 16 waves, K split over 1 / 2 / 4 waves; 0: the earlier k_gemv_f16 forms) -- within the
+    F16 decode tolerance (1e-3 rel) of the reference CPU, and the shapes agree with each other."""
+    rt = libs[0]
+    x = rnd(40 + K, K * ncols, 2.0)
+    g = rnd(41, K, 1.0) + np.float32(1.0)
+    bb = rnd(42, K, 0.1)
+    w = (rnd(43, K * N, 0.05)).astype(np.float16)
+    bias = rnd(44, N, 0.2)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_2d(c, F32, K, ncols)
+        gt = L.ggml_new_tensor_1d(c, F32, K)
+        bt = L.ggml_new_tensor_1d(c, F32, K)
+        wt = L.ggml_new_tensor_2d(c, F16, K, N)
+        bi = L.ggml_new_tensor_1d(c, F32, N)
+        h = L.ggml_add(c, L.ggml_mul(c, L.ggml_norm(c, t, 1e-5), gt), bt)
+        y = L.ggml_mul_mat(c, wt, h)
+        if epi != "none":
+            y = L.ggml_add(c, y, bi)
+        if epi == "gelu":
+            y = L.ggml_gelu(c, y)
+        return [(t, x), (gt, g), (bt, bb), (wt, w), (bi, bias)], y
+
+    try:
+        assert rt.ggml_backend_mi355x_set_tuning(b"f16_bn", bn)
+        assert rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
+        a, b = both(libs, build)
+    finally:
+        rt.ggml_backend_mi355x_set_tuning(b"f16_bn", 5)
+        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", -1)
+    rel = float(np.abs(a.astype(np.float64) - b).max() / np.abs(b).max())
+    print(f"f16_bn={bn} K={K} N={N} cols={ncols} {epi}: max rel {rel:.2e}")
+    assert rel <= 1e-3
