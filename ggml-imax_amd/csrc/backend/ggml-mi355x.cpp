@@ -2950,6 +2950,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.mmv_dma = value;
         return true;
     }
+    if (strcmp(name, "f16_bp") == 0 && (value == 0 || (value == 1 && mi_diag_build()))) {  // (1: measured slower, diagnostic builds)
+        g_mi_tuning.f16_bp = value;
+        return true;
+    }
     if (strcmp(name, "f16_bn") == 0 && value >= 0 && value % 10 <= 5 && value <= 15) {
         g_mi_tuning.f16_bn = value;
         return true;

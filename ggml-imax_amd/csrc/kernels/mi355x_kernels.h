@@ -140,6 +140,7 @@ struct mi_tuning {
     int f16_nc;       // F16 decode GEMVs: columns per workgroup at most (ones digit: plain, tens: norm prologue; 0: up to 8)
     int mmv_dma;      // grouped tree-order Q4_K GEMVs on the LDS-DMA weight stream (k_mmv_dma): 0 off, 1-3 shapes, +10 default load policy
     int f16_bn;       // F16 decode GEMVs, 2..8 columns with the norm prologue (K <= 1024) on k_gemv_f16_bn: 0 off, 1-5 shapes (default 5), +10 one column too
+    int f16_bp;       // F16 decode GEMVs, 2..8 plain columns (K <= 3072) on k_gemv_f16_bn's staging form: 0 off, 1 on
 };
 extern mi_tuning g_mi_tuning;
 // the order of the graph being launched when mmv_order is -1 (set by the backend per graph)

@@ -657,13 +657,16 @@ __global__ __launch_bounds__(512) void k_gemv_f16_ps(const uint8_t * __restrict_
 // dot8, row16_sum): tree order, within the F16 tolerance of the reference.
 // KS > 1: the KS waves of a 4-row group split the row's chunks (wave part p takes chunks i = p mod KS)
 // and their partial sums meet in LDS, added in part order.
-template <int EPI, int JM, int NW, int KS = 1>
+// JM == 0 (plain, no norm: batched decode's c_proj / mlp projection): every thread stages the f32
+// columns to f16 LDS (stage_cols) instead; NCHT = 16-byte chunks per lane and row (K <= 128 NCHT).
+template <int EPI, int JM, int NW, int KS = 1, int NCHT = JM * 2>
 __global__ __launch_bounds__(64 * NW) void k_gemv_f16_bn(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
                                                         mi_src_cols x, int64_t ncols, float * __restrict__ dst, size_t ycol,
                                                         mi_f16_epilogue e, mi_norm_prologue pro, int64_t kp) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [8][kp] f16, then [NW][4][8] f32 partials
     constexpr int CPW = (8 + NW - 1) / NW;  // columns per wave
-    constexpr int NCH = JM * 256 / (kLpr * kChunk) / KS;  // 16-byte chunks per lane and row (K <= 256 JM)
+    constexpr int NCH = NCHT / KS;           // 16-byte chunks per lane and row of this wave
+    constexpr int JMV = JM > 0 ? JM : 1;
     MI_STAMP(e.stamps, 0);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int m = lane & (kLpr - 1), rg = lane >> 4;
@@ -674,16 +677,18 @@ __global__ __launch_bounds__(64 * NW) void k_gemv_f16_bn(const uint8_t * __restr
     const int64_t k8 = K / kChunk;
 
     // the wave's columns, g and b first (vmcnt retires in order), then the rows' weight chunks
-    float4 pv[CPW][JM], pg[JM], pb[JM];
+    float4 pv[CPW][JMV], pg[JMV], pb[JMV];
+    if constexpr (JM > 0) {
 #pragma unroll
-    for (int j = 0; j < CPW; j++) {
-        const int c = wid + NW * j;
-        const float * xc = (const float *) (x.base + (c < nc ? c : nc - 1) * x.nb1);
-        if (j == 0) {
-            norm_load<JM, true>(xc, K, lane, pro, pv[0], pg, pb);
-        } else {
-            float4 dg[1], db[1];
-            norm_load<JM, false>(xc, K, lane, pro, pv[j], dg, db);
+        for (int j = 0; j < CPW; j++) {
+            const int c = wid + NW * j;
+            const float * xc = (const float *) (x.base + (c < nc ? c : nc - 1) * x.nb1);
+            if (j == 0) {
+                norm_load<JM, true>(xc, K, lane, pro, pv[0], pg, pb);
+            } else {
+                float4 dg[1], db[1];
+                norm_load<JM, false>(xc, K, lane, pro, pv[j], dg, db);
+            }
         }
     }
     asm volatile("" ::: "memory");
@@ -701,10 +706,15 @@ __global__ __launch_bounds__(64 * NW) void k_gemv_f16_bn(const uint8_t * __restr
         if (EPI >= 1) e_bias = e.bias[rc];
         if (EPI == 2) e_res = *(const float *) (e.resid + cc * e.resid_nb1 + rc * sizeof(float));
     }
+    if constexpr (JM > 0) {
 #pragma unroll
-    for (int j = 0; j < CPW; j++) {
-        const int c = wid + NW * j;
-        if (c < nc) norm_store<JM, true>(pv[j], pg, pb, K, kp, pro, xs + (size_t) c * kp, lane);
+        for (int j = 0; j < CPW; j++) {
+            const int c = wid + NW * j;
+            if (c < nc) norm_store<JM, true>(pv[j], pg, pb, K, kp, pro, xs + (size_t) c * kp, lane);
+        }
+    } else {
+        (void) pv; (void) pg; (void) pb;
+        stage_cols<8>(x, 0, nc, K, kp, xs);
     }
     MI_STAMP(e.stamps, 1);
     mi_lds_barrier();
@@ -917,6 +927,22 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         else if (NWv == 8) { MI_GEMV_BN_E(8, 1) } else { MI_GEMV_BN_E(4, 1) }
 #undef MI_GEMV_BN_E
 #undef MI_GEMV_BN
+    } else if (!pro.mode && ncols > 1 && K <= 3072 && !xh && g_mi_tuning.f16_bp > 0 && (N + 3) / 4 < 4096) {
+        // several plain columns: 16 waves, 4 row groups x K split over 4 (k_gemv_f16_bn, JM = 0). Measured
+        // slower than k_gemv_f16 on batched decode (profiles/r06r_batched_plain_gemv_ab.txt): opt-in,
+        // f16_bp 1 is accepted by diagnostic builds only
+        const dim3 grid((unsigned) ((N + 15) / 16));
+        const size_t lds = (size_t) 8 * kp * sizeof(uint16_t) + (size_t) 16 * 4 * 8 * sizeof(float);
+        const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
+        const uint8_t * w = (const uint8_t *) W;
+        mi_f16_epilogue es = e;
+        es.stamps = mi_stamp_take("k_gemv_f16_bp", grid.x);
+#define MI_GEMV_BP(EP, NCHT) hipLaunchKernelGGL((k_gemv_f16_bn<EP, 0, 16, 4, NCHT>), grid, dim3(1024), lds, s, w, nb01, K, N, x, ncols, dst, ycol, es, pro, kp)
+#define MI_GEMV_BP_E(NCHT) switch (epi) { case 0: MI_GEMV_BP(0, NCHT); break; case 1: MI_GEMV_BP(1, NCHT); break; \
+                                              case 2: MI_GEMV_BP(2, NCHT); break; default: MI_GEMV_BP(3, NCHT); break; }
+        if (K <= 1024) { MI_GEMV_BP_E(8) } else { MI_GEMV_BP_E(24) }
+#undef MI_GEMV_BP_E
+#undef MI_GEMV_BP
     } else if (pro.mode) {  // supported() guarantees one pass (K <= 3072)
         if (K <= 1024) launch_one<4>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);
         else launch_one<12>(per, W, nb01, K, N, x, xh, ncols, dst, ycol, e, pro, s, nc, ks, rgs);

@@ -510,3 +510,41 @@ def test_norm_prologue_gemv_columns(libs, bn, K, N, ncols, epi):
     rel = float(np.abs(a.astype(np.float64) - b).max() / np.abs(b).max())
     print(f"f16_bn={bn} K={K} N={N} cols={ncols} {epi}: max rel {rel:.2e}")
     assert rel <= 1e-3
+
+
+@pytest.mark.parametrize("bp", [0, 1])
+@pytest.mark.parametrize("K,N,ncols,epi", [(768, 768, 8, "resid"), (3072, 768, 8, "resid"), (1000, 130, 3, "bias"), (256, 64, 2, "none")])
+def test_plain_gemv_columns(libs, bp, K, N, ncols, epi):
+    """F16 mul_mat of 2..8 plain columns (+ bias, + residual): batched decode's c_proj / mlp projection.
+    f16_bp 1: 16-wave workgroups of 16 rows, K split over 4 waves, the columns staged once per
+    workgroup (k_gemv_f16_bn's plain form; measured slower on batched decode, 0.63-0.64 vs 0.59-0.60
+    ms/step, profiles/r06r_batched_plain_gemv_ab.txt: diagnostic builds only); 0: k_gemv_f16. Within
+    1e-3 rel of the reference CPU."""
+    rt = libs[0]
+    x = rnd(50 + K, K * ncols, 1.0)
+    w = (rnd(51, K * N, 0.05)).astype(np.float16)
+    bias = rnd(52, N, 0.2)
+    res = rnd(53, N * ncols, 1.0)
+
+    def build(L, c):
+        t = L.ggml_new_tensor_2d(c, F32, K, ncols)
+        wt = L.ggml_new_tensor_2d(c, F16, K, N)
+        bi = L.ggml_new_tensor_1d(c, F32, N)
+        rs = L.ggml_new_tensor_2d(c, F32, N, ncols)
+        y = L.ggml_mul_mat(c, wt, t)
+        if epi != "none":
+            y = L.ggml_add(c, y, bi)
+        if epi == "resid":
+            y = L.ggml_add(c, y, rs)
+        return [(t, x), (wt, w), (bi, bias), (rs, res)], y
+
+    try:
+        if not rt.ggml_backend_mi355x_set_tuning(b"f16_bp", bp):
+            pytest.skip("f16_bp 1: diagnostic builds only (measured slower)")
+        assert rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
+        a, b = both(libs, build)
+    finally:
+        rt.ggml_backend_mi355x_set_tuning(b"f16_bp", 0)
+        rt.ggml_backend_mi355x_set_tuning(b"mmv_order", -1)
+    rel = float(np.abs(a.astype(np.float64) - b).max() / np.abs(b).max())
+    assert rel <= 1e-3, rel
