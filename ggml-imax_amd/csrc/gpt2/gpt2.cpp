@@ -850,10 +850,13 @@ int gpt2_decode_batch(gpt2_model * m, int n_tokens, const int32_t * tokens, cons
             fprintf(stderr, "gpt2_decode_batch: graph compute failed\n");
             return 1;
         }
-        if (logits) {
-            if (all_logits) ggml_backend_tensor_get(out, logits, 0, sizeof(float) * nv * n_tokens);
-            else ggml_backend_tensor_get(out, logits, sizeof(float) * nv * (n_tokens - 1), sizeof(float) * nv);
+        // logits == nullptr: into the pinned staging, read in place by the caller (gpt2_logits_host)
+        float * dl = logits ? logits : (m->host_io && lg_size <= ggml_nbytes(m->logits_host) ? (float *) m->logits_host->data : nullptr);
+        if (!dl) {
+            fprintf(stderr, "gpt2_decode_batch: no logits destination (staging too small)\n");
+            return -3;
         }
+        ggml_backend_tensor_get(out, dl, lg_off, lg_size);
     } else {
         const ggml_status st = plan ? ggml_backend_graph_plan_compute(m->backend, plan) : ggml_backend_graph_compute_async(m->backend, gf);
         if (st != GGML_STATUS_SUCCESS) {
@@ -876,7 +879,7 @@ int gpt2_decode_batch(gpt2_model * m, int n_tokens, const int32_t * tokens, cons
         }
         ggml_backend_synchronize(m->backend);
         if (plan) ggml_backend_graph_plan_free(m->backend, plan);  // its graph has run
-        if (logits) memcpy(logits, m->logits_host->data, lg_size);
+        if (logits) memcpy(logits, m->logits_host->data, lg_size);  // else: the caller reads gpt2_logits_host()
     }
     m->us_build = t1 - t0;
     m->us_alloc = t2 - t1;

@@ -458,7 +458,11 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
         for (int u = 0; u < U; u++) {
             const int it = u < nit ? u : nit - 1;
             const int64_t c = (int64_t) it * kLpr + m;
+#ifdef MI_TALL_NT  // (A/B builds: nontemporal weight loads for the lm_head)
+            w[u] = __builtin_nontemporal_load((const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16));
+#else
             w[u] = *(const uint4 *) (wrow + (c < k8 ? c : k8 - 1) * 16);  // (zeroed past K at use)
+#endif
         }
         if (EPI >= 1) eb = e.bias[r];
     };

@@ -211,6 +211,8 @@ class Model:
         self.n_vocab = hp.n_vocab
         # the host staging of the last token's logits (host_io), read in place by eval(copy=False)
         self._staged = None
+        # (the staging holds min(n_ctx, n_batch) rows of logits, gpt2_model_load_ex)
+        self._staged_bytes = hp.n_vocab * min(hp.n_ctx, n_batch if n_batch > 0 else 8) * 4
         if lib.has("gpt2_logits_host"):
             ptr = lib.gpt2_logits_host(self.m)
             if ptr:
@@ -233,16 +235,25 @@ class Model:
             raise RuntimeError("gpt2_eval failed")
         return out
 
-    def decode_batch(self, tokens, pos, seq_id, all_logits: bool = True) -> np.ndarray:
+    def decode_batch(self, tokens, pos, seq_id, all_logits: bool = True, copy: bool = True) -> np.ndarray:
         """gpt2_decode_batch (examples/gpt-2/main-batched.cpp gpt2_decode): token i of sequence
-        seq_id[i] at position pos[i]; logits [n_tokens or 1, n_vocab]."""
+        seq_id[i] at position pos[i]; logits [n_tokens or 1, n_vocab]. copy=False (host_io models):
+        a view of the pinned logits staging, valid until the next eval / decode_batch (as
+        llama_get_logits_ith returns a pointer into the context's logits)."""
         tok = np.ascontiguousarray(np.asarray(tokens, dtype=np.int32))
         p = np.ascontiguousarray(np.asarray(pos, dtype=np.int32))
         s = np.ascontiguousarray(np.asarray(seq_id, dtype=np.int32))
         n = len(tok)
         assert len(p) == n and len(s) == n
-        out = np.empty((n if all_logits else 1, self.n_vocab), dtype=np.float32)
-        rc = self.lib.gpt2_decode_batch(self.m, n, tok.ctypes.data, p.ctypes.data, s.ctypes.data, out.ctypes.data, 1 if all_logits else 0)
+        rows = n if all_logits else 1
+        view = None
+        if not copy and self._staged is not None and self.lib.has("gpt2_logits_host"):
+            ptr = self.lib.gpt2_logits_host(self.m)
+            if ptr and rows * self.n_vocab * 4 <= self._staged_bytes:
+                view = np.ctypeslib.as_array((ctypes.c_float * (rows * self.n_vocab)).from_address(ptr)).reshape(rows, self.n_vocab)
+        out = view if view is not None else np.empty((rows, self.n_vocab), dtype=np.float32)
+        rc = self.lib.gpt2_decode_batch(self.m, n, tok.ctypes.data, p.ctypes.data, s.ctypes.data,
+                                        None if view is not None else out.ctypes.data, 1 if all_logits else 0)
         if rc != 0:
             raise RuntimeError(f"gpt2_decode_batch failed ({rc})")
         return out
@@ -288,17 +299,18 @@ class Model:
             pass
 
 
-def run_batched(model: "Model", prompt: list[int], n_parallel: int, forced: list[list[int]]) -> np.ndarray:
+def run_batched(model: "Model", prompt: list[int], n_parallel: int, forced: list[list[int]], copy: bool = True) -> np.ndarray:
     """main-batched.cpp's flow, teacher-forced: the prompt decoded once as sequence 0, its cells
     shared with sequences 1..n_parallel-1 (gpt2_kv_cache_seq_cp), then one batch per step holding
     token forced[t][s] of every sequence s at position len(prompt) + t. Returns the prompt's last
-    logits followed by every step's n_parallel rows: [1 + steps * n_parallel, n_vocab]."""
+    logits followed by every step's n_parallel rows: [1 + steps * n_parallel, n_vocab].
+    copy=False: each step's logits read in place from the staging (decode_batch), saved by value here."""
     model.kv_clear()
     n = len(prompt)
-    outs = [model.decode_batch(prompt, list(range(n)), [0] * n, all_logits=False)]
+    outs = [np.array(model.decode_batch(prompt, list(range(n)), [0] * n, all_logits=False, copy=copy))]
     for s in range(1, n_parallel):
         model.kv_seq_cp(0, s, -1, -1)
     for t, row in enumerate(forced):
         assert len(row) == n_parallel
-        outs.append(model.decode_batch(row, [n + t] * n_parallel, list(range(n_parallel)), all_logits=True))
+        outs.append(np.array(model.decode_batch(row, [n + t] * n_parallel, list(range(n_parallel)), all_logits=True, copy=copy)))
     return np.concatenate(outs)

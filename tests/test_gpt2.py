@@ -640,6 +640,25 @@ def _batched_gpu_vs_ref(model_path, n_parallel):
 
 
 @pytest.mark.gpu
+def test_batched_logits_in_place_equal_copied(model_path):
+    """decode_batch(copy=False) -- the logits read in place from the pinned staging, as the batched
+    bench's loop does -- returns the same bits as the copied logits, step after step (the view of
+    one step is consumed before the next call overwrites the staging)."""
+    lib = G.runtime()
+    be = G.mi355x_backend(lib)
+    ours = gpt2.Model(lib, model_path, be, n_ctx=256, n_batch=8)
+    try:
+        prompt = ours.tokenize(PROMPT)[:8]
+        forced = _batched_scenario(8)
+        a = gpt2.run_batched(ours, prompt, 8, forced, copy=True)
+        b = gpt2.run_batched(ours, prompt, 8, forced, copy=False)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    finally:
+        ours.free()
+        lib.ggml_backend_free(be)
+
+
+@pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(REF_GPT2), reason="make -C oracle gpt2")
 @pytest.mark.parametrize("n_parallel", [2, 4, 8])
 def test_batched_sequences_match_reference_cpu(model_path, n_parallel):
