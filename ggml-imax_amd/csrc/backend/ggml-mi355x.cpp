@@ -757,6 +757,31 @@ static const char * planes_of(mi_backend_ctx * ctx, const ggml_tensor * a, const
     return mi_planes_get(a->type, a->data, a->nb[1], a->ne[0], a->ne[1], ctx->stream);
 }
 
+// The 16-byte-aligned copy of a Q4_0 weight for the tree-order decode GEMV (mmq_planes.hip
+// k_q40_repack; created before any capture, renewed by the same write paths as the planes): the
+// same conditions as planes_of -- a graph leaf in this backend's own device buffer
+static const char * q40r_of(mi_backend_ctx * ctx, const ggml_tensor * a) {
+    if (!g_mi_tuning.q40r || a->type != GGML_TYPE_Q4_0 || a->op != GGML_OP_NONE || a->ne[2] != 1 || a->ne[3] != 1 || is_split_tensor(a))
+        return nullptr;
+    const ggml_backend_buffer_t buf = a->view_src ? a->view_src->buffer : a->buffer;
+    if (!buffer_is_mi355x(buf) || ((mi_buffer_ctx *) buf->context)->device != ctx->device) return nullptr;
+    return mi_planes_get(a->type, a->data, a->nb[1], a->ne[0], a->ne[1], ctx->stream);
+}
+
+// A Q4_0 decode group in tree order on the repacked copies (FmtQ0R): every member's weight must
+// have one, else the canonical blocks (FmtQ0Pair) -- both give the same bits
+static void q40r_apply(mi_backend_ctx * ctx, mi_mmv_group & g, const ggml_tensor * const * w) {
+    if (g.type != GGML_TYPE_Q4_0 || !g_mi_tuning.q40r || mi_mmv_order() != 0 || g_mi_tuning.mmv_variant % 10 == 1) return;
+    const void * p[kMiMaxMembers];
+    for (int m = 0; m < g.n; m++) {
+        p[m] = q40r_of(ctx, w[m]);
+        if (!p[m]) return;
+    }
+    for (int m = 0; m < g.n; m++) g.m[m].W = p[m];
+    g.nb01 = (size_t) (g.K / 32 * 18);
+    g.q0r = 1;
+}
+
 // The mul_mat of (src0, src1) with src0's rows taken from (W, N) and the output written at out
 // (column strides nb1..nb3): op_mul_mat runs the whole node through it, the split-buffer path
 // (op_mul_mat_split) each device's row slice.
@@ -1150,6 +1175,8 @@ static void rope_tables_prepare(mi_backend_ctx * ctx, const ggml_cgraph * cgraph
         const ggml_tensor * n = cgraph->nodes[i];
         if (n->op == GGML_OP_ROPE && n->src[0] && n->src[0]->type == GGML_TYPE_F32) rope_table_ensure(ctx, n);
         if (n->op == GGML_OP_MUL_MAT) (void) planes_of(ctx, n->src[0], n->src[1]);
+        // (decode GEMVs of a tree-order graph: the Q4_0 weights' aligned copies)
+        if (n->op == GGML_OP_MUL_MAT && n->src[1]->ne[1] <= 8 && mi_mmv_order() == 0) (void) q40r_of(ctx, n->src[0]);
     }
 }
 
@@ -1311,11 +1338,14 @@ static int run_fused_group(mi_backend_ctx * ctx, ggml_cgraph * cgraph, int i) {
     g.nb01 = first->src[0]->nb[1];
     g.xcol = first->src[1]->nb[1];
     g.ycol = first->nb[1];
+    const ggml_tensor * wts[kMiMaxMembers];
     for (int m = 0; m < g.n; m++) {
         g.m[m].W = members[m]->src[0]->data;
         g.m[m].X = (const char *) members[m]->src[1]->data;
         g.m[m].dst = (float *) members[m]->data;
+        wts[m] = members[m]->src[0];
     }
+    q40r_apply(ctx, g, wts);
     mi_mul_mat_q_fused(g, ctx->stream);
     ctx->last_launches++;
     for (ggml_tensor * m : members) invalidate_activations(ctx, m);
@@ -1584,6 +1614,7 @@ static int try_fuse_q_gemv(mi_backend_ctx * ctx, ggml_cgraph * g, int i, const m
     grp.m[0].W = w->data;
     grp.m[0].X = (const char *) x->data;
     grp.m[0].dst = (float *) out->data;
+    q40r_apply(ctx, grp, &w);
     mi_mul_mat_q_fused(grp, ctx->stream);
     ctx->last_launches++;
     return last;
@@ -2176,7 +2207,10 @@ static bool graph_capturable(const ggml_cgraph * cgraph) {
 // Everything the node pass does synchronously -- table uploads, scratch growth -- done up front,
 // so that a capture of the pass only enqueues kernels on ctx->stream. Scratch: the pass's own
 // estimate plus room for the attention planner's Q copies (at most every CONT node's bytes).
+static int graph_decode_order(const ggml_cgraph * g);
+
 static void prepare_for_capture(mi_backend_ctx * ctx, const ggml_cgraph * cgraph) {
+    tl_mi_graph_order = graph_decode_order(cgraph);  // (the graph's order decides which weight copies it needs)
     op_tables(ctx);
     rope_tables_prepare(ctx, cgraph);
     size_t cont_bytes = 0;
@@ -3001,6 +3035,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "planes") == 0 && value >= 0 && value <= 1) {
         g_mi_tuning.planes = value;
+        return true;
+    }
+    if (strcmp(name, "q40r") == 0 && value >= 0 && value <= 1) {
+        g_mi_tuning.q40r = value;
         return true;
     }
     if (strcmp(name, "f16_waves") == 0 && value >= 0) {

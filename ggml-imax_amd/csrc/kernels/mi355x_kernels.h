@@ -102,6 +102,7 @@ struct mi_mmv_group {
     } pro;
     int pro_off = 0;   // set by the launcher: LDS byte offset of the normalized columns
     uint64_t * stamps = nullptr;  // diagnostic builds: per-workgroup phase stamps (g_mi_stamp_dev)
+    int q0r = 0;       // Q4_0: every member's W is its 16-byte-aligned repacked copy (mi_planes_get type 2), nb01 = K / 32 * 18
     mi_mmv_member m[kMiMaxMembers];
 };
 // Diagnostic builds (make DIAG=1): when non-null, the decode kernels write s_memrealtime phase
@@ -141,6 +142,7 @@ struct mi_tuning {
     int mmv_dma;      // grouped tree-order Q4_K GEMVs on the LDS-DMA weight stream (k_mmv_dma): 0 off, 1-3 shapes, +10 default load policy
     int f16_bn;       // F16 decode GEMVs, 2..8 columns with the norm prologue (K <= 1024) on k_gemv_f16_bn: 0 off, 1-5 shapes (default 5), +10 one column too
     int f16_bp;       // F16 decode GEMVs, 2..8 plain columns (K <= 3072) on k_gemv_f16_bn's staging form: 0 off, 1 on
+    int q40r;         // tree-order Q4_0 decode GEMVs on the 16-byte-aligned repacked copy (mmq_planes.hip k_q40_repack, FmtQ0R): 1 on (default), 0 off
 };
 extern mi_tuning g_mi_tuning;
 // the order of the graph being launched when mmv_order is -1 (set by the backend per graph)
@@ -240,6 +242,8 @@ void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N
 // mmq_variant bits of opt-in kernel forms measured slower than the defaults: diagnostic builds only
 constexpr int kMiMmqDiagBits = (1 << 19) | (1 << 26);  // (bit 2^17 doubles as k_mmqx's full-width bit)
 constexpr int64_t kMiPlanesMinCols = 129;  // prompts of more columns take the planes kernel
+// Type 2 (Q4_0, g_mi_tuning.q40r): the tree-order decode GEMV's 16-byte-aligned copy instead
+// (k_q40_repack: per row the quants of every block, then their f16 scales; K / 32 * 18 bytes a row).
 const char * mi_planes_get(int type, const void * W, size_t nb01, int64_t K, int64_t N, hipStream_t s);
 void mi_planes_refresh(const void * lo, size_t bytes, hipStream_t s);
 void mi_planes_drop(const void * lo, size_t bytes);

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <iterator>
 #include <map>
 #include <mutex>
 
@@ -280,6 +281,33 @@ __global__ __launch_bounds__(512, 1) void k_mmqr(mi_mmx_group grp, uint64_t * st
     }
 }
 
+// ---- Q4_0 decode weights, 16-byte aligned (round 6) -------------------------------------------------
+// The canonical Q4_0 block (d f16, 16 bytes of nibbles; 18 bytes, ggml-common.h block_q4_0) leaves
+// the quants 2-byte aligned, so the tree-order GEMV (FmtQ0Pair) loads each 36-byte block pair with
+// dword loads that straddle 16-byte and cache-line boundaries. The repacked copy of row n (the same
+// bytes, K / 32 * 18 per row, rows packed) puts the quants first and the scales after them:
+//   [b * 16 .. b * 16 + 15]   block b's 16 quant bytes        (pair p = 32 bytes at 32 p)
+//   [nblk * 16 + 2 b]        block b's d                     (pair p = one dword at nblk * 16 + 4 p)
+// so a lane's pair is two aligned dwordx4 loads plus one dword, and consecutive lanes read
+// consecutive bytes (FmtQ0R, mmv_fused_impl.h). One thread per block, grid (N, row chunks).
+__global__ __launch_bounds__(256) void k_q40_repack(const uint8_t * __restrict__ W, size_t nb01, int64_t nblk, uint8_t * __restrict__ out) {
+    const int64_t n = blockIdx.x;
+    const int64_t b = (int64_t) blockIdx.y * 256 + threadIdx.x;
+    if (b >= nblk) return;
+    const uint16_t * src = (const uint16_t *) (W + (size_t) n * nb01 + (size_t) b * 18);  // 2-byte aligned
+    uint16_t h[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) h[i] = src[i];
+    uint8_t * row = out + (size_t) n * (size_t) nblk * 18;
+    uint4 q;
+    q.x = h[1] | ((uint32_t) h[2] << 16);
+    q.y = h[3] | ((uint32_t) h[4] << 16);
+    q.z = h[5] | ((uint32_t) h[6] << 16);
+    q.w = h[7] | ((uint32_t) h[8] << 16);
+    *(uint4 *) (row + (size_t) b * 16) = q;
+    *(uint16_t *) (row + (size_t) nblk * 16 + (size_t) b * 2) = h[0];
+}
+
 // ---- the cache ------------------------------------------------------------------------------------
 struct PlanesEntry {
     int type;
@@ -298,6 +326,12 @@ std::atomic<uint64_t> g_planes_gen{0};       // bumped whenever an entry is crea
 int planes_enabled() { return g_mi_tuning.planes; }
 
 void launch_repack(const PlanesEntry & e, const void * W, hipStream_t s) {
+    if (e.type == 2) {
+        const int64_t nblk = e.K / 32;
+        const dim3 grid((unsigned) e.N, (unsigned) ((nblk + 255) / 256));
+        hipLaunchKernelGGL(k_q40_repack, grid, dim3(256), 0, s, (const uint8_t *) W, e.nb01, nblk, (uint8_t *) e.planes);
+        return;
+    }
     const int S = (int) (e.K / 256);
     const int64_t nt = (e.N + 31) / 32;
     const dim3 grid((unsigned) S, (unsigned) nt);
@@ -308,10 +342,12 @@ void launch_repack(const PlanesEntry & e, const void * W, hipStream_t s) {
 } // namespace
 
 const char * mi_planes_get(int type, const void * W, size_t nb01, int64_t K, int64_t N, hipStream_t s) {
-    // (Q4_K: the planes kernel beats the canonical one; Q5_K's 3 planes do not fit its LDS stages)
-    if (!planes_enabled() || type != 12 || K % 256 != 0 || N <= 0 || !W) return nullptr;
-    const int BS = type == 12 ? 144 : 176;
-    if (nb01 % 4 != 0 || nb01 < (size_t) (K / 256) * BS) return nullptr;
+    // (Q4_K: the planes kernel beats the canonical one; Q5_K's 3 planes do not fit its LDS stages.
+    // Q4_0: the 16-byte-aligned decode copy, g_mi_tuning.q40r)
+    if (type == 2 ? !g_mi_tuning.q40r : (!planes_enabled() || type != 12)) return nullptr;
+    if (K % 256 != 0 || N <= 0 || !W) return nullptr;
+    const int64_t row_min = type == 2 ? K / 32 * 18 : K / 256 * (type == 12 ? 144 : 176);
+    if (nb01 % (type == 2 ? 2 : 4) != 0 || (int64_t) nb01 < row_min) return nullptr;
     std::lock_guard<std::mutex> lk(g_planes_mu);
     auto it = g_planes.find((uintptr_t) W);
     if (it != g_planes.end()) {
@@ -324,13 +360,21 @@ const char * mi_planes_get(int type, const void * W, size_t nb01, int64_t K, int
         (void) hipGetLastError();
         return nullptr;  // no allocation inside a capture: this launch takes the canonical kernels
     }
+    // entries never overlap one another (mi_planes_refresh relies on it): a W inside another
+    // entry's span, or one whose span reaches the next entry, keeps the canonical kernels
+    const uintptr_t wa = (uintptr_t) W, wb = wa + (size_t) (N - 1) * nb01 + (size_t) row_min;
+    {
+        auto nx = g_planes.lower_bound(wa);
+        if (nx != g_planes.end() && nx->first < wb) return nullptr;
+        if (nx != g_planes.begin() && std::prev(nx)->first + std::prev(nx)->second.span > wa) return nullptr;
+    }
     PlanesEntry e;
     e.type = type;
     e.nb01 = nb01;
     e.K = K;
     e.N = N;
-    e.span = (size_t) (N - 1) * nb01 + (size_t) (K / 256) * BS;
-    e.bytes = (size_t) ((N + 31) / 32) * (K / 256) * (type == 12 ? PFmt<12>::RB : PFmt<13>::RB);
+    e.span = (size_t) (N - 1) * nb01 + (size_t) row_min;
+    e.bytes = type == 2 ? (size_t) N * (size_t) row_min : (size_t) ((N + 31) / 32) * (K / 256) * (type == 12 ? PFmt<12>::RB : PFmt<13>::RB);
     (void) hipGetDevice(&e.device);
     void * p = nullptr;
     if (hipMalloc(&p, e.bytes) != hipSuccess) {
@@ -352,7 +396,10 @@ void mi_planes_refresh(const void * lo, size_t bytes, hipStream_t s) {
     const uintptr_t a = (uintptr_t) lo, b = a + bytes;
     int dev = -1;
     (void) hipGetDevice(&dev);
-    for (auto it = g_planes.begin(); it != g_planes.end() && it->first < b; ++it) {
+    // entries do not overlap one another: the only one that can start below a is the last such
+    auto it = g_planes.lower_bound(a);
+    if (it != g_planes.begin()) --it;
+    for (; it != g_planes.end() && it->first < b; ++it) {
         const PlanesEntry & e = it->second;
         if (it->first + e.span <= a || e.device != dev) continue;
         launch_repack(e, (const void *) it->first, s);

@@ -160,6 +160,7 @@ __device__ __forceinline__ void quantize_row16(const float4 (&v4)[4], int lane, 
 
 template <bool Q5>
 struct FmtKQ {
+    static constexpr bool KL = false;  // load() does not need K
     static constexpr int QKA = 256;  // activation block
     static constexpr int ITEM = 64;  // elements per item
     static constexpr int BS = Q5 ? 176 : 144;
@@ -378,6 +379,7 @@ struct FmtKQ {
 // (aligned down) and re-align with v_alignbyte; d is a separate 2-byte load.
 template <bool Q8>
 struct FmtQ0 {
+    static constexpr bool KL = false;
     static constexpr int QKA = 32;
     static constexpr int ITEM = 32;
     static constexpr int BS = Q8 ? 34 : 18;
@@ -518,7 +520,27 @@ struct FmtQ0 {
 // Q4_0 in pairs of blocks (tree order only): an item is 2 blocks = 36 B, 4-byte aligned, so 9
 // dword loads cover it with no slack, the second block's quants are whole dwords (only the
 // first's need v_alignbyte), and a K = 4096 row is one item per lane.
+// one pair of Q4_0 blocks against its q8_0 activations: block quants t0 / t1 (16 bytes each), scales
+// dw0 / dw1; shared by FmtQ0Pair and FmtQ0R, so the canonical and the repacked layouts give the
+// same bits
+__device__ __forceinline__ float q0pair_dot(const uint32_t (&t0)[4], const uint32_t (&t1)[4], float dw0, float dw1, const int (&av0)[8],
+                                            const int (&av1)[8], uint32_t ss, float2 da, float acc) {
+    int s0 = 0, s1 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        s0 = mi_dot4((int) (t0[i] & 0x0F0F0F0Fu), av0[i], s0);
+        s0 = mi_dot4((int) ((t0[i] >> 4) & 0x0F0F0F0Fu), av0[i + 4], s0);
+        s1 = mi_dot4((int) (t1[i] & 0x0F0F0F0Fu), av1[i], s1);
+        s1 = mi_dot4((int) ((t1[i] >> 4) & 0x0F0F0F0Fu), av1[i + 4], s1);
+    }
+    s0 -= 8 * (int) (int16_t) (ss & 0xFFFF);
+    s1 -= 8 * (int) (int16_t) (ss >> 16);
+    acc = fmaf((float) s0, dw0 * da.x, acc);
+    return fmaf((float) s1, dw1 * da.y, acc);
+}
+
 struct FmtQ0Pair {
+    static constexpr bool KL = false;
     static constexpr int QKA = 32;
     static constexpr int ITEM = 64;
     struct Regs {
@@ -551,18 +573,8 @@ struct FmtQ0Pair {
     }
     __device__ static __forceinline__ float pair_dot(const Regs & r, const uint32_t (&t0)[4], float dw0, float dw1, const int (&av0)[8],
                                                      const int (&av1)[8], uint32_t ss, float2 da, float acc) {
-        int s0 = 0, s1 = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            s0 = mi_dot4((int) (t0[i] & 0x0F0F0F0Fu), av0[i], s0);
-            s0 = mi_dot4((int) ((t0[i] >> 4) & 0x0F0F0F0Fu), av0[i + 4], s0);
-            s1 = mi_dot4((int) (r.w[i + 5] & 0x0F0F0F0Fu), av1[i], s1);
-            s1 = mi_dot4((int) ((r.w[i + 5] >> 4) & 0x0F0F0F0Fu), av1[i + 4], s1);
-        }
-        s0 -= 8 * (int) (int16_t) (ss & 0xFFFF);
-        s1 -= 8 * (int) (int16_t) (ss >> 16);
-        acc = fmaf((float) s0, dw0 * da.x, acc);
-        return fmaf((float) s1, dw1 * da.y, acc);
+        const uint32_t t1[4] = {r.w[5], r.w[6], r.w[7], r.w[8]};
+        return q0pair_dot(t0, t1, dw0, dw1, av0, av1, ss, da, acc);
     }
     struct Act {
         int av0[8], av1[8];
@@ -590,6 +602,54 @@ struct FmtQ0Pair {
     }
 };
 
+// Q4_0 block pairs on the 16-byte-aligned repacked copy (tree order only; mmq_planes.hip
+// k_q40_repack): per row [K/32 blocks x 16 quant bytes][K/32 x f16 d], so item (pair) p is two
+// aligned dwordx4 at 32 p and one dword at K/2 + 4 p -- consecutive lanes read consecutive bytes.
+// The same pair arithmetic as FmtQ0Pair (q0pair_dot): bit-identical outputs.
+struct FmtQ0R {
+    static constexpr bool KL = true;  // load() needs K (the scales follow the row's quants)
+    static constexpr int QKA = 32;
+    static constexpr int ITEM = 64;
+    struct Regs {
+        uint4 q0, q1;
+        uint32_t d;
+    };
+    __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item, int64_t K) {
+        const uint32_t o = (uint32_t) item * 32;
+        r.q0 = *(const uint4 *) (row + o);
+        r.q1 = *(const uint4 *) (row + o + 16);
+        r.d = *(const uint32_t *) (row + (uint32_t) (K / 2) + 4 * (uint32_t) item);
+    }
+    __device__ static __forceinline__ float pdot(const Regs & r, const int (&av0)[8], const int (&av1)[8], uint32_t ss, float2 da, float acc) {
+        const uint32_t t0[4] = {r.q0.x, r.q0.y, r.q0.z, r.q0.w};
+        const uint32_t t1[4] = {r.q1.x, r.q1.y, r.q1.z, r.q1.w};
+        return q0pair_dot(t0, t1, mi_h2f((uint16_t) (r.d & 0xFFFF)), mi_h2f((uint16_t) (r.d >> 16)), av0, av1, ss, da, acc);
+    }
+    template <int NC>
+    __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 64);
+            const int4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            const int av0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const int av1[8] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            const uint32_t ss = *(const uint32_t *) (a.s32 + c * (K / 32) + 2 * item);
+            const float2 da = *(const float2 *) (a.d + c * (K / 32) + 2 * item);
+            acc[c] = pdot(r, av0, av1, ss, da, acc[c]);
+        }
+    }
+    using Act = FmtQ0Pair::Act;
+    __device__ static __forceinline__ void act_load(Act & v, int item, const lds_act & a, int64_t K) { FmtQ0Pair::act_load(v, item, a, K); }
+    __device__ static __forceinline__ float dot_act(const Regs & r, int, const Act & v, float acc) { return pdot(r, v.av0, v.av1, v.ss, v.da, acc); }
+};
+
+// a format's weight load (FmtQ0R's needs the row length)
+template <class F>
+__device__ __forceinline__ void fmt_load(typename F::Regs & r, const uint8_t * row, int item, int64_t K) {
+    if constexpr (F::KL) F::load(r, row, item, K);
+    else F::load(r, row, item);
+}
 
 // ------------------------------------------------------------------ the streaming kernel
 
@@ -758,14 +818,14 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
 #pragma unroll
         for (int i = 0; i < IPL; i++) {
             const int item = lane + 64 * i;
-            F::load(slot[i], wr, item < nitems ? item : nitems - 1);
+            fmt_load<F>(slot[i], wr, item < nitems ? item : nitems - 1, K);
         }
     };
     // MR > 1: ring slot = one step of MR rows; lane 16 r + i loads item i of row MR k + r
     auto prefetch_mr = [&](typename F::Regs (&slot)[IPL], int k) {
         const uint8_t * wr = wrow_of(MR * k + (lane >> 4));
         const int item = lane & 15;
-        F::load(slot[0], wr, item < nitems ? item : nitems - 1);
+        fmt_load<F>(slot[0], wr, item < nitems ? item : nitems - 1, K);
     };
     const int nsteps = MR > 1 ? (nrows + MR - 1) / MR : nrows;
     const int klast = nsteps > 0 ? nsteps - 1 : 0;
@@ -970,7 +1030,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                             const int item = base + lane;
                             if (item < nitems) {
                                 typename F::Regs rr;
-                                F::load(rr, wr, item);
+                                fmt_load<F>(rr, wr, item, K);
                                 F::template dot_ord<NC>(rr, item, lane, act, K, ncols, scr, cs, S);
                             }
                             chunk_done(base);
@@ -993,7 +1053,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                     const uint8_t * wr = wrow_of(k);
                     for (int item = lane + 64 * IPL; item < nitems; item += 64) {
                         typename F::Regs rr;
-                        F::load(rr, wr, item);
+                        fmt_load<F>(rr, wr, item, K);
                         F::template dot_ord<NC>(rr, item, item, act, K, ncols, srow, cs, S);
                     }
                 }
@@ -1031,7 +1091,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
                 const uint8_t * wr = wrow_of(k);
                 for (int item = lane + 64 * IPL; item < nitems; item += 64) {
                     typename F::Regs rr;
-                    F::load(rr, wr, item);
+                    fmt_load<F>(rr, wr, item, K);
                     F::template dot<NC>(rr, item, act, K, ncols, acc);
                 }
             }
