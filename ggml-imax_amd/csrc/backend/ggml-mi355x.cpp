@@ -771,7 +771,8 @@ static const char * q40r_of(mi_backend_ctx * ctx, const ggml_tensor * a) {
 // A Q4_0 decode group in tree order on the repacked copies (FmtQ0R): every member's weight must
 // have one, else the canonical blocks (FmtQ0Pair) -- both give the same bits
 static void q40r_apply(mi_backend_ctx * ctx, mi_mmv_group & g, const ggml_tensor * const * w) {
-    if (g.type != GGML_TYPE_Q4_0 || !g_mi_tuning.q40r || mi_mmv_order() != 0 || g_mi_tuning.mmv_variant % 10 == 1) return;
+    // (one column: with two, the aligned copy measured 2-3 % slower, profiles/r06s2_q40r_ab.txt)
+    if (g.type != GGML_TYPE_Q4_0 || g.ncols != 1 || !g_mi_tuning.q40r || mi_mmv_order() != 0 || g_mi_tuning.mmv_variant % 10 == 1) return;
     const void * p[kMiMaxMembers];
     for (int m = 0; m < g.n; m++) {
         p[m] = q40r_of(ctx, w[m]);
@@ -1176,7 +1177,7 @@ static void rope_tables_prepare(mi_backend_ctx * ctx, const ggml_cgraph * cgraph
         if (n->op == GGML_OP_ROPE && n->src[0] && n->src[0]->type == GGML_TYPE_F32) rope_table_ensure(ctx, n);
         if (n->op == GGML_OP_MUL_MAT) (void) planes_of(ctx, n->src[0], n->src[1]);
         // (decode GEMVs of a tree-order graph: the Q4_0 weights' aligned copies)
-        if (n->op == GGML_OP_MUL_MAT && n->src[1]->ne[1] <= 8 && mi_mmv_order() == 0) (void) q40r_of(ctx, n->src[0]);
+        if (n->op == GGML_OP_MUL_MAT && n->src[1]->ne[1] == 1 && mi_mmv_order() == 0) (void) q40r_of(ctx, n->src[0]);
     }
 }
 
@@ -3039,6 +3040,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "q40r") == 0 && value >= 0 && value <= 1) {
         g_mi_tuning.q40r = value;
+        return true;
+    }
+    if (strcmp(name, "mmqt_short") == 0 && value >= 0) {
+        g_mi_tuning.mmqt_short = value;
         return true;
     }
     if (strcmp(name, "f16_waves") == 0 && value >= 0) {

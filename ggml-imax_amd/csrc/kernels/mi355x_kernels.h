@@ -143,6 +143,7 @@ struct mi_tuning {
     int f16_bn;       // F16 decode GEMVs, 2..8 columns with the norm prologue (K <= 1024) on k_gemv_f16_bn: 0 off, 1-5 shapes (default 5), +10 one column too
     int f16_bp;       // F16 decode GEMVs, 2..8 plain columns (K <= 3072) on k_gemv_f16_bn's staging form: 0 off, 1 on
     int q40r;         // tree-order Q4_0 decode GEMVs on the 16-byte-aligned repacked copy (mmq_planes.hip k_q40_repack, FmtQ0R): 1 on (default), 0 off
+    int mmqt_short;   // Q4_K prompts of 33..128 columns on k_mmqt (128 x 64 tiles) when a launch has at least this many of its workgroups (default 192; 0: never)
 };
 extern mi_tuning g_mi_tuning;
 // the order of the graph being launched when mmv_order is -1 (set by the backend per graph)

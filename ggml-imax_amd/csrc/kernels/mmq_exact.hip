@@ -2421,6 +2421,26 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     // long prompts on repacked planes (mmq_planes.hip) when every member carries them (each output
     // stored once: any destination); variant bits forcing a canonical kernel (16, 128) keep it
     if (ncols >= kMiPlanesMinCols && !(var & (16 | 128)) && mi_mul_mat_mmqr_group(g, s)) return;
+    // Q4_K prompts of 33..128 columns whose launch (nearly) fills the chip with k_mmqt's 128 x 64
+    // tiles (one workgroup per CU; mmqt_short, default 192 workgroups): k_mmqt instead of k_mmqp
+    // (round 6, bit-identical). 32 rotated weights grouped 16 to a launch: B = 64 7.29 -> 5.36 us,
+    // B = 128 13.39 -> 10.04 us per mul_mat (profiles/r06s2_pf_mmqt_short.txt); by group size
+    // (r06s2b_mmqt_short_groups.txt, r06s2c_mmqt_short_threshold.txt) k_mmqt wins from 192 of its
+    // workgroups (3 x B = 128: 13.99 -> 11.19 us; 6 x B = 64: 6.98 -> 5.72 us) and loses below (4 x
+    // B = 64, 128 workgroups: 7.76 vs 7.86; a lone B = 64 member's 32: 12.4 vs 26.6 us); B = 32 stays
+    // on k_mmqp (4.52 vs 4.85). Variant bits that ask for a particular kernel turn it off.
+    constexpr int kShortTBlock = 16 | 128 | 2048 | 4096 | 8192 | (1 << 19) | (1 << 21) | (1 << 22) | (1 << 26) | (1 << 27);
+    bool short_t = false;
+    if (type == 12 && ncols > 32 && ncols <= 128 && dst_local && g_mi_tuning.mmqt_short > 0 && !(var & kShortTBlock)) {
+        int64_t tt = 0;
+        for (int i = 0; i < g.n; i++) tt += ((g.m[i].N + 127) / 128) * ((g.m[i].act.ncols + 63) / 64);
+        short_t = tt >= g_mi_tuning.mmqt_short;
+    }
+    if (short_t) {
+        const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
+        hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
+        return;
+    }
     const bool direct = (var & 16) || (ncols <= 128 && !(var & 128)) || !dst_local;
     if (direct) {
         const int S = (int) (K / 256);

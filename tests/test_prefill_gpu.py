@@ -441,3 +441,44 @@ def test_planes_captured_graph_after_weight_realloc(rt, backend):
         for y in outs:
             assert np.array_equal(y.view(np.uint32), base[0].view(np.uint32)), rel_err(y, base[0])
     assert _planes_stats(rt)[0] == n0
+
+
+@pytest.mark.parametrize("B", [33, 64, 100, 128])
+def test_short_prompt_mmqt_route_bit_equal(rt, backend, B):
+    """Q4_K prompts of 33..128 columns take k_mmqt (128 x 64 tiles) when the launch has at least
+    mmqt_short of its workgroups (default 192: grouped launches that nearly fill the chip), else k_mmqp.
+    Forced on (mmqt_short 1) over ragged rows and columns, it is bit-identical to k_mmqp (off)
+    and within the exact-path tolerance of the oracle."""
+    t = orc.Q4_K
+    K = 2048
+    Ns = [512, 320, 96, 1024]
+    wqs = [orc.quantize(t, synth.uniform(60 + i, K * n), K) for i, n in enumerate(Ns)]
+    xs = [synth.uniform(70 + i, K * B) for i in range(len(Ns))]
+
+    def run(mmqt_short):
+        ovh = rt.ggml_tensor_overhead() * 24 + rt.ggml_graph_overhead()
+        with G.Context(rt, ovh, no_alloc=True) as c:
+            ws = [rt.ggml_new_tensor_2d(c.ctx, t, K, n) for n in Ns]
+            xts = [rt.ggml_new_tensor_2d(c.ctx, G.GGML_TYPE_F32, K, B) for _ in Ns]
+            ys = [rt.ggml_mul_mat(c.ctx, w, x) for w, x in zip(ws, xts)]
+            g = rt.ggml_new_graph(c.ctx)
+            for y in ys:
+                rt.ggml_build_forward_expand(g, y)
+            buf = rt.ggml_backend_alloc_ctx_tensors(c.ctx, backend)
+            assert buf
+            try:
+                assert rt.ggml_backend_mi355x_set_tuning(b"mmqt_short", mmqt_short)
+                for w, wq, x, xv in zip(ws, wqs, xts, xs):
+                    G.tensor_set(rt, w, wq)
+                    G.tensor_set(rt, x, xv)
+                assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
+                assert rt.ggml_backend_mi355x_last_launch_count(backend) == 2  # one quantizer + one grouped GEMM
+                return [G.tensor_get(rt, y) for y in ys]
+            finally:
+                rt.ggml_backend_mi355x_set_tuning(b"mmqt_short", 192)
+                rt.ggml_backend_buffer_free(buf)
+
+    forced, base = run(1), run(0)
+    for i in range(len(Ns)):
+        assert np.array_equal(forced[i].view(np.uint32), base[i].view(np.uint32)), (i, rel_err(forced[i], base[i]))
+    assert rel_err(forced[1], orc.mul_mat(t, wqs[1], K, Ns[1], xs[1], B)) <= EXACT_TOL
