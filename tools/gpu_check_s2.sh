@@ -1,5 +1,5 @@
 set -eo pipefail
-OUT=gpurun_out/r06s2a
+OUT=gpurun_out/${1:-r06s2a}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
