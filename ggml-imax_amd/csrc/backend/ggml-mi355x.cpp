@@ -3042,6 +3042,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.q40r = value;
         return true;
     }
+    if (strcmp(name, "mmv_pro4") == 0 && value >= 0 && value <= 1) {
+        g_mi_tuning.mmv_pro4 = value;
+        return true;
+    }
     if (strcmp(name, "mmqt_short") == 0 && value >= 0) {
         g_mi_tuning.mmqt_short = value;
         return true;

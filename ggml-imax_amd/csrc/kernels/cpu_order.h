@@ -115,8 +115,47 @@ __device__ float wave_mean_cpu_order(const float (&v)[J], int64_t n) {
     return (float) (q / (double) n);
 }
 
+// The same for rows held four consecutive elements per lane: lane l owns k = 256 j + 4 l + i
+// (j < J, i < 4); the fallback walks k in order (j, lane, i).
+template <bool SQ, int J>
+__device__ float wave_mean_cpu_order4(const float4 (&v)[J], int64_t n) {
+    const int lane = threadIdx.x & 63;
+    double s = 0.0, a = 0.0;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if ((int64_t) j * 256 + lane * 4 + i < n) {
+                const double t = (double) sum_term<SQ>(e[i]);
+                s += t;
+                a += fabs(t);
+            }
+        }
+    }
+    s = mi_wave_sum_u_f64(s);
+    a = mi_wave_sum_u_f64(a);
+    const double B = 4.0 * (double) n * a * 0x1p-53 + 0x1p-1074;
+    const float lo = (float) ((s - B) / (double) n);
+    const float hi = (float) ((s + B) / (double) n);
+    if (lo == hi) return lo == 0.0f ? 0.0f : lo;  // the CPU's chain starts at +0.0
+    double q = 0.0;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const float e[4] = {sum_term<SQ>(v[j].x), sum_term<SQ>(v[j].y), sum_term<SQ>(v[j].z), sum_term<SQ>(v[j].w)};
+        for (int l = 0; l < 64; l++) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if ((int64_t) j * 256 + l * 4 + i < n) q += (double) __shfl(e[i], l, 64);
+            }
+        }
+    }
+    return (float) (q / (double) n);
+}
+
 } // namespace mi_cpu
 
+using mi_cpu::wave_mean_cpu_order4;
 using mi_cpu::add_rn;
 using mi_cpu::mul_rn;
 using mi_cpu::row_mean_cpu_order;

@@ -718,6 +718,74 @@ __device__ void norm_prologue(const mi_mmv_group & g, const char * X, int ncols,
     }
 }
 
+// One column with a Q8_K activation (Q4_K / Q5_K weights), K a multiple of 256 up to
+// kMiMmvProMaxK: wave 0 holds the column four consecutive elements per lane (k = 256 j + 4 l + i,
+// float4 loads), normalizes it in registers and quantizes each 256-slice straight into the LDS
+// activations (quantize_slice: the layout mi_q8K_superblock takes) -- no normalized copy through
+// LDS, no second barrier and no re-read (round 6). The arithmetic of norm_prologue element for
+// element: certified double mean / variance (wave_mean_cpu_order4), then every step rounded.
+struct norm_cols4 {
+    static constexpr int kJ = (int) (kMiMmvProMaxK / 256);
+    float4 v[kJ], gv[kJ], bv[kJ];
+};
+
+__device__ __forceinline__ void norm_cols4_load(const mi_mmv_group & g, const char * X, norm_cols4 & r) {
+    const int lane = threadIdx.x & 63;
+    const int64_t K = g.K;
+    const float * xc = (const float *) X;
+    const float * gp = g.pro.g ? g.pro.g : xc;
+    const float * bp = g.pro.b ? g.pro.b : xc;
+#pragma unroll
+    for (int j = 0; j < norm_cols4::kJ; j++) {
+        const int64_t k = (int64_t) j * 256 + lane * 4;
+        const int64_t kc = k < K ? k : K - 4;  // (unconditional loads at clamped addresses; unused past K)
+        r.v[j] = *(const float4 *) (xc + kc);
+        r.gv[j] = *(const float4 *) (gp + kc);
+        r.bv[j] = *(const float4 *) (bp + kc);
+    }
+}
+
+__device__ void norm_quant_prologue1(const mi_mmv_group & g, norm_cols4 & r, const lds_act & act) {
+    constexpr int kJ = norm_cols4::kJ;
+    const int lane = threadIdx.x & 63;
+    const int64_t K = g.K;
+    const int nsl = (int) (K / 256);
+    float scale;
+    if (g.pro.mode == 2) {
+        const float mean = wave_mean_cpu_order4<true, kJ>(r.v, K);
+        MI_STAMP(g.stamps, 6);
+        scale = 1.0f / sqrtf(add_rn(mean, g.pro.eps));
+    } else {
+        const float mean = wave_mean_cpu_order4<false, kJ>(r.v, K);
+        MI_STAMP(g.stamps, 6);
+#pragma unroll
+        for (int j = 0; j < kJ; j++) {
+            r.v[j].x = sub_rn(r.v[j].x, mean);
+            r.v[j].y = sub_rn(r.v[j].y, mean);
+            r.v[j].z = sub_rn(r.v[j].z, mean);
+            r.v[j].w = sub_rn(r.v[j].w, mean);
+        }
+        const float variance = wave_mean_cpu_order4<true, kJ>(r.v, K);
+        scale = 1.0f / sqrtf(add_rn(variance, g.pro.eps));
+    }
+    MI_STAMP(g.stamps, 5);
+#pragma unroll
+    for (int j = 0; j < kJ; j++) {
+        if (j >= nsl) break;  // wave-uniform
+        float e[4] = {r.v[j].x, r.v[j].y, r.v[j].z, r.v[j].w};
+        const float ge[4] = {r.gv[j].x, r.gv[j].y, r.gv[j].z, r.gv[j].w};
+        const float be[4] = {r.bv[j].x, r.bv[j].y, r.bv[j].z, r.bv[j].w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            float y = mul_rn(e[i], scale);
+            if (g.pro.g) y = mul_rn(y, ge[i]);
+            if (g.pro.b) y = add_rn(y, be[i]);
+            e[i] = y;
+        }
+        quantize_slice<256>(make_float4(e[0], e[1], e[2], e[3]), lane, act, K, 0, j);
+    }
+}
+
 // one output element, through the graph's epilogue: + bias[row], then + resid or GELU (the fp16
 // table lookup of ggml_vec_gelu_f32 with its +-10 clamps), then the K/V-cache row copies -- each
 // step rounded as its own node would round it
@@ -834,6 +902,10 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     //    use of it would otherwise wait for the weight loads too): the norm prologue's first
     //    column, g and b (wave 0), or the activation slices of the first quantization round
     norm_cols nc0;
+    // one Q8_K column: normalized and quantized in wave 0's registers (norm_quant_prologue1)
+    constexpr bool P4 = PRO && NC == 1 && F::QKA == 256;
+    norm_cols4 nc4;
+    const bool p4 = P4 && g.pro.mode && g.pro_q;
     const int nsl = (int) (K / 256);
     const int total = nsl * ncols;
     float4 xfirst[4];
@@ -864,7 +936,10 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
         // its join, before wave 0 requests its weights; every wave loading the column instead --
         // unconditional, ahead of the weights -- queued waves 1-3's weights behind it: Q4_K GPT-2
         // decode 0.417 -> 0.443 ms/token, profiles/r05t_bench_quick.json)
-        if (g.pro.mode && wave == 0) norm_cols_load(g, X, 0, nc0);
+        if (g.pro.mode && wave == 0) {
+            if (p4) norm_cols4_load(g, X, nc4);
+            else norm_cols_load(g, X, 0, nc0);
+        }
         epi_prefetch<NC>(g, row_begin + wave < Nr ? row_begin + wave : Nr - 1, X, epre);
     } else {
         load_round(xfirst, X, g.xcol, p_first);
@@ -888,7 +963,11 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
     //    from the normalized columns when the graph's norm chain is fused in
     const char * Xq = X;
     size_t xcolq = g.xcol;
-    if (PRO && g.pro.mode) {
+    if (PRO && g.pro.mode && p4) {
+        // (the activations complete in LDS once wave 0 is through: the barrier below publishes them)
+        if (wave == 0) norm_quant_prologue1(g, nc4, act);
+        MI_STAMP(g.stamps, 2);
+    } else if (PRO && g.pro.mode) {
         float * xn = (float *) (lds + g.pro_off);
         if (wave == 0) norm_prologue(g, X, ncols, xn, nc0);
         MI_STAMP(g.stamps, 2);  // (norm prologue: slot 2 = wave 0's norm done, instead of the barrier below)
@@ -896,7 +975,7 @@ __global__ __launch_bounds__(256) void k_mmv_stream(mi_mmv_group g) {
         Xq = (const char *) xn;
         xcolq = (size_t) K * sizeof(float);
     }
-    {
+    if (!p4) {
         for (int p0 = p_first; p0 < total; p0 += 16) {
             float4 v[4];
             if (!PRO && p0 == p_first) {
@@ -1318,6 +1397,7 @@ void launch_one(mi_mmv_group g, hipStream_t s) {
             return;
         }
     }
+    g.pro_q = PRO && NC == 1 && F::QKA == 256 && g_mi_tuning.mmv_pro4 ? 1 : 0;
     if (PRO && g.pro.mode) {
         g.pro_off = (int) ord_offset(lds);
         lds = (size_t) g.pro_off + (size_t) NC * g.K * sizeof(float);
