@@ -1940,11 +1940,15 @@ static int try_fuse_attn_proj(mi_backend_ctx * ctx, ggml_cgraph * g, int i, cons
 // 0 turns it off.
 static int g_ord_prefill_cols = getenv("GGML_MI355X_ORD_PREFILL_COLS") ? atoi(getenv("GGML_MI355X_ORD_PREFILL_COLS")) : INT_MAX;
 
+// (tree order: prompts of up to g_tree_prefill_cols columns take the same 8-column GEMV chunks;
+// set_tuning("tree_prefill_cols", n), 0 = off)
+static int g_tree_prefill_cols = getenv("GGML_MI355X_TREE_PREFILL_COLS") ? atoi(getenv("GGML_MI355X_TREE_PREFILL_COLS")) : 0;
+
 static bool ord_prefill_chunked(const ggml_tensor * n) {
-    if (n->op != GGML_OP_MUL_MAT || mi_mmv_order() != 1 || is_split_tensor(n->src[0])) return false;
+    if (n->op != GGML_OP_MUL_MAT || is_split_tensor(n->src[0])) return false;
     const ggml_tensor * a = n->src[0];
     const ggml_tensor * b = n->src[1];
-    if (b->type != GGML_TYPE_F32 || b->ne[1] <= 8 || b->ne[1] > g_ord_prefill_cols) return false;
+    if (b->type != GGML_TYPE_F32 || b->ne[1] <= 8 || b->ne[1] > (mi_mmv_order() == 1 ? g_ord_prefill_cols : g_tree_prefill_cols)) return false;
     if (a->type != GGML_TYPE_Q4_K && a->type != GGML_TYPE_Q5_K && a->type != GGML_TYPE_Q4_0 && a->type != GGML_TYPE_Q8_0) return false;
     if (!mi_mmv_fused_supported(a->type, a->ne[0], 8)) return false;
     if (a->ne[2] != 1 || a->ne[3] != 1 || b->ne[2] != 1 || b->ne[3] != 1) return false;
@@ -2255,6 +2259,7 @@ static void graph_key(const mi_backend_ctx * ctx, const ggml_cgraph * g, std::ve
     // planes entry created or dropped since (a weight buffer freed and another allocated at the same
     // address) must not replay a graph that reads freed planes
     k.push_back(mi_planes_generation());
+    k.push_back((uint64_t) (uint32_t) g_ord_prefill_cols | ((uint64_t) (uint32_t) g_tree_prefill_cols << 32));  // (chunked prompt GEMVs)
     {
         uint64_t tw[(sizeof(mi_tuning) + 7) / 8] = {};
         memcpy(tw, &g_mi_tuning, sizeof(mi_tuning));
@@ -3024,6 +3029,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "ord_prefill_cols") == 0 && value >= 0) {
         g_ord_prefill_cols = value;
+        return true;
+    }
+    if (strcmp(name, "tree_prefill_cols") == 0 && value >= 0) {
+        g_tree_prefill_cols = value;
         return true;
     }
     if (strcmp(name, "xfirst") == 0 && value >= -1 && value <= 1) {
