@@ -3017,8 +3017,8 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.mmq_variant = value;
         return true;
     }
-    if (strcmp(name, "mmq_long") == 0 && (value == 0 || value == 2 || (mi_diag_build() && (value == 1 || value == 3 || value == 4 || (value >= 16 && value <= 24))))) {
-        // 0 auto, 2 k_mmqt; diagnostic builds: 3 k_mmqt with per-half stage synchronization, 4 k_mmqv: 1 k_mmqw for Q4_K, 16-23 k_mmqt stamps / ablations,
+    if (strcmp(name, "mmq_long") == 0 && (value == 0 || value == 2 || (mi_diag_build() && (value == 1 || value == 3 || value == 4 || value == 5 || (value >= 16 && value <= 24))))) {
+        // 0 auto, 2 k_mmqt; diagnostic builds: 5 k_mmqt with the high half staggered, 3 k_mmqt with per-half stage synchronization, 4 k_mmqv: 1 k_mmqw for Q4_K, 16-23 k_mmqt stamps / ablations,
         // 24 k_mmqr per-step stamps
         g_mi_tuning.mmq_long = value;
         return true;

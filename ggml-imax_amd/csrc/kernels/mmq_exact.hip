@@ -1099,7 +1099,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmqp(mi_mmx_group 
 // the workgroup's s_barrier, so waves w and w + 4 -- the two waves of one SIMD, one of each half --
 // are no longer held in lock step: one half's combine (VALU) can run under the other half's MFMAs.
 // The halves have equal stage counts and meet at a full barrier before the final lo + hi.
-template <int TYPE, int ABL = 0, bool HS = false>
+// ST (round 6, diagnostic builds: measured 3-9 % slower than the lock-step form at B = 64..512,
+// profiles/r06s2h_mmqt_stagger_ab.txt): a stagger of the two waves of a SIMD (MI355X_MICROARCH.md, "Two waves per SIMD",
+// item 9): the high half (waves 4-7) defers each stage's combine into the next stage, ahead of that
+// stage's MFMAs -- so while waves 0-3 issue their MFMAs their partner wave runs the previous
+// combine, and the other way round. The deferred combine's LDS operands (the weight header, the U
+// fragments, d_a) are copied to registers before the stage barrier (the next DMAs overwrite that
+// buffer); the accumulators stay live until the combine. Same operations in the same order per
+// element: bit-identical.
+template <int TYPE, int ABL = 0, bool HS = false, bool ST = false>
 __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     MI_MMX_MEMBER(grp);
     using F = XFmt<TYPE>;
@@ -1118,6 +1126,9 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     constexpr int SINK = 2 * SB;              // d_a DMAs of waves 2-7 land here
     __shared__ __attribute__((aligned(16))) char lds[SINK + DB];
     __shared__ uint32_t hbar[2];              // HS: per-half arrival counters
+    constexpr int kDefB = UB + DB + BM * 16;  // ST: the high half's deferred combine operands, per area
+    static_assert(!ST || UB + DB == 2304, "deferred-area offsets");
+    __shared__ __attribute__((aligned(16))) char ldef[ST ? 2 * kDefB : 16];
 
     const int tid = (int) threadIdx.x;
     const int lane = tid & 63;
@@ -1328,6 +1339,44 @@ __global__ __launch_bounds__(512, 1) void k_mmqt(mi_mmx_group grp) {
     stage_dma(0);
     stamp_slot = 1;
     stage_wait();
+    if constexpr (ST) {
+        // the deferred combine's operands of stage u, copied by waves 4-7 into area u & 1 behind their
+        // MFMAs: [U halves 2 KB | d_a 256 B | the 128 rows' headers 2 KB] (the stage buffer itself is
+        // refilled by the next stage's DMAs)
+        auto def_area = [&](int u) { return ldef + (u & 1) * kDefB; };
+        for (int u = 0; u < SK; u++) {
+            auto dma_hook = [&](int kk) {
+                if (kk < 7) {
+                    stage_piece(u + 1, kk);
+                } else {
+#pragma unroll
+                    for (int i = 7; i <= NI; i++) stage_piece(u + 1, i);
+                }
+            };
+            if (kh && u > 0) {  // the previous stage's combine, under waves 0-3's MFMAs
+                const char * d = def_area(u - 1);
+                combine(d + 2304 + (32 * rw + r) * 16, d + xoff0, (const float *) (d + 2048), sb0 + u - 1);
+            }
+            mfma(u & 1, dma_hook);
+            if (kh) {
+                const char * hb = lds + (u & 1) * SB + HB;  // (the high half's stage image)
+                char * d = def_area(u);
+                if (lane < 32) {
+                    *(uint4 *) (d + 2304 + (32 * rw + lane) * 16) = *(const uint4 *) (hb + XB + UB + (32 * rw + lane) * F::BS);
+                    if (lane < 4) *(uint4 *) (d + 2048 + 64 * rw + 16 * lane) = *(const uint4 *) (hb + XB + UB + WB + 64 * rw + 16 * lane);
+                } else {
+                    *(uint4 *) (d + 512 * rw + 16 * (lane - 32)) = *(const uint4 *) (hb + XB + 512 * rw + 16 * (lane - 32));
+                }
+            } else {
+                combine_stage(u & 1, sb0 + u);
+            }
+            stage_wait();
+        }
+        if (kh && SK > 0) {
+            const char * d = def_area(SK - 1);
+            combine(d + 2304 + (32 * rw + r) * 16, d + xoff0, (const float *) (d + 2048), sb0 + SK - 1);
+        }
+    } else
     for (int u = 0; u < SK; u++) {
         stamp(2 + 4 * u);
         stamp_slot = 5 + 4 * u;
@@ -2436,8 +2485,15 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
         for (int i = 0; i < g.n; i++) tt += ((g.m[i].N + 127) / 128) * ((g.m[i].act.ncols + 63) / 64);
         short_t = tt >= g_mi_tuning.mmqt_short;
     }
+    // k_mmqt plain, or (diagnostic builds, mmq_long 5) with the high half staggered (ST; measured
+    // 3-9 % slower, profiles/r06s2h_mmqt_stagger_ab.txt)
+    const bool st = MI_DIAG && g_mi_tuning.mmq_long == 5;
     if (short_t) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
+#if MI_DIAG
+        if (st) hipLaunchKernelGGL((k_mmqt<12, 0, false, true>), gridt, dim3(512), 0, s, g);
+        else
+#endif
         hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
         return;
     }
@@ -2532,14 +2588,19 @@ void mi_mul_mat_mmqx_group(mi_mmx_group & g, hipStream_t s) {
     // combine deferred into the next step too: 36.9 vs 35.4 us, r04t_mmqt_split2_ab.txt -- all
     // removed)
     const int lng = g_mi_tuning.mmq_long;
-    if ((!MI_DIAG || lng == 0 || lng == 2 || lng == 3 || lng == 4) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
+    if ((!MI_DIAG || lng == 0 || lng == 2 || lng == 3 || lng == 4 || lng == 5) && type == 12 && !(var & ((1 << 28) | 64 | 1024))) {
         const dim3 gridt((unsigned) mmx_deal(g, 128, 64));
 #if MI_DIAG  // measured slower (round 6, profiles/r06e_mmqv_prefill.txt): diagnostic builds only
         if (lng == 3) hipLaunchKernelGGL((k_mmqt<12, 0, true>), gridt, dim3(512), 0, s, g);  // per-half stage sync
         else if (lng == 4) hipLaunchKernelGGL((k_mmqv<12>), gridt, dim3(256), 0, s, g);  // one wave per SIMD, pipelined
         else
 #endif
+#if MI_DIAG
+        if (st) hipLaunchKernelGGL((k_mmqt<12, 0, false, true>), gridt, dim3(512), 0, s, g);
+        else
+#endif
         hipLaunchKernelGGL((k_mmqt<12>), gridt, dim3(512), 0, s, g);
+        (void) st;
         return;
     }
 #if MI_DIAG

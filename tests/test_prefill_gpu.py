@@ -177,11 +177,12 @@ def test_prefill_kernels_bit_equal(rt, backend, tname, B):
         assert np.array_equal(outs[v].view(np.uint32), outs[0].view(np.uint32)), (v, rel_err(outs[v], outs[0]))
 
 
-@pytest.mark.parametrize("lng", [2, 3, 4])
+@pytest.mark.parametrize("lng", [2, 3, 4, 5])
 @pytest.mark.parametrize("K,N,B", [(256, 64, 130), (1280, 96, 257), (3072, 200, 200), (11008, 256, 136), (4096, 4096, 512)])
 def test_split_k_prefill_bit_equal(rt, backend, K, N, B, lng):
     """k_mmqt (mmq_long 2, the Q4_K kernel past 128 columns without repacked planes: the two K
-    halves of the canonical order on two waves, met in LDS; diagnostic builds also mmq_long 3, the
+    halves of the canonical order on two waves, met in LDS; diagnostic builds also mmq_long 5, the
+    same with the high half's combine deferred one stage (staggered), mmq_long 3, the
     same with each half's stages synchronized on its own, and 4, k_mmqv: one wave per SIMD over the
     whole K with the combine software-pipelined under the next superblock's MFMAs) forced onto
     ragged shapes: one superblock (empty high half), S = 5 (a one-superblock high half), S = 12,
