@@ -757,29 +757,32 @@ static const char * planes_of(mi_backend_ctx * ctx, const ggml_tensor * a, const
     return mi_planes_get(a->type, a->data, a->nb[1], a->ne[0], a->ne[1], ctx->stream);
 }
 
-// The 16-byte-aligned copy of a Q4_0 weight for the tree-order decode GEMV (mmq_planes.hip
-// k_q40_repack; created before any capture, renewed by the same write paths as the planes): the
+// The 16-byte-aligned copy of a Q4_0 / Q8_0 weight for the tree-order decode GEMV (mmq_planes.hip
+// k_q40_repack / k_q80_repack; created before any capture, renewed by the same write paths as the planes): the
 // same conditions as planes_of -- a graph leaf in this backend's own device buffer
 static const char * q40r_of(mi_backend_ctx * ctx, const ggml_tensor * a) {
-    if (!g_mi_tuning.q40r || a->type != GGML_TYPE_Q4_0 || a->op != GGML_OP_NONE || a->ne[2] != 1 || a->ne[3] != 1 || is_split_tensor(a))
+    const bool on = a->type == GGML_TYPE_Q4_0 ? g_mi_tuning.q40r : a->type == GGML_TYPE_Q8_0 ? g_mi_tuning.q80r : 0;
+    if (!on || a->op != GGML_OP_NONE || a->ne[2] != 1 || a->ne[3] != 1 || is_split_tensor(a))
         return nullptr;
     const ggml_backend_buffer_t buf = a->view_src ? a->view_src->buffer : a->buffer;
     if (!buffer_is_mi355x(buf) || ((mi_buffer_ctx *) buf->context)->device != ctx->device) return nullptr;
     return mi_planes_get(a->type, a->data, a->nb[1], a->ne[0], a->ne[1], ctx->stream);
 }
 
-// A Q4_0 decode group in tree order on the repacked copies (FmtQ0R): every member's weight must
-// have one, else the canonical blocks (FmtQ0Pair) -- both give the same bits
+// A Q4_0 / Q8_0 decode group in tree order on the repacked copies (FmtQ0R / FmtQ8R): every member's
+// weight must have one, else the canonical blocks (FmtQ0Pair / FmtQ0<true>) -- the same bits
 static void q40r_apply(mi_backend_ctx * ctx, mi_mmv_group & g, const ggml_tensor * const * w) {
     // (one column: with two, the aligned copy measured 2-3 % slower, profiles/r06s2_q40r_ab.txt)
-    if (g.type != GGML_TYPE_Q4_0 || g.ncols != 1 || !g_mi_tuning.q40r || mi_mmv_order() != 0 || g_mi_tuning.mmv_variant % 10 == 1) return;
+    const bool q4 = g.type == GGML_TYPE_Q4_0;
+    if ((!q4 && g.type != GGML_TYPE_Q8_0) || g.ncols != 1 || !(q4 ? g_mi_tuning.q40r : g_mi_tuning.q80r) || mi_mmv_order() != 0 ||
+        (q4 && g_mi_tuning.mmv_variant % 10 == 1)) return;
     const void * p[kMiMaxMembers];
     for (int m = 0; m < g.n; m++) {
         p[m] = q40r_of(ctx, w[m]);
         if (!p[m]) return;
     }
     for (int m = 0; m < g.n; m++) g.m[m].W = p[m];
-    g.nb01 = (size_t) (g.K / 32 * 18);
+    g.nb01 = (size_t) (g.K / 32 * (q4 ? 18 : 34));
     g.q0r = 1;
 }
 
@@ -3049,6 +3052,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
     }
     if (strcmp(name, "q40r") == 0 && value >= 0 && value <= 1) {
         g_mi_tuning.q40r = value;
+        return true;
+    }
+    if (strcmp(name, "q80r") == 0 && value >= 0 && value <= 1) {
+        g_mi_tuning.q80r = value;
         return true;
     }
     if (strcmp(name, "mmv_pro4") == 0 && value >= 0 && value <= 1) {

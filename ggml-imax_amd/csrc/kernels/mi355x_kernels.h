@@ -102,7 +102,7 @@ struct mi_mmv_group {
     } pro;
     int pro_off = 0;   // set by the launcher: LDS byte offset of the normalized columns
     uint64_t * stamps = nullptr;  // diagnostic builds: per-workgroup phase stamps (g_mi_stamp_dev)
-    int q0r = 0;       // Q4_0: every member's W is its 16-byte-aligned repacked copy (mi_planes_get type 2), nb01 = K / 32 * 18
+    int q0r = 0;       // Q4_0 / Q8_0: every member's W is its 16-byte-aligned repacked copy (mi_planes_get type 2 / 8), nb01 = K / 32 * 18 / 34
     int pro_q = 0;     // set by the launcher (g_mi_tuning.mmv_pro4): one Q8_K column's norm prologue quantizes from registers
     mi_mmv_member m[kMiMaxMembers];
 };
@@ -144,6 +144,7 @@ struct mi_tuning {
     int f16_bn;       // F16 decode GEMVs, 2..8 columns with the norm prologue (K <= 1024) on k_gemv_f16_bn: 0 off, 1-5 shapes (default 5), +10 one column too
     int f16_bp;       // F16 decode GEMVs, 2..8 plain columns (K <= 3072) on k_gemv_f16_bn's staging form: 0 off, 1 on
     int q40r;         // tree-order Q4_0 decode GEMVs on the 16-byte-aligned repacked copy (mmq_planes.hip k_q40_repack, FmtQ0R): 1 on (default), 0 off
+    int q80r;         // tree-order Q8_0 decode GEMVs on the 16-byte-aligned repacked copy (k_q80_repack, FmtQ8R): 1 on (default), 0 off
     int mmv_pro4;     // decode GEMVs with the norm prologue, one Q8_K column: normalize and quantize in registers (norm_quant_prologue1): 1 (default), 0 through LDS
     int mmqt_short;   // Q4_K prompts of 33..128 columns on k_mmqt (128 x 64 tiles) when a launch has at least this many of its workgroups (default 192; 0: never)
 };
@@ -245,8 +246,9 @@ void mi_mul_mat_mmqx(int type, const void * W, size_t nb01, int64_t K, int64_t N
 // mmq_variant bits of opt-in kernel forms measured slower than the defaults: diagnostic builds only
 constexpr int kMiMmqDiagBits = (1 << 19) | (1 << 26);  // (bit 2^17 doubles as k_mmqx's full-width bit)
 constexpr int64_t kMiPlanesMinCols = 129;  // prompts of more columns take the planes kernel
-// Type 2 (Q4_0, g_mi_tuning.q40r): the tree-order decode GEMV's 16-byte-aligned copy instead
-// (k_q40_repack: per row the quants of every block, then their f16 scales; K / 32 * 18 bytes a row).
+// Types 2 / 8 (Q4_0 / Q8_0, g_mi_tuning.q40r / q80r): the tree-order decode GEMV's 16-byte-aligned
+// copy instead (k_q40_repack / k_q80_repack: per row the quants of every block, then their f16
+// scales; K / 32 * 18 / 34 bytes a row).
 const char * mi_planes_get(int type, const void * W, size_t nb01, int64_t K, int64_t N, hipStream_t s);
 void mi_planes_refresh(const void * lo, size_t bytes, hipStream_t s);
 void mi_planes_drop(const void * lo, size_t bytes);

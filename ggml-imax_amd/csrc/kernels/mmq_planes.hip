@@ -308,6 +308,29 @@ __global__ __launch_bounds__(256) void k_q40_repack(const uint8_t * __restrict__
     *(uint16_t *) (row + (size_t) nblk * 16 + (size_t) b * 2) = h[0];
 }
 
+// Q8_0 (d f16 + 32 quant bytes = 34 B, block_q8_0): the same reordering -- per row the blocks' 32
+// quant bytes (block b at 32 b), then their scales (at K + 2 b) -- read by FmtQ8R.
+__global__ __launch_bounds__(256) void k_q80_repack(const uint8_t * __restrict__ W, size_t nb01, int64_t nblk, uint8_t * __restrict__ out) {
+    const int64_t n = blockIdx.x;
+    const int64_t b = (int64_t) blockIdx.y * 256 + threadIdx.x;
+    if (b >= nblk) return;
+    const uint16_t * src = (const uint16_t *) (W + (size_t) n * nb01 + (size_t) b * 34);  // 2-byte aligned
+    uint16_t h[17];
+#pragma unroll
+    for (int i = 0; i < 17; i++) h[i] = src[i];
+    uint8_t * row = out + (size_t) n * (size_t) nblk * 34;
+#pragma unroll
+    for (int v = 0; v < 2; v++) {
+        uint4 q;
+        q.x = h[1 + 8 * v] | ((uint32_t) h[2 + 8 * v] << 16);
+        q.y = h[3 + 8 * v] | ((uint32_t) h[4 + 8 * v] << 16);
+        q.z = h[5 + 8 * v] | ((uint32_t) h[6 + 8 * v] << 16);
+        q.w = h[7 + 8 * v] | ((uint32_t) h[8 + 8 * v] << 16);
+        *(uint4 *) (row + (size_t) b * 32 + 16 * v) = q;
+    }
+    *(uint16_t *) (row + (size_t) nblk * 32 + (size_t) b * 2) = h[0];
+}
+
 // ---- the cache ------------------------------------------------------------------------------------
 struct PlanesEntry {
     int type;
@@ -326,10 +349,11 @@ std::atomic<uint64_t> g_planes_gen{0};       // bumped whenever an entry is crea
 int planes_enabled() { return g_mi_tuning.planes; }
 
 void launch_repack(const PlanesEntry & e, const void * W, hipStream_t s) {
-    if (e.type == 2) {
+    if (e.type == 2 || e.type == 8) {
         const int64_t nblk = e.K / 32;
         const dim3 grid((unsigned) e.N, (unsigned) ((nblk + 255) / 256));
-        hipLaunchKernelGGL(k_q40_repack, grid, dim3(256), 0, s, (const uint8_t *) W, e.nb01, nblk, (uint8_t *) e.planes);
+        if (e.type == 2) hipLaunchKernelGGL(k_q40_repack, grid, dim3(256), 0, s, (const uint8_t *) W, e.nb01, nblk, (uint8_t *) e.planes);
+        else hipLaunchKernelGGL(k_q80_repack, grid, dim3(256), 0, s, (const uint8_t *) W, e.nb01, nblk, (uint8_t *) e.planes);
         return;
     }
     const int S = (int) (e.K / 256);
@@ -343,11 +367,12 @@ void launch_repack(const PlanesEntry & e, const void * W, hipStream_t s) {
 
 const char * mi_planes_get(int type, const void * W, size_t nb01, int64_t K, int64_t N, hipStream_t s) {
     // (Q4_K: the planes kernel beats the canonical one; Q5_K's 3 planes do not fit its LDS stages.
-    // Q4_0: the 16-byte-aligned decode copy, g_mi_tuning.q40r)
-    if (type == 2 ? !g_mi_tuning.q40r : (!planes_enabled() || type != 12)) return nullptr;
+    // Q4_0 / Q8_0: the 16-byte-aligned decode copies, g_mi_tuning.q40r / q80r)
+    const bool q0 = type == 2 || type == 8;  // the aligned decode copies (Q4_0 / Q8_0)
+    if (type == 2 ? !g_mi_tuning.q40r : type == 8 ? !g_mi_tuning.q80r : (!planes_enabled() || type != 12)) return nullptr;
     if (K % 256 != 0 || N <= 0 || !W) return nullptr;
-    const int64_t row_min = type == 2 ? K / 32 * 18 : K / 256 * (type == 12 ? 144 : 176);
-    if (nb01 % (type == 2 ? 2 : 4) != 0 || (int64_t) nb01 < row_min) return nullptr;
+    const int64_t row_min = q0 ? K / 32 * (type == 2 ? 18 : 34) : K / 256 * (type == 12 ? 144 : 176);
+    if (nb01 % (q0 ? 2 : 4) != 0 || (int64_t) nb01 < row_min) return nullptr;
     std::lock_guard<std::mutex> lk(g_planes_mu);
     auto it = g_planes.find((uintptr_t) W);
     if (it != g_planes.end()) {
@@ -374,7 +399,7 @@ const char * mi_planes_get(int type, const void * W, size_t nb01, int64_t K, int
     e.K = K;
     e.N = N;
     e.span = (size_t) (N - 1) * nb01 + (size_t) row_min;
-    e.bytes = type == 2 ? (size_t) N * (size_t) row_min : (size_t) ((N + 31) / 32) * (K / 256) * (type == 12 ? PFmt<12>::RB : PFmt<13>::RB);
+    e.bytes = q0 ? (size_t) N * (size_t) row_min : (size_t) ((N + 31) / 32) * (K / 256) * (type == 12 ? PFmt<12>::RB : PFmt<13>::RB);
     (void) hipGetDevice(&e.device);
     void * p = nullptr;
     if (hipMalloc(&p, e.bytes) != hipSuccess) {

@@ -644,6 +644,47 @@ struct FmtQ0R {
     __device__ static __forceinline__ float dot_act(const Regs & r, int, const Act & v, float acc) { return pdot(r, v.av0, v.av1, v.ss, v.da, acc); }
 };
 
+// Q8_0 blocks on the 16-byte-aligned repacked copy (tree order only; k_q80_repack): per row [K/32
+// blocks x 32 quant bytes][K/32 x f16 d], item = one block as for FmtQ0<true> (lane l: blocks l,
+// l + 64, ...) with FmtQ0<true>'s arithmetic (block_dot): bit-identical outputs. A lane's block is
+// two aligned dwordx4; its scale comes with its neighbour's in one dword (selected by parity).
+struct FmtQ8R {
+    static constexpr bool KL = true;
+    static constexpr int QKA = 32;
+    static constexpr int ITEM = 32;
+    using Q = FmtQ0<true>;
+    struct Regs {
+        uint4 q0, q1;
+        uint32_t dd;
+        uint32_t odd;  // 16 if the item is odd (its d in the high half of dd)
+    };
+    __device__ static __forceinline__ void load(Regs & r, const uint8_t * row, int item, int64_t K) {
+        const uint32_t o = (uint32_t) item * 32;
+        r.q0 = *(const uint4 *) (row + o);
+        r.q1 = *(const uint4 *) (row + o + 16);
+        r.dd = *(const uint32_t *) (row + (uint32_t) K + 4 * ((uint32_t) item >> 1));
+        r.odd = ((uint32_t) item & 1) * 16;
+    }
+    __device__ static __forceinline__ float bdot(const Regs & r, const int (&av)[8], float da, float acc) {
+        const uint32_t t[8] = {r.q0.x, r.q0.y, r.q0.z, r.q0.w, r.q1.x, r.q1.y, r.q1.z, r.q1.w};
+        return Q::block_dot(t, mi_h2f((uint16_t) ((r.dd >> r.odd) & 0xFFFF)), av, 0, da, acc);
+    }
+    template <int NC>
+    __device__ static __forceinline__ void dot(const Regs & r, int item, const lds_act & a, int64_t K, int ncols, float (&acc)[NC]) {
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (NC > 1 && c >= ncols) break;
+            const int4 * p = (const int4 *) (a.qs + c * K + (int64_t) item * 32);
+            const int4 a0 = p[0], a1 = p[1];
+            const int av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            acc[c] = bdot(r, av, a.d[c * (K / 32) + item], acc[c]);
+        }
+    }
+    using Act = Q::Act;
+    __device__ static __forceinline__ void act_load(Act & v, int item, const lds_act & a, int64_t K) { Q::act_load(v, item, a, K); }
+    __device__ static __forceinline__ float dot_act(const Regs & r, int, const Act & v, float acc) { return bdot(r, v.av, v.da, acc); }
+};
+
 // a format's weight load (FmtQ0R's needs the row length)
 template <class F>
 __device__ __forceinline__ void fmt_load(typename F::Regs & r, const uint8_t * row, int item, int64_t K) {

@@ -1,12 +1,13 @@
-"""Q4_0 decode GEMVs on the 16-byte-aligned repacked weight copy (mmq_planes.hip k_q40_repack,
-mmv_fused_impl.h FmtQ0R; round 6).
+"""Q4_0 / Q8_0 decode GEMVs on the 16-byte-aligned repacked weight copies (mmq_planes.hip
+k_q40_repack / k_q80_repack, mmv_fused_impl.h FmtQ0R / FmtQ8R; round 6).
 
-The canonical block_q4_0 (ggml-common.h: f16 d + 16 quant bytes = 18 B) leaves the quants 2-byte
-aligned. In tree order the backend streams a per-row repacked copy instead -- all the row's quant
+The canonical block_q4_0 / block_q8_0 (ggml-common.h: f16 d + 16 / 32 quant bytes = 18 / 34 B)
+leave the quants 2-byte aligned. In tree order the backend streams a per-row repacked copy instead -- all the row's quant
 bytes, then all its scales -- kept next to the canonical bytes by the planes cache, which every
 backend write path renews. The pair arithmetic is shared with the canonical-layout kernel, so:
-  * repacked vs canonical (q40r 0): bit-identical, and both within the exact-path tolerance of the
-    reference's vec_dot_q4_0_q8_0 (ggml-quants.c:3469-3874) via the oracle;
+  * repacked vs canonical (q40r / q80r 0): bit-identical, and both within the exact-path tolerance
+    of the reference's vec_dot_q4_0_q8_0 / vec_dot_q8_0_q8_0 (ggml-quants.c:3469-3874, :4819) via
+    the oracle;
   * set_tensor / get_tensor keep returning the reference bytes, and partial or asynchronous weight
     writes reach the copy (the next GEMV sees the new rows);
   * the copy is dropped with its buffer.
@@ -44,37 +45,44 @@ def _stats(rt):
     return int(rt.ggml_backend_mi355x_planes_stats(ctypes.byref(b))), int(b.value)
 
 
+KNOB = {"q4_0": b"q40r", "q8_0": b"q80r"}
+
+
+@pytest.mark.parametrize("tname", ["q4_0", "q8_0"])
 @pytest.mark.parametrize("K,N,B", [(256, 64, 1), (768, 2304, 1), (4096, 4096, 1), (4096, 300, 1), (3072, 768, 1), (11008, 130, 1),
                                    (1024, 4097, 1), (4096, 512, 2)])
-def test_q40_repacked_gemv_bit_equal_canonical(rt, backend, K, N, B):
+def test_q40_repacked_gemv_bit_equal_canonical(rt, backend, tname, K, N, B):
     """One column on the aligned copy (several columns keep the canonical blocks: measured faster
-    there), bit-identical to the canonical-layout kernel."""
-    t = orc.Q4_0
+    there for Q4_0), bit-identical to the canonical-layout kernel."""
+    t = orc.TYPES_BY_NAME[tname]
+    knob = KNOB[tname]
     wq = orc.quantize(t, synth.uniform(K + 7 * N, K * N), K)
     x = synth.uniform(K + 9 * B, K * B)
     n0, _ = _stats(rt)
     assert rt.ggml_backend_mi355x_set_tuning(b"mmv_order", 0)
     try:
-        assert rt.ggml_backend_mi355x_set_tuning(b"q40r", 0)
+        assert rt.ggml_backend_mi355x_set_tuning(knob, 0)
         canon = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
-        assert _stats(rt)[0] == n0, "q40r 0 must not create a copy"
-        assert rt.ggml_backend_mi355x_set_tuning(b"q40r", 1)
+        assert _stats(rt)[0] == n0, "knob 0 must not create a copy"
+        assert rt.ggml_backend_mi355x_set_tuning(knob, 1)
         before = _stats(rt)[0]
         rep = G.mul_mat_once(rt, backend, t, wq, K, N, x, B)
         if B > 1:
             assert _stats(rt)[0] == before
     finally:
-        rt.ggml_backend_mi355x_set_tuning(b"q40r", 1)
+        rt.ggml_backend_mi355x_set_tuning(knob, 1)
         rt.ggml_backend_mi355x_set_tuning(b"mmv_order", -1)
     assert _stats(rt)[0] == n0, "the copy of a freed buffer must be dropped with it"
     assert np.array_equal(rep.view(np.uint32), canon.view(np.uint32)), rel_err(rep, canon)
     assert rel_err(rep, orc.mul_mat(t, wq, K, N, x, B)) <= 1e-5
 
 
-def test_q40_repacked_follows_weight_writes(rt, backend):
+@pytest.mark.parametrize("tname", ["q4_0", "q8_0"])
+def test_q40_repacked_follows_weight_writes(rt, backend, tname):
     """set_tensor at an offset (rows 37..120) and an async write (rows 150..169) renew the copy;
     get_tensor returns the canonical bytes; the copy exists while the buffer lives."""
-    t = orc.Q4_0
+    t = orc.TYPES_BY_NAME[tname]
+    knob = KNOB[tname]
     K, N, B = 4096, 192, 1
     rb = orc.row_size(t, K)
     wq = orc.quantize(t, synth.uniform(181, K * N), K)
@@ -120,12 +128,12 @@ def test_q40_repacked_follows_weight_writes(rt, backend):
                 rt.ggml_backend_tensor_get(w, back.ctypes.data, 0, back.nbytes)
                 assert np.array_equal(back, mixed)
                 # the canonical kernel on the same (written) bytes: the same bits
-                assert rt.ggml_backend_mi355x_set_tuning(b"q40r", 0)
+                assert rt.ggml_backend_mi355x_set_tuning(knob, 0)
                 assert rt.ggml_backend_graph_compute(backend, g) == G.GGML_STATUS_SUCCESS
                 y4 = G.tensor_get(rt, y)
                 assert np.array_equal(y3.view(np.uint32), y4.view(np.uint32)), rel_err(y3, y4)
             finally:
-                rt.ggml_backend_mi355x_set_tuning(b"q40r", 1)
+                rt.ggml_backend_mi355x_set_tuning(knob, 1)
                 rt.ggml_backend_buffer_free(buf)
         assert _stats(rt)[0] == n0
     finally:
