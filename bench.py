@@ -167,9 +167,12 @@ def gpt2_bench(lib, backend, n_decode=128, n_batch=8, path=None, label="GPT-2-11
             lg = m.eval(n_past, [nxt], copy=False)
             nxt = int(np.argmax(lg[-1]))
         n_past = len(toks)
+        t_eval = 0.0  # gpt2_eval alone: the reference program's "predict time" (sampling excluded)
         t0 = time.perf_counter()
         for _ in range(n_decode):
+            te = time.perf_counter()
             lg = m.eval(n_past, [nxt], copy=False)
+            t_eval += time.perf_counter() - te
             n_past += 1
             nxt = int(np.argmax(lg[-1]))
         t_dec = time.perf_counter() - t0
@@ -183,6 +186,10 @@ def gpt2_bench(lib, backend, n_decode=128, n_batch=8, path=None, label="GPT-2-11
         t_pred = t_prompt + t_dec
         return {"model": label, "decode_tokens_per_s": round(n_decode / t_dec, 1),
                 "ms_per_decode_token": round(t_dec / n_decode * 1e3, 4),
+                # main-backend.cpp:880 / :936 time gpt2_eval (logits readback included) apart from the
+                # host sampling (:897-901, its own "sample time"); ms_per_decode_token above includes
+                # this harness's host argmax
+                "ms_per_decode_token_predict": round(t_eval / n_decode * 1e3, 4),
                 "prompt_tokens": len(toks), "prompt_tokens_per_s": round(len(toks) / t_prompt, 1),
                 "ms_per_token_reference_definition": round(t_pred / n_past * 1e3, 4),
                 "graph_nodes": st["nodes"], "kernel_launches_per_token": lib.ggml_backend_mi355x_last_launch_count(backend),
@@ -250,11 +257,15 @@ def gpt2_batched_bench(lib, backend, n_parallel=8, n_steps=48):
             lg = m.decode_batch(nxt, [len(prompt) + w] * n_parallel, seqs)
             nxt = [int(v) for v in np.argmax(lg, axis=1)]
         t0 = time.perf_counter()
+        t_dec = 0.0  # gpt2_decode alone: main-batched.cpp's "predict time" (:1171-1180), sampling excluded
         for t in range(n_steps):
             # (logits read in place from the pinned staging, as main-batched.cpp reads llama's
             # logits buffer; copy=True adds a 1.6 MB host memcpy per step)
+            td = time.perf_counter()
             lg = m.decode_batch(nxt, [len(prompt) + 4 + t] * n_parallel, seqs, copy=False)
+            t_dec += time.perf_counter() - td
             nxt = [int(v) for v in np.argmax(lg, axis=1)]
+        predict.append(t_dec)
         return time.perf_counter() - t0
 
     def stats():
@@ -268,13 +279,18 @@ def gpt2_batched_bench(lib, backend, n_parallel=8, n_steps=48):
             lib.gpt2_batch_stats(m.m, a)
         return list(a)
 
+    predict = []
     try:
         run()  # untimed pass: first captures of each topology, allocator and cache warm-up
         s0, b0 = stats(), bstats()
         dt = run()
+        dt_pred = predict[-1]
         s1, b1 = stats(), bstats()
         r = {"workload": f"{n_parallel} sequences sharing an 8-token prompt, {n_steps} batched decode steps (main-batched.cpp)",
              "decode_tokens_per_s": round(n_parallel * n_steps / dt, 1), "ms_per_step": round(dt / n_steps * 1e3, 4),
+             "ms_per_step_predict": round(dt_pred / n_steps * 1e3, 4),
+             "note": "ms_per_step: the whole step incl. this harness's host argmax over the 8 x n_vocab logits; "
+                     "ms_per_step_predict: gpt2_decode alone, main-batched.cpp's predict time (its sampling is timed apart)",
              "kernel_launches_per_step": lib.ggml_backend_mi355x_last_launch_count(backend),
              "parity": "within 1e-3 of the reference CPU, bit-identical with mmv_order=1 (tests/test_gpt2.py batched tests)",
              "graph_compute_calls": {"direct": s1[3] - s0[3], "replays": s1[4] - s0[4], "captures": s1[5] - s0[5]},
