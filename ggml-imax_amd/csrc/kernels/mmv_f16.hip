@@ -544,6 +544,94 @@ __global__ __launch_bounds__(256) void k_gemv_f16_tall(const uint8_t * __restric
     MI_STAMP(e.stamps, 7);
 }
 
+// Tall matrices (lm_head) with 2..8 columns on the matrix cores (round 6): k_gemv_f16_tall's dot8
+// reads every column's 16 activation bytes from LDS for each 16 weight bytes, so at 8 columns the
+// LDS traffic is 8x the weight stream (batched decode's lm_head: 28.7 us for 77 MB). Here each wave
+// holds the normalized f16 columns once, as the B operands of v_mfma_f32_16x16x32_f16 for the whole
+// K (lane l: column l % 16, K slice 8 (l / 16) of each 32-deep step; columns >= nc are zero), and
+// streams 16-row weight tiles as the A operand (lane l: row l % 16, the same K slice): one MFMA per
+// 32-deep step, the accumulator's lane l then holds column l % 16 of rows 4 (l / 16) .. + 3.
+// f16 x f16 products are exact in f32; the accumulation order is the matrix core's (tree order:
+// within 1e-5 of the reference's vec_dot_f16). Staging and the norm prologue as k_gemv_f16_tall.
+// NK: 32-deep K steps (K <= 32 NK, K % 32 == 0).
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+template <int EPI, int JM, int NK>
+__global__ __launch_bounds__(256) void k_gemv_f16_mt(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                     mi_src_cols x, int ncols, float * __restrict__ dst, size_t ycol,
+                                                     mi_f16_epilogue e, mi_norm_prologue pro, int64_t kp) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [8][kp] f16
+    MI_STAMP(e.stamps, 0);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int nc = ncols < 8 ? ncols : 8;
+    const int nk = (int) (K / 32);
+    const int64_t ntiles = (N + 15) / 16, stride = (int64_t) gridDim.x * 4;
+    int64_t tile = (int64_t) blockIdx.x * 4 + wid;
+    auto load_tile = [&](half8 (&a)[NK], int64_t ti) {
+        const int64_t r = ti * 16 + li;
+        const uint8_t * wrow = W + (r < N ? r : N - 1) * nb01 + (size_t) lk * 16;
+#pragma unroll
+        for (int t = 0; t < NK; t++) a[t] = *(const half8 *) (wrow + (size_t) (t < nk ? t : nk - 1) * 64);
+    };
+    constexpr bool GB = JM > 0 && JM <= 4;
+    float4 pv[JM > 0 ? JM : 1], pg[GB ? JM : 1], pb[GB ? JM : 1];
+    if constexpr (JM > 0) norm_load<JM, GB>((const float *) (x.base + (size_t) (wid < nc ? wid : 0) * x.nb1), K, lane, pro, pv, pg, pb);
+    half8 a[NK];
+    load_tile(a, tile < ntiles ? tile : ntiles - 1);  // the first tile's weights in flight under the staging
+    if constexpr (JM > 0) {
+        if (wid < nc) {
+            if (wid + 4 < nc) {
+                float4 nv[JM];
+                const float * xc2 = (const float *) (x.base + (size_t) (wid + 4) * x.nb1);
+#pragma unroll
+                for (int j = 0; j < JM; j++) {
+                    const int64_t k = (int64_t) j * 256 + lane * 4;
+                    nv[j] = *(const float4 *) (xc2 + (k < K ? k : K - 4));  // (zeroed in norm_store)
+                }
+                norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) wid * kp, lane);
+                norm_store<JM, GB>(nv, pg, pb, K, kp, pro, xs + (size_t) (wid + 4) * kp, lane);
+            } else {
+                norm_store<JM, GB>(pv, pg, pb, K, kp, pro, xs + (size_t) wid * kp, lane);
+            }
+        }
+    } else {
+        stage_cols<4>(x, 0, nc, K, kp, xs);
+    }
+    mi_lds_barrier();
+    MI_STAMP(e.stamps, 2);
+    // the columns as B operands for the whole K (zero past nc)
+    half8 b[NK];
+#pragma unroll
+    for (int t = 0; t < NK; t++) {
+        const half8 v = *(const half8 *) (xs + (size_t) (li < nc ? li : 0) * kp + (size_t) (t < nk ? t : 0) * 32 + lk * 8);
+        b[t] = li < nc && t < nk ? v : half8{};
+    }
+    typedef float f32x4v_t __attribute__((ext_vector_type(4)));
+    for (; tile < ntiles; tile += stride) {
+        f32x4v_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t < NK; t++)
+            if (t < nk) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], b[t], acc, 0, 0, 0);
+        if (tile + stride < ntiles) load_tile(a, tile + stride);  // (the registers are free once the MFMAs read them)
+        const float v4[4] = {acc.x, acc.y, acc.z, acc.w};
+        if (li < nc) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int64_t row = tile * 16 + lk * 4 + q;
+                if (row < N) {
+                    float v = v4[q];
+                    if (EPI >= 1) v = v + e.bias[row];
+                    if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
+                    *(float *) ((char *) dst + (size_t) li * ycol + row * sizeof(float)) = v;
+                    if (e.copy[0].ptr && row >= e.copy[0].row0 && row < e.copy[0].row1)
+                        *(float *) (e.copy[0].ptr + (size_t) li * e.copy[0].col_stride + (row - e.copy[0].row0) * sizeof(float)) = v;
+                }
+            }
+        }
+    }
+    MI_STAMP(e.stamps, 7);
+}
+
 // The F16 GEMV of one column whose input is a norm chain over a value still held as partial sums
 // (mi_attn_proj's per-head parts, mi_norm_prologue::parts): workgroup = RW waves x 4 rows (RW =
 // blockDim / 64), each wave the whole K of its rows in one register pass. The workgroup adds the
@@ -870,6 +958,20 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         const int epi = e.gelu_table ? 3 : (e.bias ? 1 : 0);
         const uint8_t * w = (const uint8_t *) W;
         mi_f16_epilogue es = e;
+        if (nc >= 2 && ncols >= 2 && K % 32 == 0 && K <= 768 && g_mi_tuning.f16_mt) {
+            // several columns on the matrix cores (k_gemv_f16_mt): 16-row tiles, grid-stride
+            const dim3 gridm((unsigned) std::min<int64_t>(((N + 15) / 16 + 3) / 4, 512));
+            const size_t ldsm = (size_t) 8 * kp * sizeof(uint16_t);
+            es.stamps = mi_stamp_take("k_gemv_f16_mt", gridm.x);
+#define MI_GEMV_MT(EP, JMV) hipLaunchKernelGGL((k_gemv_f16_mt<EP, JMV, 24>), gridm, dim3(256), ldsm, s, w, nb01, K, N, x, (int) ncols, dst, ycol, es, pro, kp)
+            if (pro.mode) {
+                if (epi == 0) MI_GEMV_MT(0, 4); else if (epi == 1) MI_GEMV_MT(1, 4); else MI_GEMV_MT(3, 4);
+            } else {
+                if (epi == 0) MI_GEMV_MT(0, 0); else if (epi == 1) MI_GEMV_MT(1, 0); else MI_GEMV_MT(3, 0);
+            }
+#undef MI_GEMV_MT
+            return;
+        }
         es.stamps = mi_stamp_take("k_gemv_f16_tall", grid.x);
         es.xfirst = g_mi_tuning.xfirst == 1;  // (off by default: GPT-2 decode 304 -> 316 us per token with it)
 #define MI_GEMV_TALL_N(EP, JMV, NCV) hipLaunchKernelGGL((k_gemv_f16_tall<EP, 8, JMV, NCV>), grid, dim3(256), lds, s, w, nb01, K, N, x, (int) ncols, dst, ycol, es, pro, kp)

@@ -16,7 +16,7 @@ for spec in sys.argv[1:] or ["f16_rgs=0"]:
     for k, v in kv:
         assert lib.ggml_backend_mi355x_set_tuning(k.encode(), int(v)), k
     r = bench.gpt2_batched_bench(lib, be, n_steps=24)
-    print(f"{spec:40s} ms/step {r['ms_per_step']:.4f}  launches {r['kernel_launches_per_step']}  "
+    print(f"{spec:40s} ms/step {r['ms_per_step']:.4f}  predict {r.get('ms_per_step_predict', 0):.4f}  launches {r['kernel_launches_per_step']}  "
           f"no-capture {r.get('no_graph_capture', {}).get('ms_per_step')}", flush=True)
     for k, v in kv:
         lib.ggml_backend_mi355x_set_tuning(k.encode(), 0)
