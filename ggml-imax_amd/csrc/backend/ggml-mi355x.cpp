@@ -3058,6 +3058,10 @@ bool ggml_backend_mi355x_set_tuning(const char * name, int value) {
         g_mi_tuning.q80r = value;
         return true;
     }
+    if (strcmp(name, "f16_m8") == 0 && (value == 0 || (value == 1 && mi_diag_build()))) {  // (1: measured slower, diagnostic builds)
+        g_mi_tuning.f16_m8 = value;
+        return true;
+    }
     if (strcmp(name, "f16_mt") == 0 && value >= 0 && value <= 1) {
         g_mi_tuning.f16_mt = value;
         return true;

@@ -147,6 +147,7 @@ struct mi_tuning {
     int q80r;         // tree-order Q8_0 decode GEMVs on the 16-byte-aligned repacked copy (k_q80_repack, FmtQ8R): 1 on (default), 0 off
     int mmv_pro4;     // decode GEMVs with the norm prologue, one Q8_K column: normalize and quantize in registers (norm_quant_prologue1): 1 (default), 0 through LDS
     int f16_mt;       // tall F16 GEMVs (lm_head) of 2..8 columns, K <= 768, on the matrix cores (k_gemv_f16_mt): 1 on (default), 0 k_gemv_f16_tall
+    int f16_m8;       // plain F16 GEMVs of 2..8 columns (K <= 4096, K % 32 == 0) on the matrix cores (k_gemv_f16_m8): 0 off (default), 1 on (diagnostic builds: measured slower)
     int mmqt_short;   // Q4_K prompts of 33..128 columns on k_mmqt (128 x 64 tiles) when a launch has at least this many of its workgroups (default 192; 0: never)
 };
 extern mi_tuning g_mi_tuning;

@@ -632,6 +632,102 @@ __global__ __launch_bounds__(256) void k_gemv_f16_mt(const uint8_t * __restrict_
     MI_STAMP(e.stamps, 7);
 }
 
+#if MI_DIAG
+// (diagnostic builds only: measured slower than k_gemv_f16 on batched decode, 0.515 -> 0.568 ms/step,
+// profiles/r06s2k_batched_f16_m8_ab.txt -- a 16-row tile per workgroup leaves 48 workgroups for the
+// 768-row projections, fewer than the streams the weight rows need)
+// Plain (no norm prologue) F16 GEMVs of 2..8 columns on the matrix cores (round 6, batched decode's
+// attention / MLP output projections): one workgroup of NW waves per 16-row tile, the K steps
+// (32 deep) dealt to the waves in contiguous runs of at most NKW; each lane loads its A operand (row
+// l % 16, K slice 8 (l / 16) of a step) straight from the weights and its B operand (column l % 16,
+// the same K slice) straight from the f32 columns, rounded to f16 in registers -- no LDS staging of
+// the columns, each workgroup reads only its K runs of them once. The waves' 16 x 16 partial tiles
+// are added in wave order by wave 0, which applies the epilogue (bias, residual, GELU, row copies).
+// Tree order (f32 sums in the matrix core's order): within 1e-5 of the reference's vec_dot_f16.
+template <int EPI, int NKW, int NW>
+__global__ __launch_bounds__(64 * NW) void k_gemv_f16_m8(const uint8_t * __restrict__ W, size_t nb01, int64_t K, int64_t N,
+                                                         mi_src_cols x, int ncols, float * __restrict__ dst, size_t ycol,
+                                                         mi_f16_epilogue e) {
+    __shared__ float red[NW][64][4];
+    MI_STAMP(e.stamps, 0);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int nc = ncols < 8 ? ncols : 8;
+    const int nk = (int) (K / 32);
+    const int spw = (nk + NW - 1) / NW;                 // steps per wave (<= NKW, launcher)
+    const int t0 = wid * spw, t1 = t0 + spw < nk ? t0 + spw : nk;
+    const int64_t r0 = (int64_t) blockIdx.x * 16;
+    const int64_t r = r0 + li;
+    const uint8_t * wrow = W + (r < N ? r : N - 1) * nb01 + (size_t) lk * 16;
+    const char * xc = x.base + (size_t) (li < nc ? li : 0) * x.nb1 + (size_t) lk * 32;
+    half8 a[NKW];
+    float4 xv[NKW][2];
+#pragma unroll
+    for (int i = 0; i < NKW; i++) {
+        const int t = t0 + i < t1 ? t0 + i : (t1 > t0 ? t1 - 1 : 0);  // (clamped: unconditional loads)
+        a[i] = *(const half8 *) (wrow + (size_t) t * 64);
+    }
+    // (the epilogue operands ride behind the weights)
+    float e_bias[4], e_res[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int64_t rq = r0 + lk * 4 + q;
+        const int64_t rc = rq < N ? rq : N - 1;
+        e_bias[q] = EPI >= 1 ? e.bias[rc] : 0.0f;
+        e_res[q] = EPI == 2 ? *(const float *) (e.resid + (size_t) (li < nc ? li : 0) * e.resid_nb1 + rc * sizeof(float)) : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < NKW; i++) {
+        const int t = t0 + i < t1 ? t0 + i : (t1 > t0 ? t1 - 1 : 0);
+        xv[i][0] = *(const float4 *) (xc + (size_t) t * 128);
+        xv[i][1] = *(const float4 *) (xc + (size_t) t * 128 + 16);
+    }
+    typedef float f32x4v_t __attribute__((ext_vector_type(4)));
+    f32x4v_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < NKW; i++) {
+        if (t0 + i < t1) {
+            half8 b;
+            b[0] = (_Float16) xv[i][0].x; b[1] = (_Float16) xv[i][0].y; b[2] = (_Float16) xv[i][0].z; b[3] = (_Float16) xv[i][0].w;
+            b[4] = (_Float16) xv[i][1].x; b[5] = (_Float16) xv[i][1].y; b[6] = (_Float16) xv[i][1].z; b[7] = (_Float16) xv[i][1].w;
+            if (li >= nc) b = half8{};
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b, acc, 0, 0, 0);
+        }
+    }
+    MI_STAMP(e.stamps, 3);
+    red[wid][lane][0] = acc.x;
+    red[wid][lane][1] = acc.y;
+    red[wid][lane][2] = acc.z;
+    red[wid][lane][3] = acc.w;
+    mi_lds_barrier();
+    if (wid != 0) return;
+    float v4[4] = {red[0][lane][0], red[0][lane][1], red[0][lane][2], red[0][lane][3]};
+#pragma unroll
+    for (int w = 1; w < NW; w++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) v4[q] += red[w][lane][q];
+    if (li < nc) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int64_t row = r0 + lk * 4 + q;
+            if (row < N) {
+                float v = v4[q];
+                if (EPI >= 1) v = v + e_bias[q];
+                if (EPI == 2) v = v + e_res[q];
+                if (EPI == 3) v = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : mi_h2f(e.gelu_table[mi_f2h(v)]));
+                *(float *) ((char *) dst + (size_t) li * ycol + row * sizeof(float)) = v;
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    if (e.copy[k].ptr && row >= e.copy[k].row0 && row < e.copy[k].row1)
+                        *(float *) (e.copy[k].ptr + (size_t) li * e.copy[k].col_stride + (row - e.copy[k].row0) * sizeof(float)) = v;
+                }
+            }
+        }
+    }
+    MI_STAMP(e.stamps, 7);
+}
+#endif  // MI_DIAG
+
 // The F16 GEMV of one column whose input is a norm chain over a value still held as partial sums
 // (mi_attn_proj's per-head parts, mi_norm_prologue::parts): workgroup = RW waves x 4 rows (RW =
 // blockDim / 64), each wave the whole K of its rows in one register pass. The workgroup adds the
@@ -1033,6 +1129,23 @@ void mi_mul_mat_f16_fast(const void * W, size_t nb01, int64_t K, int64_t N, cons
         else if (NWv == 8) { MI_GEMV_BN_E(8, 1) } else { MI_GEMV_BN_E(4, 1) }
 #undef MI_GEMV_BN_E
 #undef MI_GEMV_BN
+#if MI_DIAG
+    } else if (!pro.mode && ncols > 1 && K % 32 == 0 && K <= 4096 && !xh && g_mi_tuning.f16_m8 > 0 && (N + 3) / 4 < 4096) {
+        // several plain columns on the matrix cores (k_gemv_f16_m8): per 16-row tile 4 waves (K <= 1024,
+        // at most 8 steps of 32 each) or 8 (at most 16 steps each)
+        const int nk = (int) (K / 32);
+        const dim3 grid((unsigned) ((N + 15) / 16));
+        const int epi = e.gelu_table ? 3 : (e.resid ? 2 : (e.bias ? 1 : 0));
+        const uint8_t * w = (const uint8_t *) W;
+        mi_f16_epilogue es = e;
+        es.stamps = mi_stamp_take("k_gemv_f16_m8", grid.x);
+#define MI_GEMV_M8(EP, NKWV, NWV) hipLaunchKernelGGL((k_gemv_f16_m8<EP, NKWV, NWV>), grid, dim3(64 * NWV), 0, s, w, nb01, K, N, x, (int) ncols, dst, ycol, es)
+#define MI_GEMV_M8_E(NKWV, NWV) switch (epi) { case 0: MI_GEMV_M8(0, NKWV, NWV); break; case 1: MI_GEMV_M8(1, NKWV, NWV); break; \
+                                                   case 2: MI_GEMV_M8(2, NKWV, NWV); break; default: MI_GEMV_M8(3, NKWV, NWV); break; }
+        if (nk <= 32) { MI_GEMV_M8_E(8, 4) } else { MI_GEMV_M8_E(16, 8) }
+#undef MI_GEMV_M8_E
+#undef MI_GEMV_M8
+#endif
     } else if (!pro.mode && ncols > 1 && K <= 3072 && !xh && g_mi_tuning.f16_bp > 0 && (N + 3) / 4 < 4096) {
         // several plain columns: 16 waves, 4 row groups x K split over 4 (k_gemv_f16_bn, JM = 0). Measured
         // slower than k_gemv_f16 on batched decode (profiles/r06r_batched_plain_gemv_ab.txt): opt-in,

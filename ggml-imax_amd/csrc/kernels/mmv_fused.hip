@@ -38,7 +38,7 @@ static int env_int(const char * name, int def) {
 }
 
 // mmv_blocks == 0: size the grid from the kernel's residency (hipOccupancy...) per instance
-mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 0), env_int("GGML_MI355X_MMV_VARIANT", 0), env_int("GGML_MI355X_F16_VARIANT", 0), 0, env_int("GGML_MI355X_MMQ_VARIANT", 0), env_int("GGML_MI355X_ATTN_VARIANT", 0), env_int("GGML_MI355X_ATTN_ABL", 0), env_int("GGML_MI355X_MMV_ORDER", -1), env_int("GGML_MI355X_F16_WAVES", 0), env_int("GGML_MI355X_F16_RGS", 0), env_int("GGML_MI355X_F16_PS_WAVES", 0), env_int("GGML_MI355X_MMQ_LONG", 0), env_int("GGML_MI355X_XFIRST", -1), env_int("GGML_MI355X_F16_NORM_WAVES", 0), env_int("GGML_MI355X_PLANES", 0), env_int("GGML_MI355X_F16_NC", 10), env_int("GGML_MI355X_MMV_DMA", 0), env_int("GGML_MI355X_F16_BN", 5), env_int("GGML_MI355X_F16_BP", 0), env_int("GGML_MI355X_Q40R", 1), env_int("GGML_MI355X_Q80R", 1), env_int("GGML_MI355X_MMV_PRO4", 1), env_int("GGML_MI355X_F16_MT", 1), env_int("GGML_MI355X_MMQT_SHORT", 192)};
+mi_tuning g_mi_tuning = {env_int("GGML_MI355X_MMV_BLOCKS", 0), env_int("GGML_MI355X_MMV_VARIANT", 0), env_int("GGML_MI355X_F16_VARIANT", 0), 0, env_int("GGML_MI355X_MMQ_VARIANT", 0), env_int("GGML_MI355X_ATTN_VARIANT", 0), env_int("GGML_MI355X_ATTN_ABL", 0), env_int("GGML_MI355X_MMV_ORDER", -1), env_int("GGML_MI355X_F16_WAVES", 0), env_int("GGML_MI355X_F16_RGS", 0), env_int("GGML_MI355X_F16_PS_WAVES", 0), env_int("GGML_MI355X_MMQ_LONG", 0), env_int("GGML_MI355X_XFIRST", -1), env_int("GGML_MI355X_F16_NORM_WAVES", 0), env_int("GGML_MI355X_PLANES", 0), env_int("GGML_MI355X_F16_NC", 10), env_int("GGML_MI355X_MMV_DMA", 0), env_int("GGML_MI355X_F16_BN", 5), env_int("GGML_MI355X_F16_BP", 0), env_int("GGML_MI355X_Q40R", 1), env_int("GGML_MI355X_Q80R", 1), env_int("GGML_MI355X_MMV_PRO4", 1), env_int("GGML_MI355X_F16_MT", 1), env_int("GGML_MI355X_F16_M8", 0), env_int("GGML_MI355X_MMQT_SHORT", 192)};
 thread_local int tl_mi_graph_order = 0;
 
 // ---- diagnostic phase stamps (make DIAG=1 builds; MI_STAMP in mi355x_common.h) ----
