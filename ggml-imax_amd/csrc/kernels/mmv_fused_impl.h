@@ -786,6 +786,97 @@ __device__ __forceinline__ void norm_cols4_load(const mi_mmv_group & g, const ch
     }
 }
 
+// Q8_K of J 256-slices held four consecutive floats per lane (slice j: v[j]), all slices' steps
+// interleaved (mi_q8K_superblock's arithmetic per slice: the first element of largest |x| keeps its
+// sign, iscale = -127 / max, q = min(127, RNE via the fma bit trick), d = 1 / iscale; zero slices
+// d = 0), so the slices' wave reductions and divisions overlap instead of running one after the other
+template <int J>
+__device__ __forceinline__ void quantize_slices_q8K(const float (&v)[J][4], int nsl, int lane, const lds_act & a, int64_t K) {
+    uint32_t ab[J];
+    int bi[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        float best = 0.0f;
+        int bidx = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const float ax = fabsf(v[j][i]);
+            if (ax > best) { best = ax; bidx = i; }  // first occurrence within the lane
+        }
+        ab[j] = __float_as_uint(best);
+        bi[j] = bidx;
+    }
+    uint32_t am[J], key[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) am[j] = ab[j];
+    auto mx = [](uint32_t x, uint32_t y) { return x > y ? x : y; };
+    auto mn = [](uint32_t x, uint32_t y) { return x < y ? x : y; };
+#pragma unroll
+    for (int j = 0; j < J; j++) am[j] = mx(am[j], (uint32_t) mi_dpp<MI_DPP_QP_1032>(0, (int) am[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) am[j] = mx(am[j], (uint32_t) mi_dpp<MI_DPP_QP_2301>(0, (int) am[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) am[j] = mx(am[j], (uint32_t) mi_dpp<MI_DPP_ROW_HALF_MIRROR>(0, (int) am[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) am[j] = mx(am[j], (uint32_t) mi_dpp<MI_DPP_ROW_MIRROR>(0, (int) am[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) am[j] = mx(am[j], (uint32_t) mi_dpp<MI_DPP_ROW_BCAST15, 0xA>(0, (int) am[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) am[j] = mx(am[j], (uint32_t) mi_dpp<MI_DPP_ROW_BCAST31, 0xC>(0, (int) am[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        am[j] = (uint32_t) __builtin_amdgcn_readlane((int) am[j], 63);
+        key[j] = ab[j] == am[j] ? (uint32_t) (lane * 4 + bi[j]) : 0xFFFFFFFFu;
+    }
+    constexpr int kId = -1;
+#pragma unroll
+    for (int j = 0; j < J; j++) key[j] = mn(key[j], (uint32_t) mi_dpp<MI_DPP_QP_1032>(kId, (int) key[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) key[j] = mn(key[j], (uint32_t) mi_dpp<MI_DPP_QP_2301>(kId, (int) key[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) key[j] = mn(key[j], (uint32_t) mi_dpp<MI_DPP_ROW_HALF_MIRROR>(kId, (int) key[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) key[j] = mn(key[j], (uint32_t) mi_dpp<MI_DPP_ROW_MIRROR>(kId, (int) key[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) key[j] = mn(key[j], (uint32_t) mi_dpp<MI_DPP_ROW_BCAST15, 0xA>(kId, (int) key[j]));
+#pragma unroll
+    for (int j = 0; j < J; j++) key[j] = mn(key[j], (uint32_t) mi_dpp<MI_DPP_ROW_BCAST31, 0xC>(kId, (int) key[j]));
+    float iscale[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const uint32_t idx = (uint32_t) __builtin_amdgcn_readlane((int) key[j], 63);
+        const int owner = (int) (idx >> 2), sel = (int) (idx & 3);
+        const float mine = sel == 0 ? v[j][0] : sel == 1 ? v[j][1] : sel == 2 ? v[j][2] : v[j][3];
+        const float vmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), owner & 63));
+        iscale[j] = am[j] != 0 ? -127.f / vmax : 0.0f;
+    }
+    int s[J];
+    uint32_t packed[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        packed[j] = 0;
+        s[j] = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const float t = __builtin_fmaf(iscale[j], v[j][i], 12582912.f);
+            int q = (__float_as_int(t) & 0x007fffff) - 0x00400000;
+            q = q < 127 ? q : 127;
+            if (am[j] == 0) q = 0;
+            s[j] += q;
+            packed[j] |= ((uint32_t) (q & 0xFF)) << (8 * i);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < J; j++) s[j] = mi_sum8(s[j]);
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        if (j >= nsl) break;  // wave-uniform
+        *(uint32_t *) (a.qs + j * 256 + lane * 4) = packed[j];
+        if ((lane & 7) == 0) a.s32[j * 8 + (lane >> 3)] = (int16_t) s[j];
+        if (lane == 0) a.d[j] = am[j] != 0 ? 1.0f / iscale[j] : 0.0f;
+    }
+}
+
 __device__ void norm_quant_prologue1(const mi_mmv_group & g, norm_cols4 & r, const lds_act & act) {
     constexpr int kJ = norm_cols4::kJ;
     const int lane = threadIdx.x & 63;
@@ -810,21 +901,21 @@ __device__ void norm_quant_prologue1(const mi_mmv_group & g, norm_cols4 & r, con
         scale = 1.0f / sqrtf(add_rn(variance, g.pro.eps));
     }
     MI_STAMP(g.stamps, 5);
+    float y[kJ][4];
 #pragma unroll
     for (int j = 0; j < kJ; j++) {
-        if (j >= nsl) break;  // wave-uniform
-        float e[4] = {r.v[j].x, r.v[j].y, r.v[j].z, r.v[j].w};
+        const float e[4] = {r.v[j].x, r.v[j].y, r.v[j].z, r.v[j].w};
         const float ge[4] = {r.gv[j].x, r.gv[j].y, r.gv[j].z, r.gv[j].w};
         const float be[4] = {r.bv[j].x, r.bv[j].y, r.bv[j].z, r.bv[j].w};
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            float y = mul_rn(e[i], scale);
-            if (g.pro.g) y = mul_rn(y, ge[i]);
-            if (g.pro.b) y = add_rn(y, be[i]);
-            e[i] = y;
+            float t = mul_rn(e[i], scale);
+            if (g.pro.g) t = mul_rn(t, ge[i]);
+            if (g.pro.b) t = add_rn(t, be[i]);
+            y[j][i] = j < nsl ? t : 0.0f;  // (slices past K: zero, not stored)
         }
-        quantize_slice<256>(make_float4(e[0], e[1], e[2], e[3]), lane, act, K, 0, j);
     }
+    quantize_slices_q8K<kJ>(y, nsl, lane, act, K);
 }
 
 // one output element, through the graph's epilogue: + bias[row], then + resid or GELU (the fp16
